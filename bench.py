@@ -1,0 +1,328 @@
+"""Benchmark of the semantic TSDF hot path on MI355X (BASELINE.json metric:
+"Mvoxel-updates/s + frames/s, 512^3 semantic TSDF @ 640x480").
+
+One step = one frame of the per-frame integrate (src/SfM_CUDA/tsdf.cu:18-70 semantics:
+SDF + gated colour + 32-bin instance histogram) over the whole volume, inputs resident
+in HBM.  N=1 runs configuration C3 (512^3 semantic, synthetic 640x480 stream with masks).
+N>1 ranks (torchrun, one process per GPU) each own an interleaved Z-slab shard of a
+512 x 512 x (512 N) volume, so every GPU integrates 512^3 voxels per frame (weak
+scaling; Z-slab sharding needs no collective for integrate).
+
+value = voxels integrated by all ranks / max-over-ranks wall time of the K timed steps.
+Extra fields: frames/s of the full per-frame pipeline (association raycast + relabel +
+integrate, N=1), render time, the integrate kernel's HBM roofline and the CPU baseline
+(NumPy restatement of tsdf.py:78-120 + SfM gate, bounded sample, 1 core).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "slam-maskrcnn_amd"))
+
+METRIC = "Mvoxel-updates/s + frames/s, 512^3 semantic TSDF @ 640x480"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+KI = (520.9, 521.0, 325.1, 249.7)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def dist_setup(n_gpus):
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != n_gpus:
+        if world == 1 and n_gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    pg = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method="env://")
+        pg = dist
+    return rank, world, local, pg
+
+
+def barrier(pg, local):
+    if pg is not None:
+        import torch
+
+        pg.barrier(device_ids=[local])
+        torch.cuda.synchronize()
+
+
+def max_over_ranks(pg, local, x: float) -> float:
+    if pg is None:
+        return x
+    import torch
+
+    t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
+    pg.all_reduce(t, op=pg.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(pg, local, x: float) -> float:
+    if pg is None:
+        return x
+    import torch
+
+    t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
+    pg.all_reduce(t, op=pg.ReduceOp.SUM)
+    return float(t.item())
+
+
+def cpu_baseline(frames, p, f0, x_planes=64, slabs=3):
+    """NumPy restatement of tsdf.py:78-120 (+ SfM gate/histogram), 1 core, over a bounded
+    sample: `slabs` x `x_planes` x-planes of the 512^3 volume, one frame each."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    try:
+        from threadpoolctl import threadpool_limits
+    except Exception:  # pragma: no cover
+        threadpool_limits = None
+    D = p.dim[0]
+    Dy, Dz = p.dim[1], p.dim[2]
+    assert D == Dy == Dz, "the CPU baseline runs on the cubic N=1 volume"
+    K = np.eye(4, dtype=np.float32)
+    K[(0, 1, 0, 1), (0, 1, 2, 2)] = KI
+    vs = np.array(p.vol_start[:], np.float64)
+    vx = np.array(p.voxel[:], np.float64)
+    mu = float(p.mu)
+    n = x_planes * Dy * Dz
+    sdf = np.full(n, np.float32(mu), np.float32)
+    wt = np.zeros(n, np.int32)
+    col = np.zeros((n, 3), np.uint8)
+    hist = np.zeros((n, 32), np.uint32)
+    total_vox = 0
+    t_total = 0.0
+    ctx = threadpool_limits(limits=1) if threadpool_limits else None
+    try:
+        for s in range(slabs):
+            fr = frames[(s % len(frames))]
+            E = (fr.w2c @ f0.c2w).astype(np.float64)
+            x0 = (D // 2 - x_planes // 2 + (s - slabs // 2) * x_planes) % max(D - x_planes, 1)
+            # shift the origin so the slab [x0, x0+x_planes) is processed in a local buffer
+            vs_s = vs.copy()
+            vs_s[0] = vs[0] + x0 * vx[0]
+            sdf[:] = np.float32(mu)
+            wt[:] = 0
+            t0 = time.perf_counter()
+            O.numpy_integrate(sdf, wt, col, D, vs_s, vx, mu, K, E, fr.depth, fr.rgb, x_range=(0, x_planes),
+                              semantic=True, gate=0.99, mask=fr.mask, hist=hist)
+            t_total += time.perf_counter() - t0
+            total_vox += n
+    finally:
+        if ctx is not None:
+            ctx.__exit__(None, None, None)
+    return {"value": total_vox / t_total / 1e6, "unit": "Mvoxel-updates/s", "cores": 1, "kind": "port",
+            "sample": f"{slabs} x {x_planes} x-planes of the {D}^3 volume ({total_vox} voxel-updates, "
+                      f"{t_total:.1f} s), NumPy restatement of tsdf.py:78-120 + SfM gate/histogram, "
+                      f"1 BLAS thread"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--dim", type=int, default=512)
+    ap.add_argument("--frames", type=int, default=16, help="distinct synthetic frames cycled through")
+    ap.add_argument("--z-chunk", type=int, default=32)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pipeline", action="store_true")
+    ap.add_argument("--cpu-planes", type=int, default=64)
+    ap.add_argument("--cpu-slabs", type=int, default=3)
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
+                    help="per-launch HBM bytes of the integrate kernel from rocprofv3 PMC (see profiles/)")
+    args = ap.parse_args()
+
+    rank, world, local, pg = dist_setup(args.gpus)
+    import semtsdf
+    from semtsdf import _lib as L
+    from semtsdf.synth import SyntheticStream
+    from semtsdf.volume import DeviceBuffer
+
+    semtsdf.load()
+    D = args.dim
+    W, H = 640, 480
+    t_gen = time.perf_counter()
+    stream = SyntheticStream(seed=1, noise=True)
+    f0 = stream.frame(0)
+    frames = [stream.frame(k) for k in range(1, args.frames + 1)]
+    log(f"[bench rank {rank}] generated {len(frames) + 1} frames in {time.perf_counter() - t_gen:.1f}s")
+
+    p = semtsdf.default_params(D, KI, W, H)
+    p.dim[2] = D * world
+    semtsdf.place_from_frame(p, f0.depth, float(np.mean(f0.depth[f0.depth > 0])) / 5000.0, L.PLACE_SFM)
+    p.flags = L.F_SEMANTIC | L.F_GATE_COLOR
+    if world > 1:
+        p.z_nshards = world
+        p.z_shard = rank
+        p.z_chunk = args.z_chunk
+    vol = semtsdf.Volume(p, local)
+    st0 = vol.state()
+    voxels_per_rank = D * D * D  # owned voxels (halo planes are integrated redundantly, not counted)
+    log(f"[bench rank {rank}] volume {list(p.dim)} local {list(st0.local_dim)} "
+        f"device bytes {st0.device_bytes / 2**30:.2f} GiB")
+
+    # frames resident in HBM
+    npx = W * H
+    dbuf = DeviceBuffer(len(frames) * npx * 2)
+    rbuf = DeviceBuffer(len(frames) * npx * 3)
+    mbuf = DeviceBuffer(len(frames) * npx)
+    Es = []
+    for i, fr in enumerate(frames):
+        dbuf.upload(fr.depth, None, i * npx * 2)
+        rbuf.upload(fr.rgb, None, i * npx * 3)
+        mbuf.upload(fr.gt_ids, None, i * npx)  # globally consistent ids: integrate-only step
+        Es.append((fr.w2c @ f0.c2w).astype(np.float32))
+    vol.sync()
+
+    def step(k):
+        i = k % len(frames)
+        vol.integrate_dev(dbuf.ptr + i * npx * 2, rbuf.ptr + i * npx * 3, mbuf.ptr + i * npx, Es[i])
+
+    for k in range(args.warmup):
+        step(k)
+    vol.sync()
+    vol.reset_timing()
+    vol.set_instrumentation(events=True, count=False)
+    barrier(pg, local)
+    vol.sync()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(args.warmup + k)
+    vol.sync()
+    barrier(pg, local)
+    t1 = time.perf_counter()
+    elapsed = max_over_ranks(pg, local, t1 - t0)
+    tm = vol.timing()
+    vol.set_instrumentation(events=False, count=False)
+    kern_ms = tm.integrate_ms / max(tm.n_integrate, 1)
+
+    # algorithmic bytes of the same launches (counts are a function of the frame only)
+    vol.reset_timing()
+    vol.set_instrumentation(events=False, count=True)
+    for k in range(args.steps):
+        step(args.warmup + k)
+    tc = vol.timing()
+    vol.set_instrumentation(events=False, count=False)
+    touched = tc.touched / args.steps
+    gated = tc.gated / args.steps
+    bytes_per_launch = 16.0 * touched + 14.0 * gated + 6.0 * npx
+    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+
+    total_vox = sum_over_ranks(pg, local, float(voxels_per_rank) * args.steps)
+    value = total_vox / elapsed / 1e6
+
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            if tj.get("dim") == D and tj.get("n_gpus", 1) == world:
+                traffic = tj.get("bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    pipeline = None
+    if world == 1 and not args.no_pipeline:
+        # full per-frame pipeline (SfM launch_kernel order): association raycast + relabel on
+        # device, then integrate; per-frame instance labels permuted as Mask R-CNN would emit.
+        vol.reset()
+        mwork = DeviceBuffer(npx)
+        n_pipe = min(args.steps, len(frames))
+        vol.parse_frame_dev(dbuf.ptr, rbuf.ptr, mbuf.ptr, Es[0])  # first integrated frame
+        for i in range(1, 3):
+            mwork.upload(frames[i].mask, vol.stream)
+            vol.parse_frame_dev(dbuf.ptr + i * npx * 2, rbuf.ptr + i * npx * 3, mwork.ptr, Es[i])
+        vol.sync()
+        vol.reset_timing()
+        vol.set_instrumentation(events=True, count=False)
+        tp0 = time.perf_counter()
+        for k in range(n_pipe):
+            i = (3 + k) % len(frames)
+            mwork.upload(frames[i].mask, vol.stream)  # 307 KB per-frame mask (new detections)
+            vol.parse_frame_dev(dbuf.ptr + i * npx * 2, rbuf.ptr + i * npx * 3, mwork.ptr, Es[i])
+        vol.sync()
+        tp1 = time.perf_counter()
+        tp = vol.timing()
+        s2w, c = semtsdf.orbit_camera(list(p.Kinv), 0.3, float(np.mean(f0.depth[f0.depth > 0]) / 5000.0))
+        obuf = DeviceBuffer(npx * 3)
+        vol.reset_timing()
+        for _ in range(5):
+            vol.raycast_dev(s2w, c, L.RENDER_LABEL, obuf.ptr)
+        tr = vol.timing()
+        st = vol.state()
+        pipeline = {
+            "frames_per_s": n_pipe / (tp1 - tp0),
+            "ms_per_frame": (tp1 - tp0) * 1e3 / n_pipe,
+            "assoc_ms_per_frame": tp.assoc_ms / max(tp.n_assoc, 1),
+            "integrate_ms_per_frame": tp.integrate_ms / max(tp.n_integrate, 1),
+            "render_ms_per_view": tr.render_ms / max(tr.n_render, 1),
+            "num_objs": int(st.num_objs),
+        }
+        obuf.free()
+        mwork.free()
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(frames, p, f0, args.cpu_planes, args.cpu_slabs)
+
+    if rank == 0:
+        rec = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "Mvoxel-updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {
+                "workload": "C3: 512^3 semantic TSDF integrate (sdf f32, weight i32, colour u8x3, 32-bin u32 "
+                            "instance histogram), synthetic 640x480 depth+RGB+mask stream (seed 1, noise on), "
+                            "frames resident in HBM; N>1: interleaved Z-slab shards of 512x512x(512N)",
+                "volume": list(p.dim),
+                "z_chunk": int(p.z_chunk) if world > 1 else None,
+                "frames_cycled": len(frames),
+            },
+            "frames_per_s": round(args.steps / elapsed, 2),
+            "integrate_kernel_ms": round(kern_ms, 4),
+            "touched_per_frame": int(touched),
+            "gated_per_frame": int(gated),
+            "touched_mvox_per_s": round(touched / (kern_ms * 1e-3) / 1e6, 1),
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": int(bytes_per_launch),
+            },
+            "cpu_baseline": cpu,
+            "pipeline": pipeline,
+        }
+        print(json.dumps(rec), flush=True)
+    vol.close()
+    if pg is not None:
+        pg.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

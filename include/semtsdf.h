@@ -1,0 +1,212 @@
+/*
+ * semtsdf.h — C ABI of the MI355X-native semantic TSDF engine (libsemtsdf.so).
+ *
+ * This is the drop-in boundary for the fusion hot path of qq456cvb/SLAM-MaskRCNN:
+ *   - the C++ class `TSDF` of src/SfM_CUDA (tsdf.cuh:7-67, tsdf.cu:137-540) and the
+ *     `Viewer` raycast (viewer.cu:17-179), and
+ *   - the pybind11 extension `tsdf_cuda.tsdf_update` of src/TSDF_Python
+ *     (tsdf.cpp:11-33, module tsdf.cpp:35-37).
+ * Every entry point is `extern "C"`, takes plain pointers and sizes, and returns an
+ * `int` status (SEMTSDF_OK == 0).  On failure `semtsdf_last_error()` returns a
+ * thread-local message.  Host pointers are borrowed for the duration of the call; the
+ * library owns all device memory it allocates.  `stream` arguments are `hipStream_t`
+ * passed as `void*` (NULL = the handle's own stream).
+ *
+ * Volume layout (TSDF_Python tsdf.py:48-52, SfM tsdf.cu:55): flat x-major, z fastest,
+ *   idx = x*Dy*Dz + y*Dz + z.  sdf f32, weight i32, colour u8x3 (SfM) or i32x3
+ *   (TSDF_Python), histogram 32 x u32 per voxel.  On the device the histogram is kept
+ *   bin-major ([32][voxels]) so same-label lanes write coalesced; semtsdf_download()
+ *   returns the reference voxel-major [voxels][32] layout.
+ */
+#ifndef SEMTSDF_H
+#define SEMTSDF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SEMTSDF_ABI_VERSION 1
+#define SEMTSDF_MAX_OBJECTS 32 /* tsdf.cuh:4 */
+
+/* ---- status codes ------------------------------------------------------------ */
+#define SEMTSDF_OK 0
+#define SEMTSDF_ERR_INVALID (-1)     /* bad argument, shape or parameter */
+#define SEMTSDF_ERR_HIP (-2)         /* a HIP runtime call failed (message has the HIP error) */
+#define SEMTSDF_ERR_OOM (-3)         /* device allocation failed */
+#define SEMTSDF_ERR_LABEL (-4)       /* a mask label >= SEMTSDF_MAX_OBJECTS (tsdf.cu:61 UB in the reference) */
+#define SEMTSDF_ERR_STATE (-5)       /* call out of order (e.g. raycast on a sharded handle) */
+#define SEMTSDF_ERR_COMM (-6)        /* collective failure */
+#define SEMTSDF_ERR_UNSUPPORTED (-7) /* feature not available for this handle/mode */
+
+/* ---- volume flags -------------------------------------------------------------- */
+#define SEMTSDF_F_SEMANTIC 0x1u   /* 32-bin per-voxel instance histogram (SfM tsdf.cu:61) */
+#define SEMTSDF_F_GATE_COLOR 0x2u /* colour+histogram only when f < gate (SfM tsdf.cu:57) */
+#define SEMTSDF_F_COLOR_I32 0x4u  /* colour int32x3 (TSDF_Python tsdf.py:50) instead of u8x3 */
+#define SEMTSDF_F_VOTE 0x8u       /* label vote tsdf_cls/tsdf_cls_cnt (TSDF_Python/tsdf.cu:48-57) */
+#define SEMTSDF_F_NO_CULL 0x10u   /* disable brick frustum/depth culling (debug; same results) */
+
+/* ---- placement modes (a1) ---------------------------------------------- */
+#define SEMTSDF_PLACE_SFM 0    /* SfM tsdf.cu:173-199: f32, depth->u8 saturates, mean in metres */
+#define SEMTSDF_PLACE_PYTHON 1 /* TSDF_Python tsdf.py:32-47: f64, depth->u8 wraps mod 256 */
+
+/* ---- raycast render modes (a8) ------------------------------------------------------ */
+#define SEMTSDF_RENDER_LABEL 0 /* argmax instance -> palette BGR (viewer.cu:71-79) */
+#define SEMTSDF_RENDER_COLOR 1 /* trilinear colour at the hit (tsdf_render.frag:125-131) */
+
+typedef struct semtsdf_params {
+    int32_t dim[3];          /* global volume dims (Dx, Dy, Dz); reference: 256^3 (tsdf.cuh:52) */
+    float vol_start[3];      /* world position of voxel (0,0,0) (tsdf.cu:195) */
+    float vol_end[3];        /* world position of voxel (D-1) (tsdf.cu:196) */
+    float voxel[3];          /* (vol_end - vol_start)/(D-1) (tsdf.cu:197) */
+    float mu;                /* truncation, 5*voxel.x (tsdf.cu:199) */
+    float K[16];             /* row-major 4x4 intrinsic (tsdf.cu:143-146) */
+    float Kinv[16];          /* its inverse (tsdf.cu:147) */
+    int32_t width, height;   /* frame size (640x480) */
+    float depth_scale;       /* raw depth units per metre: 5000 (tsdf.cu:49) */
+    float gate;              /* colour/histogram gate on f: 0.99 (tsdf.cu:57) */
+    float box_thresh;        /* association box-mask threshold: 0.3 (tsdf.cu:128) */
+    float prior_mrcnn_err_rate; /* Configuration::prior_mrcnn_err_rate = 0.05 (configuration.h:8) */
+    float duplicate_thresh;  /* Configuration::duplicate_thresh = 0.5 (configuration.h:9; unused upstream) */
+    uint32_t flags;          /* SEMTSDF_F_* */
+    /* Z-slab sharding.  The global z axis is cut into chunks of z_chunk
+     * planes; chunk c is owned by shard c % z_nshards.  z_nshards == 1 -> whole volume
+     * (z_chunk is then ignored).  Sharded handles store one extra halo plane per chunk. */
+    int32_t z_shard, z_nshards, z_chunk;
+} semtsdf_params;
+
+typedef struct semtsdf_vol semtsdf_vol; /* opaque volume handle */
+
+typedef struct semtsdf_state {
+    uint32_t n_obs;          /* integrated frames used by association (tsdf.cuh:46) */
+    int32_t num_objs;        /* next global instance id (tsdf.cuh:61) */
+    int32_t local_dim[3];    /* stored dims on this device (z includes halo planes) */
+    uint64_t local_voxels;   /* local_dim product */
+    uint64_t device_bytes;   /* bytes of device memory owned by the handle */
+} semtsdf_state;
+
+/* Per-frame association result (filter_overlaps tsdf.cu:304-416). */
+typedef struct semtsdf_assoc_stats {
+    int32_t max_obj_now;                /* max(mask)+1 of the incoming mask */
+    int32_t num_objs;                   /* after relabel */
+    int32_t assigned_prev[SEMTSDF_MAX_OBJECTS]; /* current label i -> previous id, or -1 */
+    float assigned_prob[SEMTSDF_MAX_OBJECTS];   /* exp(A/C) of the accepted match */
+    uint8_t lut[256];                   /* old label -> new label applied to the mask */
+} semtsdf_assoc_stats;
+
+/* Accumulated kernel timings (HIP events on the launch stream). */
+typedef struct semtsdf_timing {
+    double integrate_ms;  /* sum over integrate kernel launches */
+    double assoc_ms;      /* sum over association (march+accumulate+decide+relabel) */
+    double render_ms;     /* sum over raycast render launches */
+    uint64_t n_integrate, n_assoc, n_render;
+    uint64_t touched;     /* voxels updated (count mode only) */
+    uint64_t gated;       /* voxels whose colour/histogram were updated (count mode only) */
+} semtsdf_timing;
+
+/* ---- library ------------------------------------------------------------------------ */
+const char* semtsdf_last_error(void);
+int semtsdf_abi_version(void);
+int semtsdf_device_count(int* out);
+int semtsdf_set_device(int device);
+int semtsdf_stream_create(void** out_stream);
+int semtsdf_stream_destroy(void* stream);
+int semtsdf_stream_sync(void* stream);
+int semtsdf_dev_malloc(void** out, size_t bytes);
+int semtsdf_dev_free(void* ptr);
+/* kind: 1 = host->device, 2 = device->host, 3 = device->device (async on stream) */
+int semtsdf_memcpy(void* dst, const void* src, size_t bytes, int kind, void* stream);
+
+/* ---- parameters / placement (a1) --------------------------------------------------- */
+/* Fill defaults: K from (fx, fy, cx, cy) as tsdf.cu:137-147, constants of §a10, cubic dim. */
+int semtsdf_params_default(semtsdf_params* p, int dim, const float intrinsics[4], int width, int height);
+/* Place the volume from the first frame's depth (tsdf.cu:173-199 / tsdf.py:32-47).
+ * mean_depth is in metres for SEMTSDF_PLACE_SFM and in raw depth units for
+ * SEMTSDF_PLACE_PYTHON (tsdf.py:38-40). Writes vol_start, vol_end, voxel, mu. */
+int semtsdf_place_from_frame(semtsdf_params* p, const uint16_t* depth, double mean_depth, int mode);
+
+/* ---- volume lifecycle ------------------------------------------------------------- */
+int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out);
+int semtsdf_destroy(semtsdf_vol* v);
+int semtsdf_get_params(const semtsdf_vol* v, semtsdf_params* out);
+int semtsdf_get_state(const semtsdf_vol* v, semtsdf_state* out);
+int semtsdf_set_state(semtsdf_vol* v, uint32_t n_obs, int32_t num_objs);
+void* semtsdf_get_stream(const semtsdf_vol* v);
+/* sdf := mu (metres, tsdf.cu:243-244), weight/colour/histogram := 0, n_obs = num_objs = 0. */
+int semtsdf_reset(semtsdf_vol* v, void* stream);
+
+/* ---- integrate (a4) ------------------------------------------------------------------
+ * One frame into the volume: E = extrinsic * init_extrinsic_inv (row-major 4x4 f32,
+ * tsdf.cu:217).  depth u16 [H*W], rgb u8 [H*W*3], mask u8 [H*W] (labels < 32; may be
+ * NULL unless SEMANTIC).  Does NOT change n_obs (the driver semtsdf_parse_frame does). */
+int semtsdf_integrate(semtsdf_vol* v, const uint16_t* depth, const uint8_t* rgb,
+                      const uint8_t* mask, const float E[16], void* stream);
+/* Same with device pointers (inputs already resident in HBM). */
+int semtsdf_integrate_dev(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d,
+                          const uint8_t* mask_d, const float E[16], void* stream);
+/* Label-vote mode input (TSDF_Python/tsdf.cu:48-57): cls is int32 [H*W]. */
+int semtsdf_integrate_vote_dev(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d,
+                               const int32_t* cls_d, const float E[16], void* stream);
+
+/* ---- association (a5 + a6) -----------------------------------------------------------
+ * Raycast the volume from the current camera (back_proj_kernel tsdf.cu:72-135), fuse the
+ * 32x32 log-likelihood accumulation on device, decide assignments (tsdf.cu:337-389) and
+ * relabel the mask in place.  Requires n_obs > 0 (tsdf.cu:426).  Host-pointer variant
+ * copies the mask in and the relabelled mask back out; stats may be NULL. */
+int semtsdf_associate(semtsdf_vol* v, uint8_t* mask_inout, const float E[16],
+                      semtsdf_assoc_stats* stats, void* stream);
+int semtsdf_associate_dev(semtsdf_vol* v, uint8_t* mask_d, const float E[16],
+                          semtsdf_assoc_stats* stats_host_or_null, void* stream);
+/* Debug/parity: per-pixel probs [H*W*32] f32 and box_mask [H*W*32] u8 exactly as the
+ * reference back_proj_kernel leaves them (zeros where no hit).  Host outputs. */
+int semtsdf_assoc_probs(semtsdf_vol* v, const float E[16], float* probs, uint8_t* box_mask, void* stream);
+
+/* ---- per-frame driver (a7: TSDF::parse_frame/launch_kernel tsdf.cu:171-228,418-504) ----
+ * Integrated-frame count n_obs: if n_obs > 0 associate (relabels mask), else
+ * num_objs = max(mask)+1; then integrate; n_obs++.  Placement is the caller's job
+ * (semtsdf_place_from_frame + semtsdf_create). */
+int semtsdf_parse_frame(semtsdf_vol* v, const uint16_t* depth, const uint8_t* rgb,
+                        uint8_t* mask_inout, const float E[16], semtsdf_assoc_stats* stats, void* stream);
+int semtsdf_parse_frame_dev(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d,
+                            uint8_t* mask_d, const float E[16], void* stream);
+
+/* ---- raycast render (a8: Viewer::show_tsdf viewer.cu:137-179) -------------------------
+ * Orbit camera helper: s2w = rot(angle, dist) * Kinv, c = ((dist+0.5) sin, 0, (dist+0.5)(1-cos)). */
+int semtsdf_orbit_camera(const float Kinv[16], float angle, float dist, float s2w[16], float c[3]);
+/* out_bgr u8 [H*W*3] (host) black where nothing is hit; out_t f32 [H*W] (host, optional)
+ * refined hit distance or -1. */
+int semtsdf_raycast(semtsdf_vol* v, const float s2w[16], const float c[3], int mode,
+                    uint8_t* out_bgr, float* out_t, void* stream);
+int semtsdf_raycast_dev(semtsdf_vol* v, const float s2w[16], const float c[3], int mode,
+                        uint8_t* out_bgr_d, float* out_t_d, void* stream);
+
+/* ---- state transfer (parity, checkpoint/resume) ------------------------------------------
+ * Reference layouts, local storage (for an unsharded handle: the whole volume).  Any
+ * pointer may be NULL.  color is u8 [N*3] or i32 [N*3] per SEMTSDF_F_COLOR_I32; hist is
+ * voxel-major u32 [N*32] (tsdf.cu:249); cls/cls_cnt i32 [N] (vote mode). */
+int semtsdf_download(semtsdf_vol* v, float* sdf, int32_t* wt, void* color, uint32_t* hist,
+                     int32_t* cls, int32_t* cls_cnt);
+int semtsdf_upload(semtsdf_vol* v, const float* sdf, const int32_t* wt, const void* color,
+                   const uint32_t* hist, const int32_t* cls, const int32_t* cls_cnt);
+
+/* ---- measurement ------------------------------------------------------------------------ */
+/* enable bit0: record HIP events around kernels; bit1: count touched/gated voxels. */
+int semtsdf_set_instrumentation(semtsdf_vol* v, int enable);
+int semtsdf_get_timing(semtsdf_vol* v, semtsdf_timing* out); /* synchronises the stream */
+int semtsdf_reset_timing(semtsdf_vol* v);
+
+/* ---- drop-in for tsdf_cuda.tsdf_update (TSDF_Python/tsdf.cpp:11-33, exact argument order) --
+ * Host arrays updated in place: tsdf_diff f32[D^3], tsdf_color i32[D^3*3], tsdf_wt i32[D^3],
+ * tsdf_cls i32[D^3], tsdf_cls_cnt i32[D^3]; vol_start f32[3]; intrinsic f32[16];
+ * depth u16[H*W]; color u8[H*W*3]; cls i32[H*W]; extrinsic2init f32[16]. */
+int semtsdf_tsdf_update(float* tsdf_diff, int32_t* tsdf_color, int32_t* tsdf_wt, int32_t* tsdf_cls,
+                        int32_t* tsdf_cls_cnt, int vol_dim, const float* vol_start, float voxel,
+                        float miu, const float* intrinsic, const uint16_t* depth, const uint8_t* color,
+                        const int32_t* cls, const float* extrinsic2init, int width, int height);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SEMTSDF_H */

@@ -1,0 +1,989 @@
+// C-ABI host layer of libsemtsdf.so (include/semtsdf.h).
+//
+// Replaces the host side of the reference fusion engine:
+//   TSDF::TSDF / parse_frame / init_cuda_vars / launch_kernel  src/SfM_CUDA/tsdf.cu:137-280,418-504
+//   Viewer::show_tsdf                                          src/SfM_CUDA/viewer.cu:137-179
+//   tsdf_cuda.tsdf_update (pybind11)                           src/TSDF_Python/tsdf.cpp:11-33, tsdf.cu:61-125
+// Differences by design: every HIP call is checked and reported through an int status and
+// a thread-local message (the reference checks only cudaGetLastError and throws
+// std::string); all device work is stream-ordered and asynchronous; association runs on
+// the device (no 49 MB probs/box_mask D2H, tsdf.cu:457-458); 64-bit voxel indexing.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/semtsdf.h"
+#include "semtsdf_internal.h"
+
+using namespace semtsdf;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIPC(expr)                                                                                  \
+    do {                                                                                            \
+        hipError_t e_ = (expr);                                                                     \
+        if (e_ != hipSuccess)                                                                       \
+            return fail(e_ == hipErrorOutOfMemory ? SEMTSDF_ERR_OOM : SEMTSDF_ERR_HIP, "%s: %s (%s:%d)", \
+                        #expr, hipGetErrorString(e_), __FILE__, __LINE__);                          \
+    } while (0)
+
+// Palette of viewer.cu:93-126 (RGB triplets; written as BGR, viewer.cu:272).
+const uint8_t kPalette[kMaxObjects * 3] = {
+    230, 25,  75,  60,  180, 75,  255, 225, 25,  0,   130, 200, 245, 130, 48,  145, 30,  180,
+    70,  240, 240, 240, 50,  230, 210, 245, 60,  250, 190, 190, 0,   128, 128, 230, 190, 255,
+    170, 110, 40,  255, 250, 200, 128, 0,   0,   170, 255, 195, 230, 25,  75,  60,  180, 75,
+    255, 225, 25,  0,   130, 200, 245, 130, 48,  145, 30,  180, 70,  240, 240, 240, 50,  230,
+    210, 245, 60,  250, 190, 190, 0,   128, 128, 230, 190, 255, 170, 110, 40,  255, 250, 200,
+    128, 0,   0,   170, 255, 195};
+
+struct EventPair {
+    hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct semtsdf_vol {
+    semtsdf_params p{};
+    VolGeom g{};
+    VolBufs b{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    size_t device_bytes = 0;
+    // per-frame staging (host-pointer API)
+    uint16_t* depth_d = nullptr;
+    uint8_t* rgb_d = nullptr;
+    uint8_t* mask_d = nullptr;
+    int32_t* cls_d = nullptr;
+    DepthPyramid pyr{};
+    // association state
+    AssocTables* tables_d = nullptr;
+    AssocDecision* decision_d = nullptr;
+    int* num_objs_d = nullptr;
+    float* probs_d = nullptr;     // debug only (allocated lazily)
+    uint8_t* box_d = nullptr;
+    uint8_t* palette_d = nullptr;
+    uint8_t* render_d = nullptr;
+    float* render_t_d = nullptr;
+    unsigned long long* counters_d = nullptr;
+    AssocDecision* decision_h = nullptr;  // pinned
+    uint32_t n_obs = 0;
+    // instrumentation
+    int instr = 0;
+    std::vector<EventPair> ev_integrate, ev_assoc, ev_render;
+    double t_integrate = 0, t_assoc = 0, t_render = 0;
+    uint64_t n_integrate = 0, n_assoc = 0, n_render = 0;
+};
+
+namespace {
+
+size_t npx(const semtsdf_vol* v) { return (size_t)v->p.width * (size_t)v->p.height; }
+
+hipStream_t pick(const semtsdf_vol* v, void* s) { return s ? (hipStream_t)s : v->stream; }
+
+int dev_alloc(semtsdf_vol* v, void** p, size_t bytes) {
+    if (bytes == 0) { *p = nullptr; return SEMTSDF_OK; }
+    hipError_t e = hipMalloc(p, bytes);
+    if (e != hipSuccess)
+        return fail(e == hipErrorOutOfMemory ? SEMTSDF_ERR_OOM : SEMTSDF_ERR_HIP, "hipMalloc(%zu): %s", bytes,
+                    hipGetErrorString(e));
+    v->device_bytes += bytes;
+    return SEMTSDF_OK;
+}
+
+void free_all(semtsdf_vol* v) {
+    void* ptrs[] = {v->b.sdf, v->b.wt, v->b.color, v->b.hist, v->b.cls, v->b.cls_cnt, v->depth_d, v->rgb_d,
+                    v->mask_d, v->cls_d, v->pyr.l0, v->pyr.l1, v->pyr.l2, v->tables_d, v->decision_d,
+                    v->num_objs_d, v->probs_d, v->box_d, v->palette_d, v->render_d, v->render_t_d,
+                    v->counters_d};
+    for (void* q : ptrs)
+        if (q) (void)hipFree(q);
+    if (v->decision_h) (void)hipHostFree(v->decision_h);
+    for (auto* vec : {&v->ev_integrate, &v->ev_assoc, &v->ev_render})
+        for (auto& e : *vec) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
+    if (v->stream) (void)hipStreamDestroy(v->stream);
+}
+
+int check_params(const semtsdf_params* p) {
+    if (!p) return fail(SEMTSDF_ERR_INVALID, "params is NULL");
+    for (int i = 0; i < 3; ++i) {
+        if (p->dim[i] < 2 || p->dim[i] > 65535)
+            return fail(SEMTSDF_ERR_INVALID, "dim[%d]=%d out of range [2, 65535]", i, p->dim[i]);
+        if (!(p->voxel[i] > 0.0f) || !std::isfinite(p->voxel[i]))
+            return fail(SEMTSDF_ERR_INVALID, "voxel[%d]=%g must be > 0 (place the volume first)", i, p->voxel[i]);
+    }
+    if (!(p->mu > 0.0f)) return fail(SEMTSDF_ERR_INVALID, "mu=%g must be > 0", p->mu);
+    if (p->width <= 0 || p->height <= 0 || (int64_t)p->width * p->height > (1 << 28))
+        return fail(SEMTSDF_ERR_INVALID, "bad frame size %dx%d", p->width, p->height);
+    if (!(p->depth_scale > 0.0f)) return fail(SEMTSDF_ERR_INVALID, "depth_scale must be > 0");
+    if ((p->flags & SEMTSDF_F_VOTE) && (p->flags & SEMTSDF_F_SEMANTIC))
+        return fail(SEMTSDF_ERR_INVALID, "SEMANTIC and VOTE are exclusive");
+    if (p->z_nshards < 1 || p->z_shard < 0 || p->z_shard >= p->z_nshards)
+        return fail(SEMTSDF_ERR_INVALID, "bad shard %d of %d", p->z_shard, p->z_nshards);
+    if (p->z_nshards > 1 && (p->z_chunk < 1 || p->z_chunk > p->dim[2]))
+        return fail(SEMTSDF_ERR_INVALID, "bad z_chunk %d", p->z_chunk);
+    return SEMTSDF_OK;
+}
+
+// local z planes owned by a shard
+int local_planes(const semtsdf_params* p, int* chunk, int* halo) {
+    if (p->z_nshards == 1) { *chunk = p->dim[2]; *halo = 0; return p->dim[2]; }
+    *chunk = p->z_chunk;
+    *halo = 1;
+    const int nchunks = (p->dim[2] + p->z_chunk - 1) / p->z_chunk;
+    int mine = 0;
+    for (int c = p->z_shard; c < nchunks; c += p->z_nshards) ++mine;
+    return mine * (p->z_chunk + 1);
+}
+
+void fill_E(float dst[12], const float E[16]) {
+    for (int i = 0; i < 12; ++i) dst[i] = E[i];
+}
+
+void timing_begin(semtsdf_vol* v, std::vector<EventPair>& vec, hipStream_t s, EventPair* ep) {
+    ep->a = ep->b = nullptr;
+    if (!(v->instr & 1)) return;
+    if (hipEventCreate(&ep->a) != hipSuccess || hipEventCreate(&ep->b) != hipSuccess) return;
+    (void)hipEventRecord(ep->a, s);
+    (void)vec;
+}
+
+void timing_end(semtsdf_vol* v, std::vector<EventPair>& vec, hipStream_t s, EventPair* ep) {
+    if (!(v->instr & 1) || !ep->a) return;
+    (void)hipEventRecord(ep->b, s);
+    vec.push_back(*ep);
+}
+
+int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d, const uint8_t* mask_d,
+                   const int32_t* cls_d, const float E[16], hipStream_t s) {
+    if (!E) return fail(SEMTSDF_ERR_INVALID, "E is NULL");
+    if (!depth_d || !rgb_d) return fail(SEMTSDF_ERR_INVALID, "depth/rgb is NULL");
+    if ((v->p.flags & SEMTSDF_F_SEMANTIC) && !mask_d) return fail(SEMTSDF_ERR_INVALID, "semantic volume needs a mask");
+    if ((v->p.flags & SEMTSDF_F_VOTE) && !cls_d) return fail(SEMTSDF_ERR_INVALID, "vote volume needs cls");
+    IntegrateArgs a{};
+    a.g = v->g;
+    a.b = v->b;
+    fill_E(a.E, E);
+    const float* K = v->p.K;
+    a.K[0] = K[0]; a.K[1] = K[1]; a.K[2] = K[2];
+    a.K[3] = K[4]; a.K[4] = K[5]; a.K[5] = K[6];
+    a.K[6] = K[8]; a.K[7] = K[9]; a.K[8] = K[10];
+    a.width = v->p.width;
+    a.height = v->p.height;
+    a.depth_scale = v->p.depth_scale;
+    a.gate = v->p.gate;
+    a.flags = v->p.flags | ((v->instr & 2) ? 0x80000000u : 0u);
+    a.cull = (v->p.flags & SEMTSDF_F_NO_CULL) ? 0 : 1;
+    a.depth = depth_d;
+    a.rgb = rgb_d;
+    a.mask = mask_d;
+    a.cls = cls_d;
+    a.pyr = v->pyr;
+    a.counters = v->counters_d;
+    if (a.cull) HIPC(launch_depth_pyramid(depth_d, v->p.width, v->p.height, v->pyr, s));
+    EventPair ep;  // events bracket the integrate kernel alone (the roofline kernel)
+    timing_begin(v, v->ev_integrate, s, &ep);
+    HIPC(launch_integrate(a, s));
+    timing_end(v, v->ev_integrate, s, &ep);
+    v->n_integrate++;
+    return SEMTSDF_OK;
+}
+
+MarchCamera assoc_camera(const semtsdf_vol* v, const float E[16]) {
+    MarchCamera c{};
+    const float* Ki = v->p.Kinv;
+    c.Kinv[0] = Ki[0]; c.Kinv[1] = Ki[1]; c.Kinv[2] = Ki[2];
+    c.Kinv[3] = Ki[4]; c.Kinv[4] = Ki[5]; c.Kinv[5] = Ki[6];
+    c.Kinv[6] = Ki[8]; c.Kinv[7] = Ki[9]; c.Kinv[8] = Ki[10];
+    // Rt = E(0:3,0:3)^T, o = -Rt * t (tsdf.cu:432-435); the product is accumulated in
+    // double and rounded once, like cv::gemm on CV_32F.
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) c.Rt[i * 3 + j] = E[j * 4 + i];
+    for (int i = 0; i < 3; ++i) {
+        const double acc = (double)c.Rt[i * 3 + 0] * (double)E[3] + (double)c.Rt[i * 3 + 1] * (double)E[7] +
+                           (double)c.Rt[i * 3 + 2] * (double)E[11];
+        c.o[i] = -(float)acc;
+    }
+    c.use_s2w = 0;
+    return c;
+}
+
+int associate_impl(semtsdf_vol* v, uint8_t* mask_d, const float E[16], hipStream_t s, bool want_decision) {
+    if (v->p.z_nshards != 1) return fail(SEMTSDF_ERR_UNSUPPORTED, "association on a Z-sharded handle is not supported yet");
+    if (!(v->p.flags & SEMTSDF_F_SEMANTIC)) return fail(SEMTSDF_ERR_STATE, "association needs a SEMANTIC volume");
+    if (v->n_obs == 0) return fail(SEMTSDF_ERR_STATE, "association needs n_obs > 0 (tsdf.cu:426)");
+    EventPair ep;
+    timing_begin(v, v->ev_assoc, s, &ep);
+    HIPC(hipMemsetAsync(v->tables_d, 0, sizeof(AssocTables), s));
+    HIPC(hipMemsetAsync(&v->tables_d->first_px[0], 0xFF, sizeof(unsigned) * 256, s));
+    HIPC(launch_mask_stats(mask_d, (int)npx(v), v->tables_d, s));
+    AssocArgs a{};
+    a.g = v->g;
+    a.b = v->b;
+    a.cam = assoc_camera(v, E);
+    a.width = v->p.width;
+    a.height = v->p.height;
+    a.n_obs = (float)v->n_obs;
+    a.eps = v->p.prior_mrcnn_err_rate;
+    a.box_thresh = v->p.box_thresh;
+    a.mask = mask_d;
+    a.tables = v->tables_d;
+    HIPC(launch_assoc_march(a, s));
+    HIPC(launch_assoc_decide(v->tables_d, v->decision_d, 0, v->p.prior_mrcnn_err_rate, v->num_objs_d, s));
+    HIPC(launch_relabel(mask_d, (int)npx(v), v->decision_d, s));
+    timing_end(v, v->ev_assoc, s, &ep);
+    v->n_assoc++;
+    if (want_decision) HIPC(hipMemcpyAsync(v->decision_h, v->decision_d, sizeof(AssocDecision), hipMemcpyDeviceToHost, s));
+    return SEMTSDF_OK;
+}
+
+void decision_to_stats(const AssocDecision& d, semtsdf_assoc_stats* st) {
+    st->max_obj_now = d.max_obj_now;
+    st->num_objs = d.num_objs_after;
+    for (int i = 0; i < kMaxObjects; ++i) {
+        st->assigned_prev[i] = d.assigned_prev[i];
+        st->assigned_prob[i] = d.assigned_prob[i];
+    }
+    memcpy(st->lut, d.lut, 256);
+}
+
+int validate_mask_host(const semtsdf_vol* v, const uint8_t* mask) {
+    const size_t n = npx(v);
+    for (size_t i = 0; i < n; ++i)
+        if (mask[i] >= kMaxObjects)
+            return fail(SEMTSDF_ERR_LABEL, "mask label %d at pixel %zu >= %d (tsdf.cu:61 would overflow)", mask[i], i,
+                        kMaxObjects);
+    return SEMTSDF_OK;
+}
+
+int check_bad_label(semtsdf_vol* v, hipStream_t s) {
+    unsigned long long c[3];
+    HIPC(hipMemcpyAsync(c, v->counters_d, sizeof(c), hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    if (c[2]) {
+        unsigned long long z = 0;
+        HIPC(hipMemcpyAsync(v->counters_d + 2, &z, sizeof(z), hipMemcpyHostToDevice, s));
+        HIPC(hipStreamSynchronize(s));
+        return fail(SEMTSDF_ERR_LABEL, "a mask label >= %d reached the integrate kernel (histogram update skipped)",
+                    kMaxObjects);
+    }
+    return SEMTSDF_OK;
+}
+
+}  // namespace
+
+// =====================================================================================
+extern "C" {
+
+const char* semtsdf_last_error(void) { return g_err.c_str(); }
+int semtsdf_abi_version(void) { return SEMTSDF_ABI_VERSION; }
+
+int semtsdf_device_count(int* out) {
+    if (!out) return fail(SEMTSDF_ERR_INVALID, "out is NULL");
+    HIPC(hipGetDeviceCount(out));
+    return SEMTSDF_OK;
+}
+
+int semtsdf_set_device(int device) {
+    HIPC(hipSetDevice(device));
+    return SEMTSDF_OK;
+}
+
+int semtsdf_stream_create(void** out) {
+    if (!out) return fail(SEMTSDF_ERR_INVALID, "out is NULL");
+    hipStream_t s;
+    HIPC(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *out = (void*)s;
+    return SEMTSDF_OK;
+}
+
+int semtsdf_stream_destroy(void* s) {
+    if (s) HIPC(hipStreamDestroy((hipStream_t)s));
+    return SEMTSDF_OK;
+}
+
+int semtsdf_stream_sync(void* s) {
+    HIPC(hipStreamSynchronize((hipStream_t)s));
+    return SEMTSDF_OK;
+}
+
+int semtsdf_dev_malloc(void** out, size_t bytes) {
+    if (!out) return fail(SEMTSDF_ERR_INVALID, "out is NULL");
+    HIPC(hipMalloc(out, bytes));
+    return SEMTSDF_OK;
+}
+
+int semtsdf_dev_free(void* p) {
+    if (p) HIPC(hipFree(p));
+    return SEMTSDF_OK;
+}
+
+int semtsdf_memcpy(void* dst, const void* src, size_t bytes, int kind, void* stream) {
+    hipMemcpyKind k;
+    switch (kind) {
+        case 1: k = hipMemcpyHostToDevice; break;
+        case 2: k = hipMemcpyDeviceToHost; break;
+        case 3: k = hipMemcpyDeviceToDevice; break;
+        default: return fail(SEMTSDF_ERR_INVALID, "bad memcpy kind %d", kind);
+    }
+    HIPC(hipMemcpyAsync(dst, src, bytes, k, (hipStream_t)stream));
+    return SEMTSDF_OK;
+}
+
+int semtsdf_params_default(semtsdf_params* p, int dim, const float intr[4], int width, int height) {
+    if (!p || !intr) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    memset(p, 0, sizeof(*p));
+    p->dim[0] = p->dim[1] = p->dim[2] = dim;
+    const float fx = intr[0], fy = intr[1], cx = intr[2], cy = intr[3];
+    // K as tsdf.cu:143-146 (4x4, row-major)
+    p->K[0] = fx; p->K[2] = cx; p->K[5] = fy; p->K[6] = cy; p->K[10] = 1.0f; p->K[15] = 1.0f;
+    // K^-1, computed exactly in double and rounded once
+    p->Kinv[0] = (float)(1.0 / (double)fx);
+    p->Kinv[2] = (float)(-(double)cx / (double)fx);
+    p->Kinv[5] = (float)(1.0 / (double)fy);
+    p->Kinv[6] = (float)(-(double)cy / (double)fy);
+    p->Kinv[10] = 1.0f;
+    p->Kinv[15] = 1.0f;
+    p->width = width;
+    p->height = height;
+    p->depth_scale = 5000.0f;
+    p->gate = 0.99f;
+    p->box_thresh = 0.3f;
+    p->prior_mrcnn_err_rate = 0.05f;
+    p->duplicate_thresh = 0.5f;
+    p->flags = SEMTSDF_F_SEMANTIC | SEMTSDF_F_GATE_COLOR;
+    p->z_shard = 0;
+    p->z_nshards = 1;
+    p->z_chunk = dim;
+    return SEMTSDF_OK;
+}
+
+int semtsdf_place_from_frame(semtsdf_params* p, const uint16_t* depth, double mean_depth, int mode) {
+    if (!p || !depth) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    const int W = p->width, H = p->height;
+    if (W <= 0 || H <= 0) return fail(SEMTSDF_ERR_INVALID, "bad frame size");
+    // boundingRect(findNonZero(depth -> u8)) : SfM saturates (tsdf.cu:180), Python wraps (tsdf.py:35)
+    int x0 = W, y0 = H, x1 = -1, y1 = -1;
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            const uint16_t d = depth[(size_t)y * W + x];
+            const bool nz = (mode == SEMTSDF_PLACE_PYTHON) ? ((d & 0xFF) != 0) : (d != 0);
+            if (nz) {
+                x0 = std::min(x0, x); x1 = std::max(x1, x);
+                y0 = std::min(y0, y); y1 = std::max(y1, y);
+            }
+        }
+    if (x1 < 0) return fail(SEMTSDF_ERR_INVALID, "depth frame has no valid pixel");
+    const int rx = x0, ry = y0, rw = x1 - x0 + 1, rh = y1 - y0 + 1;
+    const float* Ki = p->Kinv;
+    if (mode == SEMTSDF_PLACE_PYTHON) {
+        // tsdf.py:36-47, float64 throughout from the f32 K^-1 entries
+        const double md = mean_depth / 5000.0;
+        double tl[3], br[3];
+        const double tv[3] = {(double)rx, (double)ry, 1.0}, bv[3] = {(double)(rx + rw), (double)(ry + rh), 1.0};
+        for (int i = 0; i < 3; ++i) {
+            tl[i] = ((double)Ki[i * 4 + 0] * tv[0] + (double)Ki[i * 4 + 1] * tv[1]) + (double)Ki[i * 4 + 2] * tv[2];
+            br[i] = ((double)Ki[i * 4 + 0] * bv[0] + (double)Ki[i * 4 + 1] * bv[1]) + (double)Ki[i * 4 + 2] * bv[2];
+            tl[i] *= md;
+            br[i] *= md;
+        }
+        const double dx = tl[0] - br[0], dy = tl[1] - br[1];
+        const double half = std::sqrt(dx * dx + dy * dy) / 2.0;
+        double vox[3];
+        for (int i = 0; i < 3; ++i) {
+            const double c = (tl[i] + br[i]) / 2.0;
+            const double s = c - half, e = c + half;
+            p->vol_start[i] = (float)s;
+            p->vol_end[i] = (float)e;
+            vox[i] = (e - s) / (double)(p->dim[i] - 1);
+            p->voxel[i] = (float)vox[i];
+        }
+        p->mu = (float)(5.0 * vox[0]);  // tsdf.py:47, rounded to f32 for the kernel argument
+    } else {
+        // tsdf.cu:185-199, f32 cv::Mat arithmetic (gemm accumulates in double)
+        const float md = (float)mean_depth;
+        float tl[4], br[4];
+        const float tv[4] = {(float)rx, (float)ry, 1.0f, 1.0f};
+        const float bv[4] = {(float)(rx + rw), (float)(ry + rh), 1.0f, 1.0f};
+        for (int i = 0; i < 4; ++i) {
+            double at = 0, ab = 0;
+            for (int k = 0; k < 4; ++k) {
+                at += (double)Ki[i * 4 + k] * (double)tv[k];
+                ab += (double)Ki[i * 4 + k] * (double)bv[k];
+            }
+            tl[i] = (float)((double)(float)at * (double)md);
+            br[i] = (float)((double)(float)ab * (double)md);
+        }
+        const float dx = tl[0] - br[0], dy = tl[1] - br[1];
+        const float half = (float)(std::sqrt(std::pow((double)dx, 2) + std::pow((double)dy, 2)) / 2.0);
+        for (int i = 0; i < 3; ++i) {
+            const float c = (tl[i] + br[i]) * 0.5f;
+            p->vol_start[i] = c - half;
+            p->vol_end[i] = c + half;
+            p->voxel[i] = (p->vol_end[i] - p->vol_start[i]) / (float)(p->dim[i] - 1);
+        }
+        p->mu = 5.0f * p->voxel[0];
+    }
+    return SEMTSDF_OK;
+}
+
+int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
+    if (!out) return fail(SEMTSDF_ERR_INVALID, "out is NULL");
+    *out = nullptr;
+    int rc = check_params(p);
+    if (rc) return rc;
+    HIPC(hipSetDevice(device));
+    semtsdf_vol* v = new semtsdf_vol();
+    v->p = *p;
+    v->device = device;
+    int chunk, halo;
+    const int lz = local_planes(p, &chunk, &halo);
+    VolGeom& g = v->g;
+    g.dimx = p->dim[0]; g.dimy = p->dim[1]; g.dimz = p->dim[2];
+    g.lz = lz;
+    g.shard = p->z_shard; g.nshards = p->z_nshards; g.chunk = chunk; g.halo = halo;
+    for (int i = 0; i < 3; ++i) { g.start[i] = p->vol_start[i]; g.end[i] = p->vol_end[i]; g.voxel[i] = p->voxel[i]; }
+    g.mu = p->mu;
+    g.nvox = (uint64_t)g.dimx * (uint64_t)g.dimy * (uint64_t)lz;
+    const size_t n = g.nvox;
+    const size_t px = (size_t)p->width * p->height;
+    auto bail = [&](int code) { free_all(v); delete v; return code; };
+    if (hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking) != hipSuccess)
+        return bail(fail(SEMTSDF_ERR_HIP, "hipStreamCreate failed"));
+    const bool ci32 = p->flags & SEMTSDF_F_COLOR_I32;
+    if ((rc = dev_alloc(v, (void**)&v->b.sdf, n * 4))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&v->b.wt, n * 4))) return bail(rc);
+    if ((rc = dev_alloc(v, &v->b.color, n * 3 * (ci32 ? 4 : 1)))) return bail(rc);
+    if (p->flags & SEMTSDF_F_SEMANTIC)
+        if ((rc = dev_alloc(v, (void**)&v->b.hist, n * kMaxObjects * 4))) return bail(rc);
+    if (p->flags & SEMTSDF_F_VOTE) {
+        if ((rc = dev_alloc(v, (void**)&v->b.cls, n * 4))) return bail(rc);
+        if ((rc = dev_alloc(v, (void**)&v->b.cls_cnt, n * 4))) return bail(rc);
+        if ((rc = dev_alloc(v, (void**)&v->cls_d, px * 4))) return bail(rc);
+    }
+    if ((rc = dev_alloc(v, (void**)&v->depth_d, px * 2))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&v->rgb_d, px * 3))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&v->mask_d, px))) return bail(rc);
+    DepthPyramid& pyr = v->pyr;
+    pyr.w0 = (p->width + 7) / 8; pyr.h0 = (p->height + 7) / 8;
+    pyr.w1 = (p->width + 31) / 32; pyr.h1 = (p->height + 31) / 32;
+    pyr.w2 = (p->width + 127) / 128; pyr.h2 = (p->height + 127) / 128;
+    if ((rc = dev_alloc(v, (void**)&pyr.l0, (size_t)pyr.w1 * 4 * pyr.h1 * 4 * 2))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&pyr.l1, (size_t)pyr.w1 * pyr.h1 * 2))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&pyr.l2, (size_t)pyr.w2 * pyr.h2 * 4))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&v->tables_d, sizeof(AssocTables)))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&v->decision_d, sizeof(AssocDecision)))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&v->num_objs_d, 16))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&v->counters_d, 4 * sizeof(unsigned long long)))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&v->palette_d, sizeof(kPalette)))) return bail(rc);
+    if (hipHostMalloc((void**)&v->decision_h, sizeof(AssocDecision), 0) != hipSuccess)
+        return bail(fail(SEMTSDF_ERR_HIP, "hipHostMalloc failed"));
+    if (hipMemcpy(v->palette_d, kPalette, sizeof(kPalette), hipMemcpyHostToDevice) != hipSuccess)
+        return bail(fail(SEMTSDF_ERR_HIP, "palette upload failed"));
+    if ((rc = semtsdf_reset(v, nullptr))) return bail(rc);
+    if (hipStreamSynchronize(v->stream) != hipSuccess) return bail(fail(SEMTSDF_ERR_HIP, "sync failed"));
+    *out = v;
+    return SEMTSDF_OK;
+}
+
+int semtsdf_destroy(semtsdf_vol* v) {
+    if (!v) return SEMTSDF_OK;
+    (void)hipSetDevice(v->device);
+    (void)hipStreamSynchronize(v->stream);
+    free_all(v);
+    delete v;
+    return SEMTSDF_OK;
+}
+
+int semtsdf_get_params(const semtsdf_vol* v, semtsdf_params* out) {
+    if (!v || !out) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    *out = v->p;
+    return SEMTSDF_OK;
+}
+
+int semtsdf_get_state(const semtsdf_vol* v, semtsdf_state* out) {
+    if (!v || !out) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    int n = 0;
+    HIPC(hipMemcpyAsync(&n, v->num_objs_d, sizeof(int), hipMemcpyDeviceToHost, v->stream));
+    HIPC(hipStreamSynchronize(v->stream));
+    out->n_obs = v->n_obs;
+    out->num_objs = n;
+    out->local_dim[0] = v->g.dimx;
+    out->local_dim[1] = v->g.dimy;
+    out->local_dim[2] = v->g.lz;
+    out->local_voxels = v->g.nvox;
+    out->device_bytes = v->device_bytes;
+    return SEMTSDF_OK;
+}
+
+int semtsdf_set_state(semtsdf_vol* v, uint32_t n_obs, int32_t num_objs) {
+    if (!v) return fail(SEMTSDF_ERR_INVALID, "NULL handle");
+    v->n_obs = n_obs;
+    HIPC(hipMemcpyAsync(v->num_objs_d, &num_objs, sizeof(int), hipMemcpyHostToDevice, v->stream));
+    HIPC(hipStreamSynchronize(v->stream));
+    return SEMTSDF_OK;
+}
+
+void* semtsdf_get_stream(const semtsdf_vol* v) { return v ? (void*)v->stream : nullptr; }
+
+int semtsdf_reset(semtsdf_vol* v, void* stream) {
+    if (!v) return fail(SEMTSDF_ERR_INVALID, "NULL handle");
+    HIPC(hipSetDevice(v->device));
+    hipStream_t s = pick(v, stream);
+    const size_t n = v->g.nvox;
+    HIPC(launch_fill_volume(v->g, v->b, v->p.flags, s));
+    HIPC(hipMemsetAsync(v->b.wt, 0, n * 4, s));
+    HIPC(hipMemsetAsync(v->b.color, 0, n * 3 * ((v->p.flags & SEMTSDF_F_COLOR_I32) ? 4 : 1), s));
+    if (v->b.hist) HIPC(hipMemsetAsync(v->b.hist, 0, n * kMaxObjects * 4, s));
+    if (v->b.cls) HIPC(hipMemsetAsync(v->b.cls, 0, n * 4, s));
+    if (v->b.cls_cnt) HIPC(hipMemsetAsync(v->b.cls_cnt, 0, n * 4, s));
+    HIPC(hipMemsetAsync(v->num_objs_d, 0, 16, s));
+    HIPC(hipMemsetAsync(v->counters_d, 0, 4 * sizeof(unsigned long long), s));
+    v->n_obs = 0;
+    return SEMTSDF_OK;
+}
+
+int semtsdf_integrate(semtsdf_vol* v, const uint16_t* depth, const uint8_t* rgb, const uint8_t* mask,
+                      const float E[16], void* stream) {
+    if (!v || !depth || !rgb) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    HIPC(hipSetDevice(v->device));
+    hipStream_t s = pick(v, stream);
+    const size_t n = npx(v);
+    const bool sem = v->p.flags & SEMTSDF_F_SEMANTIC;
+    if (sem) {
+        if (!mask) return fail(SEMTSDF_ERR_INVALID, "semantic volume needs a mask");
+        int rc = validate_mask_host(v, mask);
+        if (rc) return rc;
+    }
+    HIPC(hipMemcpyAsync(v->depth_d, depth, n * 2, hipMemcpyHostToDevice, s));
+    HIPC(hipMemcpyAsync(v->rgb_d, rgb, n * 3, hipMemcpyHostToDevice, s));
+    if (sem) HIPC(hipMemcpyAsync(v->mask_d, mask, n, hipMemcpyHostToDevice, s));
+    int rc = integrate_impl(v, v->depth_d, v->rgb_d, sem ? v->mask_d : nullptr, nullptr, E, s);
+    if (rc) return rc;
+    HIPC(hipStreamSynchronize(s));  // host buffers are borrowed for the call only
+    return SEMTSDF_OK;
+}
+
+int semtsdf_integrate_dev(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d, const uint8_t* mask_d,
+                          const float E[16], void* stream) {
+    if (!v) return fail(SEMTSDF_ERR_INVALID, "NULL handle");
+    return integrate_impl(v, depth_d, rgb_d, mask_d, nullptr, E, pick(v, stream));
+}
+
+int semtsdf_integrate_vote_dev(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d, const int32_t* cls_d,
+                               const float E[16], void* stream) {
+    if (!v) return fail(SEMTSDF_ERR_INVALID, "NULL handle");
+    if (!(v->p.flags & SEMTSDF_F_VOTE)) return fail(SEMTSDF_ERR_STATE, "volume is not in VOTE mode");
+    return integrate_impl(v, depth_d, rgb_d, nullptr, cls_d, E, pick(v, stream));
+}
+
+int semtsdf_associate(semtsdf_vol* v, uint8_t* mask_inout, const float E[16], semtsdf_assoc_stats* stats,
+                      void* stream) {
+    if (!v || !mask_inout || !E) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    HIPC(hipSetDevice(v->device));
+    int rc = validate_mask_host(v, mask_inout);
+    if (rc) return rc;
+    hipStream_t s = pick(v, stream);
+    HIPC(hipMemcpyAsync(v->mask_d, mask_inout, npx(v), hipMemcpyHostToDevice, s));
+    rc = associate_impl(v, v->mask_d, E, s, true);
+    if (rc) return rc;
+    HIPC(hipMemcpyAsync(mask_inout, v->mask_d, npx(v), hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    if (stats) decision_to_stats(*v->decision_h, stats);
+    if (v->decision_h->bad_label)
+        return fail(SEMTSDF_ERR_LABEL, "association produced %d objects (> %d)", v->decision_h->num_objs_after,
+                    kMaxObjects);
+    return SEMTSDF_OK;
+}
+
+int semtsdf_associate_dev(semtsdf_vol* v, uint8_t* mask_d, const float E[16], semtsdf_assoc_stats* stats,
+                          void* stream) {
+    if (!v || !mask_d || !E) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    hipStream_t s = pick(v, stream);
+    int rc = associate_impl(v, mask_d, E, s, stats != nullptr);
+    if (rc) return rc;
+    if (stats) {
+        HIPC(hipStreamSynchronize(s));
+        decision_to_stats(*v->decision_h, stats);
+    }
+    return SEMTSDF_OK;
+}
+
+int semtsdf_assoc_probs(semtsdf_vol* v, const float E[16], float* probs, uint8_t* box_mask, void* stream) {
+    if (!v || !E || !probs || !box_mask) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    if (v->p.z_nshards != 1) return fail(SEMTSDF_ERR_UNSUPPORTED, "sharded handle");
+    if (!(v->p.flags & SEMTSDF_F_SEMANTIC)) return fail(SEMTSDF_ERR_STATE, "needs a SEMANTIC volume");
+    HIPC(hipSetDevice(v->device));
+    hipStream_t s = pick(v, stream);
+    const size_t n = npx(v) * kMaxObjects;
+    if (!v->probs_d) {
+        int rc = dev_alloc(v, (void**)&v->probs_d, n * 4);
+        if (rc) return rc;
+        rc = dev_alloc(v, (void**)&v->box_d, n);
+        if (rc) return rc;
+    }
+    // tables scratch is reused; the mask is all-zero so no log terms are needed
+    HIPC(hipMemsetAsync(v->mask_d, 0, npx(v), s));
+    HIPC(hipMemsetAsync(v->tables_d, 0, sizeof(AssocTables), s));
+    AssocArgs a{};
+    a.g = v->g;
+    a.b = v->b;
+    a.cam = assoc_camera(v, E);
+    a.width = v->p.width;
+    a.height = v->p.height;
+    a.n_obs = (float)(v->n_obs ? v->n_obs : 1);
+    a.eps = v->p.prior_mrcnn_err_rate;
+    a.box_thresh = v->p.box_thresh;
+    a.mask = v->mask_d;
+    a.tables = v->tables_d;
+    a.probs_out = v->probs_d;
+    a.box_out = v->box_d;
+    HIPC(launch_assoc_march(a, s));
+    HIPC(hipMemcpyAsync(probs, v->probs_d, n * 4, hipMemcpyDeviceToHost, s));
+    HIPC(hipMemcpyAsync(box_mask, v->box_d, n, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    return SEMTSDF_OK;
+}
+
+int semtsdf_parse_frame(semtsdf_vol* v, const uint16_t* depth, const uint8_t* rgb, uint8_t* mask_inout,
+                        const float E[16], semtsdf_assoc_stats* stats, void* stream) {
+    if (!v || !depth || !rgb || !E) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    HIPC(hipSetDevice(v->device));
+    hipStream_t s = pick(v, stream);
+    const size_t n = npx(v);
+    const bool sem = v->p.flags & SEMTSDF_F_SEMANTIC;
+    if (sem) {
+        if (!mask_inout) return fail(SEMTSDF_ERR_INVALID, "semantic volume needs a mask");
+        int rc = validate_mask_host(v, mask_inout);
+        if (rc) return rc;
+    }
+    HIPC(hipMemcpyAsync(v->depth_d, depth, n * 2, hipMemcpyHostToDevice, s));
+    HIPC(hipMemcpyAsync(v->rgb_d, rgb, n * 3, hipMemcpyHostToDevice, s));
+    if (sem) {
+        HIPC(hipMemcpyAsync(v->mask_d, mask_inout, n, hipMemcpyHostToDevice, s));
+        if (v->n_obs > 0) {
+            int rc = associate_impl(v, v->mask_d, E, s, true);
+            if (rc) return rc;
+        } else {
+            HIPC(hipMemsetAsync(v->tables_d, 0, sizeof(AssocTables), s));
+            HIPC(hipMemsetAsync(&v->tables_d->first_px[0], 0xFF, sizeof(unsigned) * 256, s));
+            HIPC(launch_mask_stats(v->mask_d, (int)n, v->tables_d, s));
+            HIPC(launch_first_frame_objs(v->tables_d, v->num_objs_d, s));
+        }
+    }
+    int rc = integrate_impl(v, v->depth_d, v->rgb_d, sem ? v->mask_d : nullptr, nullptr, E, s);
+    if (rc) return rc;
+    v->n_obs++;
+    if (sem) HIPC(hipMemcpyAsync(mask_inout, v->mask_d, n, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    if (sem && v->n_obs > 1) {
+        if (stats) decision_to_stats(*v->decision_h, stats);
+        if (v->decision_h->bad_label)
+            return fail(SEMTSDF_ERR_LABEL, "association produced %d objects (> %d)", v->decision_h->num_objs_after,
+                        kMaxObjects);
+    } else if (stats) {
+        memset(stats, 0, sizeof(*stats));
+        for (int i = 0; i < kMaxObjects; ++i) stats->assigned_prev[i] = -1;
+        for (int i = 0; i < 256; ++i) stats->lut[i] = (uint8_t)i;
+        int no = 0;
+        HIPC(hipMemcpy(&no, v->num_objs_d, sizeof(int), hipMemcpyDeviceToHost));
+        stats->num_objs = no;
+        stats->max_obj_now = no;
+    }
+    if (sem) return check_bad_label(v, s);
+    return SEMTSDF_OK;
+}
+
+int semtsdf_parse_frame_dev(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d, uint8_t* mask_d,
+                            const float E[16], void* stream) {
+    if (!v || !E) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    hipStream_t s = pick(v, stream);
+    const bool sem = v->p.flags & SEMTSDF_F_SEMANTIC;
+    if (sem) {
+        if (!mask_d) return fail(SEMTSDF_ERR_INVALID, "semantic volume needs a mask");
+        if (v->n_obs > 0) {
+            int rc = associate_impl(v, mask_d, E, s, false);
+            if (rc) return rc;
+        } else {
+            HIPC(hipMemsetAsync(v->tables_d, 0, sizeof(AssocTables), s));
+            HIPC(hipMemsetAsync(&v->tables_d->first_px[0], 0xFF, sizeof(unsigned) * 256, s));
+            HIPC(launch_mask_stats(mask_d, (int)npx(v), v->tables_d, s));
+            HIPC(launch_first_frame_objs(v->tables_d, v->num_objs_d, s));
+        }
+    }
+    int rc = integrate_impl(v, depth_d, rgb_d, sem ? mask_d : nullptr, nullptr, E, s);
+    if (rc) return rc;
+    v->n_obs++;
+    return SEMTSDF_OK;
+}
+
+int semtsdf_orbit_camera(const float Kinv[16], float angle, float dist, float s2w[16], float c[3]) {
+    if (!Kinv || !s2w || !c) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    // viewer.cu:140-146
+    const float ca = cosf(angle), sa = sinf(angle);
+    const float rot[16] = {ca, 0, -sa, dist * sa, 0, 1, 0, 0, sa, 0, ca, dist - dist * ca, 0, 0, 0, 1};
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            double acc = 0;
+            for (int k = 0; k < 4; ++k) acc += (double)rot[i * 4 + k] * (double)Kinv[k * 4 + j];
+            s2w[i * 4 + j] = (float)acc;
+        }
+    const float r = dist + 0.5f;
+    c[0] = r * sa;
+    c[1] = 0.0f;
+    c[2] = r - r * ca;
+    return SEMTSDF_OK;
+}
+
+static int raycast_impl(semtsdf_vol* v, const float s2w[16], const float c[3], int mode, uint8_t* out_bgr_d,
+                        float* out_t_d, hipStream_t s) {
+    if (v->p.z_nshards != 1) return fail(SEMTSDF_ERR_UNSUPPORTED, "raycast on a Z-sharded handle is not supported yet");
+    if (mode == SEMTSDF_RENDER_LABEL && !(v->p.flags & SEMTSDF_F_SEMANTIC))
+        return fail(SEMTSDF_ERR_STATE, "label render needs a SEMANTIC volume");
+    RenderArgs a{};
+    a.g = v->g;
+    a.b = v->b;
+    for (int i = 0; i < 12; ++i) a.cam.s2w[i] = s2w[i];
+    a.cam.o[0] = c[0]; a.cam.o[1] = c[1]; a.cam.o[2] = c[2];
+    a.cam.use_s2w = 1;
+    a.width = v->p.width;
+    a.height = v->p.height;
+    a.mode = mode;
+    a.color_i32 = (v->p.flags & SEMTSDF_F_COLOR_I32) ? 1 : 0;
+    a.palette = v->palette_d;
+    a.out_bgr = out_bgr_d;
+    a.out_t = out_t_d;
+    EventPair ep;
+    timing_begin(v, v->ev_render, s, &ep);
+    HIPC(launch_render(a, s));
+    timing_end(v, v->ev_render, s, &ep);
+    v->n_render++;
+    return SEMTSDF_OK;
+}
+
+int semtsdf_raycast(semtsdf_vol* v, const float s2w[16], const float c[3], int mode, uint8_t* out_bgr, float* out_t,
+                    void* stream) {
+    if (!v || !s2w || !c || !out_bgr) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    HIPC(hipSetDevice(v->device));
+    hipStream_t s = pick(v, stream);
+    const size_t n = npx(v);
+    if (!v->render_d) {
+        int rc = dev_alloc(v, (void**)&v->render_d, n * 3);
+        if (rc) return rc;
+        rc = dev_alloc(v, (void**)&v->render_t_d, n * 4);
+        if (rc) return rc;
+    }
+    int rc = raycast_impl(v, s2w, c, mode, v->render_d, v->render_t_d, s);
+    if (rc) return rc;
+    HIPC(hipMemcpyAsync(out_bgr, v->render_d, n * 3, hipMemcpyDeviceToHost, s));
+    if (out_t) HIPC(hipMemcpyAsync(out_t, v->render_t_d, n * 4, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    return SEMTSDF_OK;
+}
+
+int semtsdf_raycast_dev(semtsdf_vol* v, const float s2w[16], const float c[3], int mode, uint8_t* out_bgr_d,
+                        float* out_t_d, void* stream) {
+    if (!v || !s2w || !c || !out_bgr_d) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    return raycast_impl(v, s2w, c, mode, out_bgr_d, out_t_d, pick(v, stream));
+}
+
+int semtsdf_download(semtsdf_vol* v, float* sdf, int32_t* wt, void* color, uint32_t* hist, int32_t* cls,
+                     int32_t* cls_cnt) {
+    if (!v) return fail(SEMTSDF_ERR_INVALID, "NULL handle");
+    HIPC(hipSetDevice(v->device));
+    hipStream_t s = v->stream;
+    const size_t n = v->g.nvox;
+    if (sdf) HIPC(hipMemcpyAsync(sdf, v->b.sdf, n * 4, hipMemcpyDeviceToHost, s));
+    if (wt) HIPC(hipMemcpyAsync(wt, v->b.wt, n * 4, hipMemcpyDeviceToHost, s));
+    if (color)
+        HIPC(hipMemcpyAsync(color, v->b.color, n * 3 * ((v->p.flags & SEMTSDF_F_COLOR_I32) ? 4 : 1),
+                            hipMemcpyDeviceToHost, s));
+    if (cls) {
+        if (!v->b.cls) return fail(SEMTSDF_ERR_STATE, "not a VOTE volume");
+        HIPC(hipMemcpyAsync(cls, v->b.cls, n * 4, hipMemcpyDeviceToHost, s));
+    }
+    if (cls_cnt) {
+        if (!v->b.cls_cnt) return fail(SEMTSDF_ERR_STATE, "not a VOTE volume");
+        HIPC(hipMemcpyAsync(cls_cnt, v->b.cls_cnt, n * 4, hipMemcpyDeviceToHost, s));
+    }
+    if (hist) {
+        if (!v->b.hist) return fail(SEMTSDF_ERR_STATE, "not a SEMANTIC volume");
+        const uint64_t chunk = std::min<uint64_t>(n, 1ull << 22);  // 4M voxels = 512 MiB staging
+        uint32_t* stage = nullptr;
+        HIPC(hipMalloc(&stage, chunk * kMaxObjects * 4));
+        for (uint64_t v0 = 0; v0 < n; v0 += chunk) {
+            const uint64_t nv = std::min<uint64_t>(chunk, n - v0);
+            hipError_t e = launch_hist_chunk_to_vm(v->b.hist, stage, n, v0, nv, s);
+            if (e == hipSuccess) e = hipMemcpyAsync(hist + v0 * kMaxObjects, stage, nv * kMaxObjects * 4, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) {
+                (void)hipFree(stage);
+                return fail(SEMTSDF_ERR_HIP, "histogram download: %s", hipGetErrorString(e));
+            }
+        }
+        HIPC(hipFree(stage));
+    }
+    HIPC(hipStreamSynchronize(s));
+    return SEMTSDF_OK;
+}
+
+int semtsdf_upload(semtsdf_vol* v, const float* sdf, const int32_t* wt, const void* color, const uint32_t* hist,
+                   const int32_t* cls, const int32_t* cls_cnt) {
+    if (!v) return fail(SEMTSDF_ERR_INVALID, "NULL handle");
+    HIPC(hipSetDevice(v->device));
+    hipStream_t s = v->stream;
+    const size_t n = v->g.nvox;
+    if (sdf) HIPC(hipMemcpyAsync(v->b.sdf, sdf, n * 4, hipMemcpyHostToDevice, s));
+    if (wt) HIPC(hipMemcpyAsync(v->b.wt, wt, n * 4, hipMemcpyHostToDevice, s));
+    if (color)
+        HIPC(hipMemcpyAsync(v->b.color, color, n * 3 * ((v->p.flags & SEMTSDF_F_COLOR_I32) ? 4 : 1),
+                            hipMemcpyHostToDevice, s));
+    if (cls) {
+        if (!v->b.cls) return fail(SEMTSDF_ERR_STATE, "not a VOTE volume");
+        HIPC(hipMemcpyAsync(v->b.cls, cls, n * 4, hipMemcpyHostToDevice, s));
+    }
+    if (cls_cnt) {
+        if (!v->b.cls_cnt) return fail(SEMTSDF_ERR_STATE, "not a VOTE volume");
+        HIPC(hipMemcpyAsync(v->b.cls_cnt, cls_cnt, n * 4, hipMemcpyHostToDevice, s));
+    }
+    if (hist) {
+        if (!v->b.hist) return fail(SEMTSDF_ERR_STATE, "not a SEMANTIC volume");
+        const uint64_t chunk = std::min<uint64_t>(n, 1ull << 22);
+        uint32_t* stage = nullptr;
+        HIPC(hipMalloc(&stage, chunk * kMaxObjects * 4));
+        for (uint64_t v0 = 0; v0 < n; v0 += chunk) {
+            const uint64_t nv = std::min<uint64_t>(chunk, n - v0);
+            hipError_t e = hipMemcpyAsync(stage, hist + v0 * kMaxObjects, nv * kMaxObjects * 4, hipMemcpyHostToDevice, s);
+            if (e == hipSuccess) e = launch_hist_chunk_to_bm(stage, v->b.hist, n, v0, nv, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) {
+                (void)hipFree(stage);
+                return fail(SEMTSDF_ERR_HIP, "histogram upload: %s", hipGetErrorString(e));
+            }
+        }
+        HIPC(hipFree(stage));
+    }
+    HIPC(hipStreamSynchronize(s));
+    return SEMTSDF_OK;
+}
+
+int semtsdf_set_instrumentation(semtsdf_vol* v, int enable) {
+    if (!v) return fail(SEMTSDF_ERR_INVALID, "NULL handle");
+    v->instr = enable;
+    return SEMTSDF_OK;
+}
+
+static double drain(std::vector<EventPair>& vec) {
+    double t = 0;
+    for (auto& e : vec) {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, e.a, e.b) == hipSuccess) t += ms;
+        (void)hipEventDestroy(e.a);
+        (void)hipEventDestroy(e.b);
+    }
+    vec.clear();
+    return t;
+}
+
+int semtsdf_get_timing(semtsdf_vol* v, semtsdf_timing* out) {
+    if (!v || !out) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    HIPC(hipSetDevice(v->device));
+    HIPC(hipStreamSynchronize(v->stream));
+    HIPC(hipDeviceSynchronize());
+    v->t_integrate += drain(v->ev_integrate);
+    v->t_assoc += drain(v->ev_assoc);
+    v->t_render += drain(v->ev_render);
+    unsigned long long c[3] = {0, 0, 0};
+    HIPC(hipMemcpy(c, v->counters_d, sizeof(c), hipMemcpyDeviceToHost));
+    out->integrate_ms = v->t_integrate;
+    out->assoc_ms = v->t_assoc;
+    out->render_ms = v->t_render;
+    out->n_integrate = v->n_integrate;
+    out->n_assoc = v->n_assoc;
+    out->n_render = v->n_render;
+    out->touched = c[0];
+    out->gated = c[1];
+    return SEMTSDF_OK;
+}
+
+int semtsdf_reset_timing(semtsdf_vol* v) {
+    if (!v) return fail(SEMTSDF_ERR_INVALID, "NULL handle");
+    HIPC(hipSetDevice(v->device));
+    HIPC(hipDeviceSynchronize());
+    drain(v->ev_integrate);
+    drain(v->ev_assoc);
+    drain(v->ev_render);
+    v->t_integrate = v->t_assoc = v->t_render = 0;
+    v->n_integrate = v->n_assoc = v->n_render = 0;
+    HIPC(hipMemset(v->counters_d, 0, 2 * sizeof(unsigned long long)));
+    return SEMTSDF_OK;
+}
+
+// Drop-in for tsdf_cuda.tsdf_update: whole-volume in, kernel, whole-volume out, like the
+// reference (TSDF_Python/tsdf.cu:78-112), but with a cached device volume instead of a
+// fresh thrust allocation per call.
+int semtsdf_tsdf_update(float* tsdf_diff, int32_t* tsdf_color, int32_t* tsdf_wt, int32_t* tsdf_cls,
+                        int32_t* tsdf_cls_cnt, int vol_dim, const float* vol_start, float voxel, float miu,
+                        const float* intrinsic, const uint16_t* depth, const uint8_t* color, const int32_t* cls,
+                        const float* extrinsic2init, int width, int height) {
+    if (!tsdf_diff || !tsdf_color || !tsdf_wt || !tsdf_cls || !tsdf_cls_cnt || !vol_start || !intrinsic || !depth ||
+        !color || !cls || !extrinsic2init)
+        return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    static std::mutex mu_cache;
+    static semtsdf_vol* cache = nullptr;
+    std::lock_guard<std::mutex> lock(mu_cache);
+    semtsdf_params p{};
+    const float intr[4] = {intrinsic[0], intrinsic[5], intrinsic[2], intrinsic[6]};
+    int rc = semtsdf_params_default(&p, vol_dim, intr, width, height);
+    if (rc) return rc;
+    for (int i = 0; i < 16; ++i) p.K[i] = intrinsic[i];
+    for (int i = 0; i < 3; ++i) {
+        p.vol_start[i] = vol_start[i];
+        p.voxel[i] = voxel;  // TSDF_Python passes the scalar voxel[0] (tsdf.py:63)
+        p.vol_end[i] = vol_start[i] + voxel * (float)(vol_dim - 1);
+    }
+    p.mu = miu;
+    p.flags = SEMTSDF_F_VOTE | SEMTSDF_F_COLOR_I32;
+    if (cache && (cache->p.dim[0] != vol_dim || cache->p.width != width || cache->p.height != height)) {
+        semtsdf_destroy(cache);
+        cache = nullptr;
+    }
+    if (!cache) {
+        rc = semtsdf_create(&p, 0, &cache);
+        if (rc) return rc;
+    }
+    semtsdf_vol* v = cache;
+    v->p = p;
+    for (int i = 0; i < 3; ++i) { v->g.start[i] = p.vol_start[i]; v->g.voxel[i] = p.voxel[i]; v->g.end[i] = p.vol_end[i]; }
+    v->g.mu = p.mu;
+    rc = semtsdf_upload(v, tsdf_diff, tsdf_wt, tsdf_color, nullptr, tsdf_cls, tsdf_cls_cnt);
+    if (rc) return rc;
+    const size_t n = npx(v);
+    hipStream_t s = v->stream;
+    HIPC(hipMemcpyAsync(v->depth_d, depth, n * 2, hipMemcpyHostToDevice, s));
+    HIPC(hipMemcpyAsync(v->rgb_d, color, n * 3, hipMemcpyHostToDevice, s));
+    HIPC(hipMemcpyAsync(v->cls_d, cls, n * 4, hipMemcpyHostToDevice, s));
+    rc = integrate_impl(v, v->depth_d, v->rgb_d, nullptr, v->cls_d, extrinsic2init, s);
+    if (rc) return rc;
+    return semtsdf_download(v, tsdf_diff, tsdf_wt, tsdf_color, nullptr, tsdf_cls, tsdf_cls_cnt);
+}
+
+}  // extern "C"

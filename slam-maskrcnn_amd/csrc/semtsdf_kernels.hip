@@ -1,0 +1,779 @@
+// gfx950 (CDNA4) kernels of the semantic TSDF engine.
+//
+// Reference semantics (restated, not ported):
+//   integrate  — src/SfM_CUDA/tsdf.cu:18-70 (design A, histogram) and
+//                src/TSDF_Python/tsdf.cu:10-58 (design B, label vote)
+//   association raycast — src/SfM_CUDA/tsdf.cu:72-135 + utils.cu:93-170
+//   association accumulation/decision — src/SfM_CUDA/tsdf.cu:304-416
+//   render raycast — src/SfM_CUDA/viewer.cu:17-86
+//
+// Floating-point contract (shared with oracle/semtsdf_oracle.c, which is an independent
+// CPU restatement): the whole file is compiled with -ffp-contract=off, every fused
+// multiply-add below is written out as fmaf(), divisions are IEEE correctly rounded
+// (hipcc default), so the f32 results are reproducible bit for bit on the host.
+//   p      = fmaf(idx, voxel, start)                            (tsdf.cu:30)
+//   dot3   = fmaf(a2,b2, fmaf(a1,b1, a0*b0))                    (helper_math dot)
+//   dot4h  = dot3 + a3                                           (w = 1)
+//   mix    = fmaf(t, b, (1-t)*a)                                 (utils.cu:94-96)
+//   normalize(v) = v * (1/sqrtf(dot3(v,v)))
+//
+// Memory layout: flat x-major volume, z fastest; a workgroup owns an 8(x) x 8(y) x 32(z)
+// brick and its 256 lanes map to (z, y), so every wave-instruction touches two
+// contiguous 128-B runs of the sdf/weight planes.  The histogram is bin-major
+// ([32][voxels]) so lanes that see the same instance label update contiguous words.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <limits.h>
+#include "semtsdf_internal.h"
+
+namespace semtsdf {
+
+// ------------------------------------------------------------------------------------
+// scalar helpers
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ int f2i_rd(float x) {
+    // __float2int_rd semantics: floor, saturate, NaN -> 0
+    const float f = floorf(x);
+    if (!(f == f)) return 0;
+    if (f >= 2147483648.0f) return INT_MAX;
+    if (f <= -2147483648.0f) return INT_MIN;
+    return (int)f;
+}
+
+__device__ __forceinline__ float dot3(float a0, float a1, float a2, float b0, float b1, float b2) {
+    return fmaf(a2, b2, fmaf(a1, b1, a0 * b0));
+}
+
+__device__ __forceinline__ float mixf(float a, float b, float t) {
+    return fmaf(t, b, (1.0f - t) * a);
+}
+
+__device__ __forceinline__ int local_to_global_z(const VolGeom& g, int l) {
+    if (g.nshards == 1) return l;
+    const int per = g.chunk + g.halo;
+    const int c = l / per;
+    const int w = l - c * per;
+    return (c * g.nshards + g.shard) * g.chunk + w;
+}
+
+// Project one voxel (reference tsdf.cu:30-44).  Returns camera-space z in *qz and the
+// pixel in *px/*py.
+__device__ __forceinline__ void project_voxel(const float* __restrict__ E, const float* __restrict__ K,
+                                              float px, float py, float pz,
+                                              float* qz_out, int* ix, int* iy) {
+    const float qx = dot3(E[0], E[1], E[2], px, py, pz) + E[3];
+    const float qy = dot3(E[4], E[5], E[6], px, py, pz) + E[7];
+    const float qz = dot3(E[8], E[9], E[10], px, py, pz) + E[11];
+    const float sx = dot3(K[0], K[1], K[2], qx, qy, qz);
+    const float sy = dot3(K[3], K[4], K[5], qx, qy, qz);
+    const float sz = dot3(K[6], K[7], K[8], qx, qy, qz);
+    *qz_out = qz;
+    *ix = f2i_rd(sx / sz);
+    *iy = f2i_rd(sy / sz);
+}
+
+// ------------------------------------------------------------------------------------
+// volume fill: sdf := mu (tsdf.cu:243-244).  Zeros are hipMemsetAsync'd by the host.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_fill_f32(float* __restrict__ p, uint64_t n, float v) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 4;
+    for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += stride) {
+        if (i + 4 <= n) {
+            *reinterpret_cast<float4*>(p + i) = make_float4(v, v, v, v);
+        } else {
+            for (uint64_t k = i; k < n; ++k) p[k] = v;
+        }
+    }
+}
+
+hipError_t launch_fill_volume(const VolGeom& g, const VolBufs& b, uint32_t flags, hipStream_t s) {
+    (void)flags;
+    const uint64_t n = g.nvox;
+    uint64_t blocks = (n / 4 + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(k_fill_f32, dim3((unsigned)blocks), dim3(256), 0, s, b.sdf, n, g.mu);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------
+// depth pyramid: max raw depth over 8/32/128-pixel tiles, for brick culling.
+// One workgroup per 32x32 pixel tile; 256 lanes x 4 pixels.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restrict__ depth, int w, int h,
+                                                       DepthPyramid p) {
+    __shared__ unsigned s_m[32][8];
+    const int tx = blockIdx.x, ty = blockIdx.y;
+    const int t = threadIdx.x;
+    const int r = t >> 3;          // row in tile
+    const int c4 = (t & 7) * 4;    // first column in tile
+    const int yy = ty * 32 + r;
+    unsigned m = 0;
+    if (yy < h) {
+        for (int k = 0; k < 4; ++k) {
+            const int xx = tx * 32 + c4 + k;
+            if (xx < w) m = max(m, (unsigned)depth[(size_t)yy * w + xx]);
+        }
+    }
+    s_m[r][t & 7] = m;
+    __syncthreads();
+    __shared__ unsigned s_l0[4][4];
+    if (t < 16) {
+        const int a = t >> 2, bcol = t & 3;  // level-0 tile (a, bcol) inside this 32x32 tile
+        unsigned mm = 0;
+        for (int rr = 0; rr < 8; ++rr) {
+            mm = max(mm, s_m[a * 8 + rr][bcol * 2]);
+            mm = max(mm, s_m[a * 8 + rr][bcol * 2 + 1]);
+        }
+        s_l0[a][bcol] = mm;
+        const int gx0 = tx * 4 + bcol, gy0 = ty * 4 + a;
+        if (gx0 < p.w0 && gy0 < p.h0) p.l0[gy0 * p.w0 + gx0] = (uint16_t)mm;
+    }
+    __syncthreads();
+    if (t == 0) {
+        unsigned mm = 0;
+        for (int a = 0; a < 4; ++a)
+            for (int bcol = 0; bcol < 4; ++bcol) mm = max(mm, s_l0[a][bcol]);
+        p.l1[ty * p.w1 + tx] = (uint16_t)mm;
+        atomicMax(p.l2 + (ty / 4) * p.w2 + (tx / 4), mm);
+    }
+}
+
+hipError_t launch_depth_pyramid(const uint16_t* depth, int w, int h, const DepthPyramid& p, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(p.l2, 0, (size_t)p.w2 * p.h2 * sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_depth_pyramid, dim3(p.w1, p.h1), dim3(256), 0, s, depth, w, h, p);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------
+// integrate
+// ------------------------------------------------------------------------------------
+constexpr int BX = 8, BY = 8, BZ = 32;
+
+// Conservative brick test run by one wave: returns 1 when no voxel of the brick can pass
+// the projection / depth tests of tsdf.cu:46-50 (culling never changes results).
+__device__ int brick_cull(const IntegrateArgs& a, int x0, int y0, int lz0, int lane) {
+    const VolGeom& g = a.g;
+    const int x1 = min(x0 + BX - 1, g.dimx - 1);
+    const int y1 = min(y0 + BY - 1, g.dimy - 1);
+    const int gz0 = local_to_global_z(g, lz0);
+    int gz1 = local_to_global_z(g, min(lz0 + BZ - 1, g.lz - 1));
+    if (gz0 >= g.dimz) return 1;  // only halo planes beyond the volume
+    gz1 = min(gz1, g.dimz - 1);
+    float umin = 3.0e38f, umax = -3.0e38f, vmin = 3.0e38f, vmax = -3.0e38f;
+    float zmin = 3.0e38f, zmax = -3.0e38f, wmin = 3.0e38f, wmax = -3.0e38f;
+    for (int c = 0; c < 8; ++c) {
+        const float px = fmaf((float)((c & 1) ? x1 : x0), g.voxel[0], g.start[0]);
+        const float py = fmaf((float)((c & 2) ? y1 : y0), g.voxel[1], g.start[1]);
+        const float pz = fmaf((float)((c & 4) ? gz1 : gz0), g.voxel[2], g.start[2]);
+        const float qx = dot3(a.E[0], a.E[1], a.E[2], px, py, pz) + a.E[3];
+        const float qy = dot3(a.E[4], a.E[5], a.E[6], px, py, pz) + a.E[7];
+        const float qz = dot3(a.E[8], a.E[9], a.E[10], px, py, pz) + a.E[11];
+        const float sx = dot3(a.K[0], a.K[1], a.K[2], qx, qy, qz);
+        const float sy = dot3(a.K[3], a.K[4], a.K[5], qx, qy, qz);
+        const float sz = dot3(a.K[6], a.K[7], a.K[8], qx, qy, qz);
+        const float u = sx / sz, v = sy / sz;
+        umin = fminf(umin, u); umax = fmaxf(umax, u);
+        vmin = fminf(vmin, v); vmax = fmaxf(vmax, v);
+        zmin = fminf(zmin, qz); zmax = fmaxf(zmax, qz);
+        wmin = fminf(wmin, sz); wmax = fmaxf(wmax, sz);
+    }
+    // The image of a box under a perspective map is the hull of its corner images only
+    // when the projective depth sz keeps one sign over the box.
+    const float zeps = 1.0e-3f;
+    if (!(wmin > zeps) && !(wmax < -zeps)) return 0;
+    if (!(umin == umin) || !(vmin == vmin) || !(umax == umax) || !(vmax == vmax)) return 0;
+    // 1-pixel guard band around the projected hull of the brick
+    const float W = (float)a.width, H = (float)a.height;
+    if (umax + 1.0f < 0.0f || umin - 1.0f > W || vmax + 1.0f < 0.0f || vmin - 1.0f > H) return 1;
+    int u0 = (int)fmaxf(floorf(umin) - 1.0f, 0.0f);
+    int u1 = (int)fminf(floorf(umax) + 1.0f, W - 1.0f);
+    int v0 = (int)fmaxf(floorf(vmin) - 1.0f, 0.0f);
+    int v1 = (int)fminf(floorf(vmax) + 1.0f, H - 1.0f);
+    if (u0 > u1 || v0 > v1) return 1;          // hull lies entirely in the guard band
+    // pick the finest pyramid level with <= 64 tiles over the footprint
+    const uint16_t* lvl;
+    int ts, lw;
+    const unsigned* lvl2 = nullptr;
+    if (((u1 >> 3) - (u0 >> 3) + 1) * ((v1 >> 3) - (v0 >> 3) + 1) <= 64) {
+        lvl = a.pyr.l0; ts = 3; lw = a.pyr.w0;
+    } else if (((u1 >> 5) - (u0 >> 5) + 1) * ((v1 >> 5) - (v0 >> 5) + 1) <= 64) {
+        lvl = a.pyr.l1; ts = 5; lw = a.pyr.w1;
+    } else {
+        lvl = nullptr; lvl2 = a.pyr.l2; ts = 7; lw = a.pyr.w2;
+    }
+    const int tx0 = u0 >> ts, tx1 = u1 >> ts, ty0 = v0 >> ts, ty1 = v1 >> ts;
+    const int ntx = tx1 - tx0 + 1;
+    const int ntiles = ntx * (ty1 - ty0 + 1);
+    unsigned m = 0;
+    for (int k = lane; k < ntiles; k += 64) {
+        const int ty = ty0 + k / ntx, tx = tx0 + k % ntx;
+        m = max(m, lvl ? (unsigned)lvl[ty * lw + tx] : lvl2[ty * lw + tx]);
+    }
+    for (int off = 32; off > 0; off >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, off, 64));
+    if (m == 0) return 1;                       // every pixel has depth 0
+    const float dmax = (float)m / a.depth_scale;
+    const float margin = 1.0e-3f + 1.0e-4f * fabsf(zmax);
+    // every voxel has qz >= zmin, so diff <= dmax - zmin; reject when that is <= -mu
+    if (dmax - zmin < -g.mu - margin) return 1;
+    return 0;
+}
+
+template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT>
+__global__ __launch_bounds__(256) void k_integrate(IntegrateArgs a) {
+    const VolGeom& g = a.g;
+    const int x0 = blockIdx.x * BX, y0 = blockIdx.y * BY, lz0 = blockIdx.z * BZ;
+    const int tid = threadIdx.x;
+    if (a.cull) {
+        __shared__ int s_skip;
+        if (tid < 64) {
+            const int sk = brick_cull(a, x0, y0, lz0, tid);
+            if (tid == 0) s_skip = sk;
+        }
+        __syncthreads();
+        if (s_skip) return;
+    }
+    const int l = lz0 + (tid & (BZ - 1));
+    const int gy = y0 + (tid >> 5);
+    unsigned n_touch = 0, n_gate = 0, bad = 0;
+    bool active = (l < g.lz) && (gy < g.dimy);
+    int gz = 0;
+    if (active) {
+        gz = local_to_global_z(g, l);
+        active = gz < g.dimz;
+    }
+    if (active) {
+        const float py = fmaf((float)gy, g.voxel[1], g.start[1]);
+        const float pz = fmaf((float)gz, g.voxel[2], g.start[2]);
+        const uint64_t plane = (uint64_t)g.dimy * (uint64_t)g.lz;
+        const uint64_t base = (uint64_t)gy * (uint64_t)g.lz + (uint64_t)l;
+        const int xe = min(x0 + BX, g.dimx);
+        for (int gx = x0; gx < xe; ++gx) {
+            const float px = fmaf((float)gx, g.voxel[0], g.start[0]);
+            float qz;
+            int ix, iy;
+            project_voxel(a.E, a.K, px, py, pz, &qz, &ix, &iy);
+            if (ix < 0 || ix >= a.width || iy < 0 || iy >= a.height) continue;
+            const int img = iy * a.width + ix;
+            const unsigned d = a.depth[img];
+            if (d == 0) continue;
+            float diff = (float)d / a.depth_scale - qz;
+            if (diff <= -g.mu) continue;
+            if (diff > g.mu) diff = g.mu;
+            diff = diff / g.mu;
+            const uint64_t v = (uint64_t)gx * plane + base;
+            const int w = a.b.wt[v];
+            const float s = a.b.sdf[v];
+            a.b.sdf[v] = fmaf(s, (float)w, diff) / (float)(w + 1);
+            if (COUNT) ++n_touch;
+            if (!GATE || diff < a.gate) {
+                if (COUNT) ++n_gate;
+                const uint8_t* rgb = a.rgb + (size_t)img * 3;
+                if (CI32) {
+                    int32_t* c = reinterpret_cast<int32_t*>(a.b.color) + v * 3;
+                    c[0] = (c[0] * w + (int)rgb[0]) / (w + 1);
+                    c[1] = (c[1] * w + (int)rgb[1]) / (w + 1);
+                    c[2] = (c[2] * w + (int)rgb[2]) / (w + 1);
+                } else {
+                    uint8_t* c = reinterpret_cast<uint8_t*>(a.b.color) + v * 3;
+                    c[0] = (uint8_t)(((int)c[0] * w + (int)rgb[0]) / (w + 1));
+                    c[1] = (uint8_t)(((int)c[1] * w + (int)rgb[1]) / (w + 1));
+                    c[2] = (uint8_t)(((int)c[2] * w + (int)rgb[2]) / (w + 1));
+                }
+                if (SEM) {
+                    const unsigned lab = a.mask[img];
+                    if (lab < (unsigned)kMaxObjects) {
+                        a.b.hist[(uint64_t)lab * g.nvox + v] += 1u;
+                    } else {
+                        bad = 1;
+                    }
+                }
+            }
+            a.b.wt[v] = w + 1;
+            if (VOTE) {
+                const int lab = a.cls[img];
+                const int cnt = a.b.cls_cnt[v];
+                if (cnt == 0) {
+                    a.b.cls[v] = lab;
+                    a.b.cls_cnt[v] = 1;
+                } else if (a.b.cls[v] == lab) {
+                    a.b.cls_cnt[v] = cnt + 1;
+                } else {
+                    a.b.cls_cnt[v] = cnt - 1;
+                }
+            }
+        }
+    }
+    if (SEM && bad) atomicOr(reinterpret_cast<unsigned*>(a.counters + 2), 1u);
+    if (COUNT) {
+        __shared__ unsigned s_cnt[2];
+        if (tid < 2) s_cnt[tid] = 0;
+        __syncthreads();
+        if (n_touch) atomicAdd(&s_cnt[0], n_touch);
+        if (n_gate) atomicAdd(&s_cnt[1], n_gate);
+        __syncthreads();
+        if (tid == 0) {
+            if (s_cnt[0]) atomicAdd(a.counters + 0, (unsigned long long)s_cnt[0]);
+            if (s_cnt[1]) atomicAdd(a.counters + 1, (unsigned long long)s_cnt[1]);
+        }
+    }
+}
+
+template <bool SEM, bool GATE, bool CI32, bool VOTE>
+static hipError_t launch_integrate_t(const IntegrateArgs& a, bool count, dim3 grid, hipStream_t s) {
+    if (count)
+        hipLaunchKernelGGL((k_integrate<SEM, GATE, CI32, VOTE, true>), grid, dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_integrate<SEM, GATE, CI32, VOTE, false>), grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_integrate(const IntegrateArgs& a, hipStream_t s) {
+    const dim3 grid((a.g.dimx + BX - 1) / BX, (a.g.dimy + BY - 1) / BY, (a.g.lz + BZ - 1) / BZ);
+    const bool count = a.counters != nullptr && (a.flags & 0x80000000u);
+    const bool sem = a.flags & 0x1u, gate = a.flags & 0x2u, ci32 = a.flags & 0x4u, vote = a.flags & 0x8u;
+    // Instantiated mode combinations: SfM semantic (u8 colour, gated), TSDF+colour (NumPy
+    // rule: i32 colour, ungated), TSDF_Python vote, plus their neighbours.
+    if (vote) {
+        if (ci32) return launch_integrate_t<false, false, true, true>(a, count, grid, s);
+        return launch_integrate_t<false, false, false, true>(a, count, grid, s);
+    }
+    if (sem) {
+        if (gate) {
+            if (ci32) return launch_integrate_t<true, true, true, false>(a, count, grid, s);
+            return launch_integrate_t<true, true, false, false>(a, count, grid, s);
+        }
+        if (ci32) return launch_integrate_t<true, false, true, false>(a, count, grid, s);
+        return launch_integrate_t<true, false, false, false>(a, count, grid, s);
+    }
+    if (gate) {
+        if (ci32) return launch_integrate_t<false, true, true, false>(a, count, grid, s);
+        return launch_integrate_t<false, true, false, false>(a, count, grid, s);
+    }
+    if (ci32) return launch_integrate_t<false, false, true, false>(a, count, grid, s);
+    return launch_integrate_t<false, false, false, false>(a, count, grid, s);
+}
+
+// ------------------------------------------------------------------------------------
+// trilinear samplers (utils.cu:99-170), clamped to the volume (the reference reads out of
+// range at the far faces; the clamp defines that case).
+// ------------------------------------------------------------------------------------
+struct Tri {
+    uint64_t i000;            // flat index of the base corner
+    uint64_t dx, dy;          // strides to x+1 / y+1 (0 when clamped)
+    uint32_t dz;
+    float fx, fy, fz;
+};
+
+__device__ __forceinline__ Tri tri_setup(const VolGeom& g, float px, float py, float pz) {
+    const float ix = (px - g.start[0]) / g.voxel[0];
+    const float iy = (py - g.start[1]) / g.voxel[1];
+    const float iz = (pz - g.start[2]) / g.voxel[2];
+    const int x = f2i_rd(ix), y = f2i_rd(iy), z = f2i_rd(iz);
+    Tri t;
+    t.fx = ix - (float)x;
+    t.fy = iy - (float)y;
+    t.fz = iz - (float)z;
+    const int xc = min(max(x, 0), g.dimx - 1), yc = min(max(y, 0), g.dimy - 1), zc = min(max(z, 0), g.dimz - 1);
+    const int xn = min(max(x + 1, 0), g.dimx - 1), yn = min(max(y + 1, 0), g.dimy - 1),
+              zn = min(max(z + 1, 0), g.dimz - 1);
+    const uint64_t plane = (uint64_t)g.dimy * (uint64_t)g.lz;
+    t.i000 = (uint64_t)xc * plane + (uint64_t)yc * g.lz + (uint64_t)zc;
+    t.dx = (uint64_t)(xn - xc) * plane;
+    t.dy = (uint64_t)(yn - yc) * (uint64_t)g.lz;
+    t.dz = (uint32_t)(zn - zc);
+    return t;
+}
+
+template <typename T>
+__device__ __forceinline__ float tri_eval(const T* __restrict__ p, const Tri& t) {
+    // d[i*4+j*2+k] = vol[x+i][y+j][z+k]
+    const T* q = p + t.i000;
+    const float d0 = (float)q[0], d1 = (float)q[t.dz];
+    const float d2 = (float)q[t.dy], d3 = (float)q[t.dy + t.dz];
+    const float d4 = (float)q[t.dx], d5 = (float)q[t.dx + t.dz];
+    const float d6 = (float)q[t.dx + t.dy], d7 = (float)q[t.dx + t.dy + t.dz];
+    const float low = mixf(mixf(d0, d4, t.fx), mixf(d2, d6, t.fx), t.fy);
+    const float high = mixf(mixf(d1, d5, t.fx), mixf(d3, d7, t.fx), t.fy);
+    return mixf(low, high, t.fz);
+}
+
+__device__ __forceinline__ float sample_sdf(const VolGeom& g, const float* sdf, float px, float py, float pz) {
+    return tri_eval(sdf, tri_setup(g, px, py, pz));
+}
+
+// The shared ray march of back_proj_kernel (tsdf.cu:90-124) and show_tsdf_kernel
+// (viewer.cu:223-257).  Returns true on a hit and the refined t.
+__device__ bool march_ray(const VolGeom& g, const float* __restrict__ sdf, float ox, float oy, float oz,
+                          float dx, float dy, float dz, float* t_hit) {
+    const float idx_ = 1.0f / dx, idy = 1.0f / dy, idz = 1.0f / dz;
+    const float tbx = idx_ * (g.start[0] - ox), tby = idy * (g.start[1] - oy), tbz = idz * (g.start[2] - oz);
+    const float ttx = idx_ * (g.end[0] - ox), tty = idy * (g.end[1] - oy), ttz = idz * (g.end[2] - oz);
+    float tnear = fmaxf(fmaxf(fminf(ttx, tbx), fminf(tty, tby)), fminf(ttz, tbz));
+    tnear = fmaxf(tnear, 0.01f);
+    float tfar = fminf(fminf(fmaxf(ttx, tbx), fmaxf(tty, tby)), fmaxf(ttz, tbz));
+    tfar = fminf(tfar, 100.0f);
+    if (tnear > tfar) return false;
+    float t = tnear + 1e-6f;
+    tfar -= 1e-6f;
+    float f_tt = 0.0f;
+    const float vx = g.voxel[0];
+    float step = vx;
+    float f_t = sample_sdf(g, sdf, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
+    if (!(f_t > 0.0f)) return false;
+    for (; t < tfar; t += step) {
+        f_tt = sample_sdf(g, sdf, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
+        if (f_tt < 0.0f) break;
+        if (f_tt < vx / 2.0f) step = vx / 4.0f;
+        f_t = f_tt;
+    }
+    if (!(f_tt < 0.0f)) return false;
+    t += step * f_tt / (f_t - f_tt);
+    *t_hit = t;
+    return true;
+}
+
+__device__ __forceinline__ void ray_assoc(const MarchCamera& c, int x, int y, float* ox, float* oy, float* oz,
+                                          float* dx, float* dy, float* dz) {
+    const float fx = (float)x, fy = (float)y;
+    const float tx = dot3(c.Kinv[0], c.Kinv[1], c.Kinv[2], fx, fy, 1.0f);
+    const float ty = dot3(c.Kinv[3], c.Kinv[4], c.Kinv[5], fx, fy, 1.0f);
+    const float tz = dot3(c.Kinv[6], c.Kinv[7], c.Kinv[8], fx, fy, 1.0f);
+    const float rx = dot3(c.Rt[0], c.Rt[1], c.Rt[2], tx, ty, tz);
+    const float ry = dot3(c.Rt[3], c.Rt[4], c.Rt[5], tx, ty, tz);
+    const float rz = dot3(c.Rt[6], c.Rt[7], c.Rt[8], tx, ty, tz);
+    const float inv = 1.0f / sqrtf(dot3(rx, ry, rz, rx, ry, rz));
+    *dx = rx * inv; *dy = ry * inv; *dz = rz * inv;
+    *ox = c.o[0]; *oy = c.o[1]; *oz = c.o[2];
+}
+
+__device__ __forceinline__ void ray_render(const MarchCamera& c, int x, int y, float* ox, float* oy, float* oz,
+                                           float* dx, float* dy, float* dz) {
+    const float fx = (float)x, fy = (float)y;
+    const float tx = dot3(c.s2w[0], c.s2w[1], c.s2w[2], fx, fy, 1.0f) + c.s2w[3];
+    const float ty = dot3(c.s2w[4], c.s2w[5], c.s2w[6], fx, fy, 1.0f) + c.s2w[7];
+    const float tz = dot3(c.s2w[8], c.s2w[9], c.s2w[10], fx, fy, 1.0f) + c.s2w[11];
+    const float rx = tx - c.o[0], ry = ty - c.o[1], rz = tz - c.o[2];
+    const float inv = 1.0f / sqrtf(dot3(rx, ry, rz, rx, ry, rz));
+    *dx = rx * inv; *dy = ry * inv; *dz = rz * inv;
+    *ox = c.o[0]; *oy = c.o[1]; *oz = c.o[2];
+}
+
+// ------------------------------------------------------------------------------------
+// mask statistics: max label and first pixel of every label (for the relabel order of
+// tsdf.cu:371-389 and num_objs of tsdf.cu:463-468)
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_mask_stats(const uint8_t* __restrict__ mask, int npx, AssocTables* t) {
+    __shared__ unsigned s_first[256];
+    __shared__ unsigned s_max;
+    for (int k = threadIdx.x; k < 256; k += 256) s_first[k] = 0xFFFFFFFFu;
+    if (threadIdx.x == 0) s_max = 0;
+    __syncthreads();
+    unsigned mx = 0;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < npx; i += gridDim.x * blockDim.x) {
+        const unsigned m = mask[i];
+        mx = max(mx, m);
+        if (m) atomicMin(&s_first[m], (unsigned)i);
+    }
+    for (int off = 32; off > 0; off >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, off, 64));
+    if ((threadIdx.x & 63) == 0) atomicMax(&s_max, mx);
+    __syncthreads();
+    for (int k = threadIdx.x; k < 256; k += 256)
+        if (s_first[k] != 0xFFFFFFFFu) atomicMin(&t->first_px[k], s_first[k]);
+    if (threadIdx.x == 0) atomicMax(&t->max_label, s_max);
+}
+
+hipError_t launch_mask_stats(const uint8_t* mask, int npx, AssocTables* t, hipStream_t s) {
+    int blocks = (npx + 255) / 256;
+    if (blocks > 256) blocks = 256;
+    hipLaunchKernelGGL(k_mask_stats, dim3(blocks), dim3(256), 0, s, mask, npx, t);
+    return hipGetLastError();
+}
+
+__global__ void k_first_frame_objs(const AssocTables* t, int* num_objs) {
+    if (threadIdx.x == 0) *num_objs = (int)t->max_label + 1;
+}
+
+hipError_t launch_first_frame_objs(const AssocTables* t, int* num_objs_dev, hipStream_t s) {
+    hipLaunchKernelGGL(k_first_frame_objs, dim3(1), dim3(64), 0, s, t, num_objs_dev);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------
+// association: ray march + trilinear histogram + fused 32x32 log-likelihood accumulation
+// (back_proj_kernel tsdf.cu:72-135 feeding filter_overlaps tsdf.cu:312-334).
+//   A[m][j] = T1[m][j] + T2[j] - T3[m][j],  C[m][j] = C1[m] + C2[j] - C3[m][j]
+// is the same sum as the reference's per-pixel loops; terms are accumulated in 2^-28
+// fixed point with integer atomics, so the totals do not depend on execution order.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ long long to_fix(float L) {
+    return (long long)rint((double)L * kFixScale);
+}
+
+__global__ __launch_bounds__(256) void k_assoc_march(AssocArgs a) {
+    __shared__ long long s_t1[kMaxObjects][kMaxObjects];
+    __shared__ long long s_t3[kMaxObjects][kMaxObjects];
+    __shared__ long long s_t2[kMaxObjects];
+    __shared__ unsigned s_c1[kMaxObjects];
+    __shared__ unsigned s_c2[kMaxObjects];
+    __shared__ unsigned s_c3[kMaxObjects][kMaxObjects];
+    const int tid = threadIdx.x;
+    for (int k = tid; k < kMaxObjects * kMaxObjects; k += 256) {
+        (&s_t1[0][0])[k] = 0;
+        (&s_t3[0][0])[k] = 0;
+        (&s_c3[0][0])[k] = 0;
+    }
+    if (tid < kMaxObjects) { s_t2[tid] = 0; s_c1[tid] = 0; s_c2[tid] = 0; }
+    __syncthreads();
+
+    const int x = blockIdx.x * 16 + (tid & 15);
+    const int y = blockIdx.y * 16 + (tid >> 4);
+    if (x < a.width && y < a.height) {
+        float ox, oy, oz, dx, dy, dz, t;
+        ray_assoc(a.cam, x, y, &ox, &oy, &oz, &dx, &dy, &dz);
+        float p[kMaxObjects];
+#pragma unroll
+        for (int k = 0; k < kMaxObjects; ++k) p[k] = 0.0f;
+        if (march_ray(a.g, a.b.sdf, ox, oy, oz, dx, dy, dz, &t)) {
+            const Tri tr = tri_setup(a.g, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
+#pragma unroll
+            for (int k = 0; k < kMaxObjects; ++k) p[k] = tri_eval(a.b.hist + (uint64_t)k * a.g.nvox, tr);
+        }
+        const int px = y * a.width + x;
+        if (a.probs_out) {
+#pragma unroll
+            for (int k = 0; k < kMaxObjects; ++k) {
+                a.probs_out[(size_t)px * kMaxObjects + k] = p[k];
+                a.box_out[(size_t)px * kMaxObjects + k] = p[k] > a.box_thresh ? 1 : 0;
+            }
+        }
+        const unsigned m = a.mask[px];
+        if (m > 0 && m < (unsigned)kMaxObjects) {
+            atomicAdd(&s_c1[m], 1u);
+#pragma unroll
+            for (int j = 1; j < kMaxObjects; ++j) {
+                const float L = logf(fmaxf(p[j] / a.n_obs, a.eps));
+                atomicAdd(reinterpret_cast<unsigned long long*>(&s_t1[m][j]), (unsigned long long)to_fix(L));
+            }
+        }
+#pragma unroll
+        for (int n = 1; n < kMaxObjects; ++n) {
+            if (p[n] > a.box_thresh) {
+                const float L = logf(fmaxf(1.0f - p[n] / a.n_obs, a.eps));
+                const unsigned long long f = (unsigned long long)to_fix(L);
+                atomicAdd(reinterpret_cast<unsigned long long*>(&s_t2[n]), f);
+                atomicAdd(&s_c2[n], 1u);
+                if (m > 0 && m < (unsigned)kMaxObjects) {
+                    atomicAdd(reinterpret_cast<unsigned long long*>(&s_t3[m][n]), f);
+                    atomicAdd(&s_c3[m][n], 1u);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    AssocTables* T = a.tables;
+    for (int k = tid; k < kMaxObjects * kMaxObjects; k += 256) {
+        const long long v1 = (&s_t1[0][0])[k];
+        if (v1) atomicAdd(reinterpret_cast<unsigned long long*>(&T->t1[0][0]) + k, (unsigned long long)v1);
+        const long long v3 = (&s_t3[0][0])[k];
+        if (v3) atomicAdd(reinterpret_cast<unsigned long long*>(&T->t3[0][0]) + k, (unsigned long long)v3);
+        const unsigned c3 = (&s_c3[0][0])[k];
+        if (c3) atomicAdd(&T->c3[0][0] + k, c3);
+    }
+    if (tid < kMaxObjects) {
+        if (s_t2[tid]) atomicAdd(reinterpret_cast<unsigned long long*>(&T->t2[tid]), (unsigned long long)s_t2[tid]);
+        if (s_c1[tid]) atomicAdd(&T->c1[tid], s_c1[tid]);
+        if (s_c2[tid]) atomicAdd(&T->c2[tid], s_c2[tid]);
+    }
+}
+
+hipError_t launch_assoc_march(const AssocArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_assoc_march, dim3((a.width + 15) / 16, (a.height + 15) / 16), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// Decision (tsdf.cu:337-389), one wave: per-(i,j) probabilities in parallel, the greedy
+// one-to-one assignment and the new-id order sequentially in lane 0.
+__global__ __launch_bounds__(64) void k_assoc_decide(const AssocTables* __restrict__ T, AssocDecision* D,
+                                                     int* num_objs_dev, float eps) {
+    __shared__ double s_prob[kMaxObjects][kMaxObjects];
+    const int max_now = (int)T->max_label + 1;
+    for (int k = threadIdx.x; k < kMaxObjects * kMaxObjects; k += 64) {
+        const int i = k / kMaxObjects, j = k % kMaxObjects;
+        double prob = 0.0;
+        if (i >= 1 && j >= 1 && i < max_now && i < kMaxObjects) {
+            const long long A = T->t1[i][j] + T->t2[j] - T->t3[i][j];
+            const long long C = (long long)T->c1[i] + (long long)T->c2[j] - (long long)T->c3[i][j];
+            if (C != 0) prob = exp(((double)A / kFixScale) / (double)C);
+        }
+        s_prob[i][j] = prob;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    const float thr = 3.0f * eps;
+    int map_i[kMaxObjects];
+    double map_p[kMaxObjects];
+    for (int j = 0; j < kMaxObjects; ++j) { map_i[j] = -1; map_p[j] = 0.0; }
+    D->max_obj_now = max_now;
+    for (int i = 0; i < kMaxObjects; ++i) { D->assigned_prev[i] = -1; D->assigned_prob[i] = 0.0f; }
+    for (int i = 1; i < max_now && i < kMaxObjects; ++i) {
+        int max_j = -1;
+        double max_p = 0.0;
+        for (int j = 1; j < kMaxObjects; ++j) {
+            if (s_prob[i][j] > max_p) { max_j = j; max_p = s_prob[i][j]; }
+        }
+        if (max_p > (double)thr) {
+            if (map_i[max_j] < 0 || map_p[max_j] < max_p) { map_i[max_j] = i; map_p[max_j] = max_p; }
+        }
+    }
+    int rev[256];
+    for (int v = 0; v < 256; ++v) rev[v] = -1;
+    for (int j = 0; j < kMaxObjects; ++j) {
+        if (map_i[j] >= 0) {
+            rev[map_i[j]] = j;
+            D->assigned_prev[map_i[j]] = j;
+            D->assigned_prob[map_i[j]] = (float)map_p[j];
+        }
+    }
+    int num = *num_objs_dev;
+    D->num_objs_before = num;
+    // unmatched labels get new ids in order of their first pixel (tsdf.cu:378-387)
+    bool done[256];
+    for (int v = 0; v < 256; ++v) { done[v] = false; D->lut[v] = (unsigned char)v; }
+    for (int v = 1; v < 256; ++v) if (rev[v] >= 0) { D->lut[v] = (unsigned char)rev[v]; done[v] = true; }
+    for (;;) {
+        unsigned best = 0xFFFFFFFFu;
+        int bv = -1;
+        for (int v = 1; v < 256; ++v) {
+            if (!done[v] && T->first_px[v] < best) { best = T->first_px[v]; bv = v; }
+        }
+        if (bv < 0) break;
+        done[bv] = true;
+        D->lut[bv] = (unsigned char)num;
+        ++num;
+    }
+    D->num_objs_after = num;
+    D->bad_label = (num > kMaxObjects || max_now > kMaxObjects) ? 1 : 0;
+    *num_objs_dev = num;
+}
+
+hipError_t launch_assoc_decide(const AssocTables* t, AssocDecision* d, int num_objs, float eps,
+                               int* num_objs_dev, hipStream_t s) {
+    (void)num_objs;
+    hipLaunchKernelGGL(k_assoc_decide, dim3(1), dim3(64), 0, s, t, d, num_objs_dev, eps);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_relabel(uint8_t* __restrict__ mask, int npx, const AssocDecision* __restrict__ d) {
+    __shared__ unsigned char s_lut[256];
+    s_lut[threadIdx.x] = d->lut[threadIdx.x];
+    __syncthreads();
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < npx; i += gridDim.x * blockDim.x) mask[i] = s_lut[mask[i]];
+}
+
+hipError_t launch_relabel(uint8_t* mask, int npx, const AssocDecision* d, hipStream_t s) {
+    int blocks = (npx + 255) / 256;
+    if (blocks > 512) blocks = 512;
+    hipLaunchKernelGGL(k_relabel, dim3(blocks), dim3(256), 0, s, mask, npx, d);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------
+// render raycast (show_tsdf_kernel viewer.cu:17-86; colour mode tsdf_render.frag:125-131)
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_render(RenderArgs a) {
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15);
+    const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= a.width || y >= a.height) return;
+    const int px = y * a.width + x;
+    float ox, oy, oz, dx, dy, dz, t;
+    ray_render(a.cam, x, y, &ox, &oy, &oz, &dx, &dy, &dz);
+    uint8_t b = 0, gch = 0, r = 0;
+    float th = -1.0f;
+    if (march_ray(a.g, a.b.sdf, ox, oy, oz, dx, dy, dz, &t)) {
+        th = t;
+        const Tri tr = tri_setup(a.g, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
+        if (a.mode == 0) {
+            float max_cnt = 0.0f;
+            int obj = 0;
+            for (int k = 0; k < kMaxObjects; ++k) {
+                const float c = tri_eval(a.b.hist + (uint64_t)k * a.g.nvox, tr);
+                if (c > max_cnt) { max_cnt = c; obj = k; }
+            }
+            if (obj > 0) {
+                b = a.palette[obj * 3 + 2];
+                gch = a.palette[obj * 3 + 1];
+                r = a.palette[obj * 3 + 0];
+            }
+        } else {
+            float cc[3];
+            for (int ch = 0; ch < 3; ++ch) {
+                // colour planes are AoS [v*3 + ch]: sample with stride 3
+                const uint64_t i000 = tr.i000 * 3 + ch;
+                const uint64_t sx = tr.dx * 3, sy = tr.dy * 3, sz = (uint64_t)tr.dz * 3;
+                float d[8];
+                for (int k = 0; k < 8; ++k) {
+                    const uint64_t off = ((k & 4) ? sx : 0) + ((k & 2) ? sy : 0) + ((k & 1) ? sz : 0);
+                    d[k] = a.color_i32 ? (float)reinterpret_cast<const int32_t*>(a.b.color)[i000 + off]
+                                       : (float)reinterpret_cast<const uint8_t*>(a.b.color)[i000 + off];
+                }
+                const float low = mixf(mixf(d[0], d[4], tr.fx), mixf(d[2], d[6], tr.fx), tr.fy);
+                const float high = mixf(mixf(d[1], d[5], tr.fx), mixf(d[3], d[7], tr.fx), tr.fy);
+                cc[ch] = mixf(low, high, tr.fz);
+            }
+            b = (uint8_t)(int)cc[0];
+            gch = (uint8_t)(int)cc[1];
+            r = (uint8_t)(int)cc[2];
+        }
+    }
+    a.out_bgr[(size_t)px * 3 + 0] = b;
+    a.out_bgr[(size_t)px * 3 + 1] = gch;
+    a.out_bgr[(size_t)px * 3 + 2] = r;
+    if (a.out_t) a.out_t[px] = th;
+}
+
+hipError_t launch_render(const RenderArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_render, dim3((a.width + 15) / 16, (a.height + 15) / 16), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------
+// histogram layout conversion (bin-major device <-> voxel-major reference export)
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_hist_to_vm(const uint32_t* __restrict__ bm, uint32_t* __restrict__ vm,
+                                                    uint64_t nvox, uint64_t v0, uint64_t nv) {
+    // vm is a chunk [nv][32] for voxels v0 .. v0+nv
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv * kMaxObjects;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t v = i / kMaxObjects, k = i % kMaxObjects;
+        vm[i] = bm[k * nvox + v0 + v];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_hist_to_bm(const uint32_t* __restrict__ vm, uint32_t* __restrict__ bm,
+                                                    uint64_t nvox, uint64_t v0, uint64_t nv) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv * kMaxObjects;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = i / nv, v = i % nv;
+        bm[k * nvox + v0 + v] = vm[v * kMaxObjects + k];
+    }
+}
+
+hipError_t launch_hist_chunk_to_vm(const uint32_t* bm, uint32_t* vm, uint64_t nvox, uint64_t v0, uint64_t nv,
+                                   hipStream_t s) {
+    uint64_t blocks = (nv * kMaxObjects + 255) / 256;
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(k_hist_to_vm, dim3((unsigned)blocks), dim3(256), 0, s, bm, vm, nvox, v0, nv);
+    return hipGetLastError();
+}
+
+hipError_t launch_hist_chunk_to_bm(const uint32_t* vm, uint32_t* bm, uint64_t nvox, uint64_t v0, uint64_t nv,
+                                   hipStream_t s) {
+    uint64_t blocks = (nv * kMaxObjects + 255) / 256;
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(k_hist_to_bm, dim3((unsigned)blocks), dim3(256), 0, s, vm, bm, nvox, v0, nv);
+    return hipGetLastError();
+}
+
+}  // namespace semtsdf

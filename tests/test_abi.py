@@ -1,0 +1,40 @@
+"""The C-ABI library loads and exports every symbol include/semtsdf.h declares (no GPU
+compute is called here)."""
+import os
+import re
+
+from conftest import ROOT
+
+
+def declared():
+    with open(os.path.join(ROOT, "include", "semtsdf.h")) as f:
+        txt = f.read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(semtsdf_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_header_and_binding_agree():
+    from semtsdf import _lib as L
+
+    names = declared()
+    assert len(names) >= 30
+    assert set(names) == set(L.SIGNATURES), set(names) ^ set(L.SIGNATURES)
+
+
+def test_library_exports_every_symbol():
+    from semtsdf import _lib as L
+
+    lib = L.load()
+    for n in declared():
+        assert hasattr(lib, n), n
+    assert lib.semtsdf_abi_version() == 1
+
+
+def test_structs_match_header_sizes():
+    import ctypes as C
+
+    from semtsdf import _lib as L
+
+    # semtsdf_params: 3 i32 + 13 f32 + 32 f32 + 2 i32 + 5 f32 + u32 + 3 i32
+    assert C.sizeof(L.Params) == 4 * (3 + 9 + 1 + 32 + 2 + 5 + 1 + 3)
+    assert C.sizeof(L.AssocStats) == 4 * (2 + 32 + 32) + 256
