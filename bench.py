@@ -140,6 +140,7 @@ def main():
     ap.add_argument("--z-chunk", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true")
+    ap.add_argument("--no-cull", action="store_true", help="debug: disable brick culling")
     ap.add_argument("--cpu-planes", type=int, default=64)
     ap.add_argument("--cpu-slabs", type=int, default=3)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
@@ -164,7 +165,7 @@ def main():
     p = semtsdf.default_params(D, KI, W, H)
     p.dim[2] = D * world
     semtsdf.place_from_frame(p, f0.depth, float(np.mean(f0.depth[f0.depth > 0])) / 5000.0, L.PLACE_SFM)
-    p.flags = L.F_SEMANTIC | L.F_GATE_COLOR
+    p.flags = L.F_SEMANTIC | L.F_GATE_COLOR | (L.F_NO_CULL if args.no_cull else 0)
     if world > 1:
         p.z_nshards = world
         p.z_shard = rank
@@ -209,6 +210,7 @@ def main():
     tm = vol.timing()
     vol.set_instrumentation(events=False, count=False)
     kern_ms = tm.integrate_ms / max(tm.n_integrate, 1)
+    prep_ms = tm.prep_ms / max(tm.n_prep, 1)
 
     # algorithmic bytes of the same launches (counts are a function of the frame only)
     vol.reset_timing()
@@ -219,6 +221,7 @@ def main():
     vol.set_instrumentation(events=False, count=False)
     touched = tc.touched / args.steps
     gated = tc.gated / args.steps
+    bricks = tc.bricks / args.steps
     bytes_per_launch = 16.0 * touched + 14.0 * gated + 6.0 * npx
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
 
@@ -303,8 +306,10 @@ def main():
             },
             "frames_per_s": round(args.steps / elapsed, 2),
             "integrate_kernel_ms": round(kern_ms, 4),
+            "prep_ms": round(prep_ms, 4),
             "touched_per_frame": int(touched),
             "gated_per_frame": int(gated),
+            "live_bricks_per_frame": int(bricks),
             "touched_mvox_per_s": round(touched / (kern_ms * 1e-3) / 1e6, 1),
             "roofline": {
                 "bound": "hbm",

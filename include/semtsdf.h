@@ -104,6 +104,9 @@ typedef struct semtsdf_timing {
     uint64_t n_integrate, n_assoc, n_render;
     uint64_t touched;     /* voxels updated (count mode only) */
     uint64_t gated;       /* voxels whose colour/histogram were updated (count mode only) */
+    uint64_t bricks;      /* 8x8x32 bricks that survived the frustum/depth cull (count mode only) */
+    double prep_ms;       /* sum over the per-frame depth-pyramid + brick-cull passes */
+    uint64_t n_prep;
 } semtsdf_timing;
 
 /* ---- library ------------------------------------------------------------------------ */

@@ -8,12 +8,13 @@
 // a thread-local message (the reference checks only cudaGetLastError and throws
 // std::string); all device work is stream-ordered and asynchronous; association runs on
 // the device (no 49 MB probs/box_mask D2H, tsdf.cu:457-458); 64-bit voxel indexing.
-#include <hip/hip_runtime_api.h>
+#include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -84,13 +85,14 @@ struct semtsdf_vol {
     uint8_t* render_d = nullptr;
     float* render_t_d = nullptr;
     unsigned long long* counters_d = nullptr;
+    uint8_t* unit_flags_d = nullptr;
     AssocDecision* decision_h = nullptr;  // pinned
     uint32_t n_obs = 0;
     // instrumentation
     int instr = 0;
-    std::vector<EventPair> ev_integrate, ev_assoc, ev_render;
-    double t_integrate = 0, t_assoc = 0, t_render = 0;
-    uint64_t n_integrate = 0, n_assoc = 0, n_render = 0;
+    std::vector<EventPair> ev_integrate, ev_assoc, ev_render, ev_prep;
+    double t_integrate = 0, t_assoc = 0, t_render = 0, t_prep = 0;
+    uint64_t n_integrate = 0, n_assoc = 0, n_render = 0, n_prep = 0;
 };
 
 namespace {
@@ -111,13 +113,13 @@ int dev_alloc(semtsdf_vol* v, void** p, size_t bytes) {
 
 void free_all(semtsdf_vol* v) {
     void* ptrs[] = {v->b.sdf, v->b.wt, v->b.color, v->b.hist, v->b.cls, v->b.cls_cnt, v->depth_d, v->rgb_d,
-                    v->mask_d, v->cls_d, v->pyr.l0, v->pyr.l1, v->pyr.l2, v->tables_d, v->decision_d,
+                    v->mask_d, v->cls_d, v->pyr.metres, v->pyr.rgbl, v->pyr.l0, v->pyr.l1, v->pyr.l2, v->tables_d, v->decision_d,
                     v->num_objs_d, v->probs_d, v->box_d, v->palette_d, v->render_d, v->render_t_d,
-                    v->counters_d};
+                    v->counters_d, v->unit_flags_d};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (v->decision_h) (void)hipHostFree(v->decision_h);
-    for (auto* vec : {&v->ev_integrate, &v->ev_assoc, &v->ev_render})
+    for (auto* vec : {&v->ev_integrate, &v->ev_assoc, &v->ev_render, &v->ev_prep})
         for (auto& e : *vec) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
     if (v->stream) (void)hipStreamDestroy(v->stream);
 }
@@ -192,13 +194,26 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
     a.gate = v->p.gate;
     a.flags = v->p.flags | ((v->instr & 2) ? 0x80000000u : 0u);
     a.cull = (v->p.flags & SEMTSDF_F_NO_CULL) ? 0 : 1;
+    {
+        static const char* dbg = getenv("SEMTSDF_DEBUG_INTEGRATE");  // timing probes only
+        a.debug = dbg ? atoi(dbg) : 0;
+    }
     a.depth = depth_d;
     a.rgb = rgb_d;
     a.mask = mask_d;
     a.cls = cls_d;
     a.pyr = v->pyr;
     a.counters = v->counters_d;
-    if (a.cull) HIPC(launch_depth_pyramid(depth_d, v->p.width, v->p.height, v->pyr, s));
+    a.unit_flags = v->unit_flags_d;
+    a.pinhole = (a.K[1] == 0.0f && a.K[3] == 0.0f && a.K[6] == 0.0f && a.K[7] == 0.0f && a.K[8] == 1.0f) ? 1 : 0;
+    if (a.debug == 2) return SEMTSDF_OK;
+    EventPair epp;
+    timing_begin(v, v->ev_prep, s, &epp);
+    HIPC(launch_depth_pyramid(depth_d, rgb_d, mask_d, v->p.width, v->p.height, v->p.depth_scale, v->pyr, s));
+    HIPC(launch_cull(a, s));
+    timing_end(v, v->ev_prep, s, &epp);
+    v->n_prep++;
+    if (a.debug == 1) return SEMTSDF_OK;
     EventPair ep;  // events bracket the integrate kernel alone (the roofline kernel)
     timing_begin(v, v->ev_integrate, s, &ep);
     HIPC(launch_integrate(a, s));
@@ -459,10 +474,11 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     VolGeom& g = v->g;
     g.dimx = p->dim[0]; g.dimy = p->dim[1]; g.dimz = p->dim[2];
     g.lz = lz;
+    g.zs = (lz + 3) & ~3;
     g.shard = p->z_shard; g.nshards = p->z_nshards; g.chunk = chunk; g.halo = halo;
     for (int i = 0; i < 3; ++i) { g.start[i] = p->vol_start[i]; g.end[i] = p->vol_end[i]; g.voxel[i] = p->voxel[i]; }
     g.mu = p->mu;
-    g.nvox = (uint64_t)g.dimx * (uint64_t)g.dimy * (uint64_t)lz;
+    g.nvox = (uint64_t)g.dimx * (uint64_t)g.dimy * (uint64_t)g.zs;
     const size_t n = g.nvox;
     const size_t px = (size_t)p->width * p->height;
     auto bail = [&](int code) { free_all(v); delete v; return code; };
@@ -471,7 +487,7 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     const bool ci32 = p->flags & SEMTSDF_F_COLOR_I32;
     if ((rc = dev_alloc(v, (void**)&v->b.sdf, n * 4))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->b.wt, n * 4))) return bail(rc);
-    if ((rc = dev_alloc(v, &v->b.color, n * 3 * (ci32 ? 4 : 1)))) return bail(rc);
+    if ((rc = dev_alloc(v, &v->b.color, n * 4 * (ci32 ? 4 : 1)))) return bail(rc);
     if (p->flags & SEMTSDF_F_SEMANTIC)
         if ((rc = dev_alloc(v, (void**)&v->b.hist, n * kMaxObjects * 4))) return bail(rc);
     if (p->flags & SEMTSDF_F_VOTE) {
@@ -486,6 +502,8 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     pyr.w0 = (p->width + 7) / 8; pyr.h0 = (p->height + 7) / 8;
     pyr.w1 = (p->width + 31) / 32; pyr.h1 = (p->height + 31) / 32;
     pyr.w2 = (p->width + 127) / 128; pyr.h2 = (p->height + 127) / 128;
+    if ((rc = dev_alloc(v, (void**)&pyr.metres, px * 4))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&pyr.rgbl, px * 4))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&pyr.l0, (size_t)pyr.w1 * 4 * pyr.h1 * 4 * 2))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&pyr.l1, (size_t)pyr.w1 * pyr.h1 * 2))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&pyr.l2, (size_t)pyr.w2 * pyr.h2 * 4))) return bail(rc);
@@ -493,6 +511,7 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     if ((rc = dev_alloc(v, (void**)&v->decision_d, sizeof(AssocDecision)))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->num_objs_d, 16))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->counters_d, 4 * sizeof(unsigned long long)))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&v->unit_flags_d, brick_count_max(g)))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->palette_d, sizeof(kPalette)))) return bail(rc);
     if (hipHostMalloc((void**)&v->decision_h, sizeof(AssocDecision), 0) != hipSuccess)
         return bail(fail(SEMTSDF_ERR_HIP, "hipHostMalloc failed"));
@@ -529,7 +548,7 @@ int semtsdf_get_state(const semtsdf_vol* v, semtsdf_state* out) {
     out->local_dim[0] = v->g.dimx;
     out->local_dim[1] = v->g.dimy;
     out->local_dim[2] = v->g.lz;
-    out->local_voxels = v->g.nvox;
+    out->local_voxels = (uint64_t)v->g.dimx * v->g.dimy * v->g.lz;
     out->device_bytes = v->device_bytes;
     return SEMTSDF_OK;
 }
@@ -551,7 +570,7 @@ int semtsdf_reset(semtsdf_vol* v, void* stream) {
     const size_t n = v->g.nvox;
     HIPC(launch_fill_volume(v->g, v->b, v->p.flags, s));
     HIPC(hipMemsetAsync(v->b.wt, 0, n * 4, s));
-    HIPC(hipMemsetAsync(v->b.color, 0, n * 3 * ((v->p.flags & SEMTSDF_F_COLOR_I32) ? 4 : 1), s));
+    HIPC(hipMemsetAsync(v->b.color, 0, n * 4 * ((v->p.flags & SEMTSDF_F_COLOR_I32) ? 4 : 1), s));
     if (v->b.hist) HIPC(hipMemsetAsync(v->b.hist, 0, n * kMaxObjects * 4, s));
     if (v->b.cls) HIPC(hipMemsetAsync(v->b.cls, 0, n * 4, s));
     if (v->b.cls_cnt) HIPC(hipMemsetAsync(v->b.cls_cnt, 0, n * 4, s));
@@ -805,34 +824,76 @@ int semtsdf_raycast_dev(semtsdf_vol* v, const float s2w[16], const float c[3], i
     return raycast_impl(v, s2w, c, mode, out_bgr_d, out_t_d, pick(v, stream));
 }
 
+// Copy a per-voxel array between the reference layout (rows of lz planes, dense) and the
+// device storage (rows padded to zs planes).  eb = bytes per voxel.
+static hipError_t copy_rows(const semtsdf_vol* v, void* dst, const void* src, size_t eb, bool to_host, hipStream_t s) {
+    const size_t rows = (size_t)v->g.dimx * v->g.dimy;
+    const size_t w = (size_t)v->g.lz * eb, pitch_dev = (size_t)v->g.zs * eb;
+    if (v->g.lz == v->g.zs)
+        return hipMemcpyAsync(dst, src, rows * w, to_host ? hipMemcpyDeviceToHost : hipMemcpyHostToDevice, s);
+    if (to_host) return hipMemcpy2DAsync(dst, w, src, pitch_dev, w, rows, hipMemcpyDeviceToHost, s);
+    return hipMemcpy2DAsync(dst, pitch_dev, src, w, w, rows, hipMemcpyHostToDevice, s);
+}
+
+// colour between the padded device layout and the reference [N][3] layout, chunked
+static int color_xfer(semtsdf_vol* v, void* host, bool to_host, hipStream_t s) {
+    const bool i32 = v->p.flags & SEMTSDF_F_COLOR_I32;
+    const size_t es = i32 ? 4 : 1;
+    const uint64_t n = (uint64_t)v->g.dimx * v->g.dimy * v->g.lz;
+    const uint64_t chunk = std::min<uint64_t>(n, 1ull << 24);
+    void* stage = nullptr;
+    HIPC(hipMalloc(&stage, chunk * 3 * es));
+    for (uint64_t v0 = 0; v0 < n; v0 += chunk) {
+        const uint64_t nv = std::min<uint64_t>(chunk, n - v0);
+        char* h = static_cast<char*>(host) + v0 * 3 * es;
+        hipError_t e;
+        if (to_host) {
+            e = launch_color_chunk(v->b.color, stage, true, i32, v->g, v0, nv, s);
+            if (e == hipSuccess) e = hipMemcpyAsync(h, stage, nv * 3 * es, hipMemcpyDeviceToHost, s);
+        } else {
+            e = hipMemcpyAsync(stage, h, nv * 3 * es, hipMemcpyHostToDevice, s);
+            if (e == hipSuccess) e = launch_color_chunk(stage, v->b.color, false, i32, v->g, v0, nv, s);
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) {
+            (void)hipFree(stage);
+            return fail(SEMTSDF_ERR_HIP, "colour transfer: %s", hipGetErrorString(e));
+        }
+    }
+    HIPC(hipFree(stage));
+    return SEMTSDF_OK;
+}
+
 int semtsdf_download(semtsdf_vol* v, float* sdf, int32_t* wt, void* color, uint32_t* hist, int32_t* cls,
                      int32_t* cls_cnt) {
     if (!v) return fail(SEMTSDF_ERR_INVALID, "NULL handle");
     HIPC(hipSetDevice(v->device));
     hipStream_t s = v->stream;
-    const size_t n = v->g.nvox;
-    if (sdf) HIPC(hipMemcpyAsync(sdf, v->b.sdf, n * 4, hipMemcpyDeviceToHost, s));
-    if (wt) HIPC(hipMemcpyAsync(wt, v->b.wt, n * 4, hipMemcpyDeviceToHost, s));
-    if (color)
-        HIPC(hipMemcpyAsync(color, v->b.color, n * 3 * ((v->p.flags & SEMTSDF_F_COLOR_I32) ? 4 : 1),
-                            hipMemcpyDeviceToHost, s));
+    if (sdf) HIPC(copy_rows(v, sdf, v->b.sdf, 4, true, s));
+    if (wt) HIPC(copy_rows(v, wt, v->b.wt, 4, true, s));
+    if (color) {
+        int rc = color_xfer(v, color, true, s);
+        if (rc) return rc;
+    }
     if (cls) {
         if (!v->b.cls) return fail(SEMTSDF_ERR_STATE, "not a VOTE volume");
-        HIPC(hipMemcpyAsync(cls, v->b.cls, n * 4, hipMemcpyDeviceToHost, s));
+        HIPC(copy_rows(v, cls, v->b.cls, 4, true, s));
     }
     if (cls_cnt) {
         if (!v->b.cls_cnt) return fail(SEMTSDF_ERR_STATE, "not a VOTE volume");
-        HIPC(hipMemcpyAsync(cls_cnt, v->b.cls_cnt, n * 4, hipMemcpyDeviceToHost, s));
+        HIPC(copy_rows(v, cls_cnt, v->b.cls_cnt, 4, true, s));
     }
     if (hist) {
         if (!v->b.hist) return fail(SEMTSDF_ERR_STATE, "not a SEMANTIC volume");
+        const uint64_t n = (uint64_t)v->g.dimx * v->g.dimy * v->g.lz;
         const uint64_t chunk = std::min<uint64_t>(n, 1ull << 22);  // 4M voxels = 512 MiB staging
         uint32_t* stage = nullptr;
         HIPC(hipMalloc(&stage, chunk * kMaxObjects * 4));
         for (uint64_t v0 = 0; v0 < n; v0 += chunk) {
             const uint64_t nv = std::min<uint64_t>(chunk, n - v0);
-            hipError_t e = launch_hist_chunk_to_vm(v->b.hist, stage, n, v0, nv, s);
-            if (e == hipSuccess) e = hipMemcpyAsync(hist + v0 * kMaxObjects, stage, nv * kMaxObjects * 4, hipMemcpyDeviceToHost, s);
+            hipError_t e = launch_hist_chunk_to_vm(v->b.hist, stage, v->g, v0, nv, s);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(hist + v0 * kMaxObjects, stage, nv * kMaxObjects * 4, hipMemcpyDeviceToHost, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e != hipSuccess) {
                 (void)hipFree(stage);
@@ -850,29 +911,31 @@ int semtsdf_upload(semtsdf_vol* v, const float* sdf, const int32_t* wt, const vo
     if (!v) return fail(SEMTSDF_ERR_INVALID, "NULL handle");
     HIPC(hipSetDevice(v->device));
     hipStream_t s = v->stream;
-    const size_t n = v->g.nvox;
-    if (sdf) HIPC(hipMemcpyAsync(v->b.sdf, sdf, n * 4, hipMemcpyHostToDevice, s));
-    if (wt) HIPC(hipMemcpyAsync(v->b.wt, wt, n * 4, hipMemcpyHostToDevice, s));
-    if (color)
-        HIPC(hipMemcpyAsync(v->b.color, color, n * 3 * ((v->p.flags & SEMTSDF_F_COLOR_I32) ? 4 : 1),
-                            hipMemcpyHostToDevice, s));
+    if (sdf) HIPC(copy_rows(v, v->b.sdf, sdf, 4, false, s));
+    if (wt) HIPC(copy_rows(v, v->b.wt, wt, 4, false, s));
+    if (color) {
+        int rc = color_xfer(v, const_cast<void*>(color), false, s);
+        if (rc) return rc;
+    }
     if (cls) {
         if (!v->b.cls) return fail(SEMTSDF_ERR_STATE, "not a VOTE volume");
-        HIPC(hipMemcpyAsync(v->b.cls, cls, n * 4, hipMemcpyHostToDevice, s));
+        HIPC(copy_rows(v, v->b.cls, cls, 4, false, s));
     }
     if (cls_cnt) {
         if (!v->b.cls_cnt) return fail(SEMTSDF_ERR_STATE, "not a VOTE volume");
-        HIPC(hipMemcpyAsync(v->b.cls_cnt, cls_cnt, n * 4, hipMemcpyHostToDevice, s));
+        HIPC(copy_rows(v, v->b.cls_cnt, cls_cnt, 4, false, s));
     }
     if (hist) {
         if (!v->b.hist) return fail(SEMTSDF_ERR_STATE, "not a SEMANTIC volume");
+        const uint64_t n = (uint64_t)v->g.dimx * v->g.dimy * v->g.lz;
         const uint64_t chunk = std::min<uint64_t>(n, 1ull << 22);
         uint32_t* stage = nullptr;
         HIPC(hipMalloc(&stage, chunk * kMaxObjects * 4));
         for (uint64_t v0 = 0; v0 < n; v0 += chunk) {
             const uint64_t nv = std::min<uint64_t>(chunk, n - v0);
-            hipError_t e = hipMemcpyAsync(stage, hist + v0 * kMaxObjects, nv * kMaxObjects * 4, hipMemcpyHostToDevice, s);
-            if (e == hipSuccess) e = launch_hist_chunk_to_bm(stage, v->b.hist, n, v0, nv, s);
+            hipError_t e =
+                hipMemcpyAsync(stage, hist + v0 * kMaxObjects, nv * kMaxObjects * 4, hipMemcpyHostToDevice, s);
+            if (e == hipSuccess) e = launch_hist_chunk_to_bm(stage, v->b.hist, v->g, v0, nv, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e != hipSuccess) {
                 (void)hipFree(stage);
@@ -911,7 +974,8 @@ int semtsdf_get_timing(semtsdf_vol* v, semtsdf_timing* out) {
     v->t_integrate += drain(v->ev_integrate);
     v->t_assoc += drain(v->ev_assoc);
     v->t_render += drain(v->ev_render);
-    unsigned long long c[3] = {0, 0, 0};
+    v->t_prep += drain(v->ev_prep);
+    unsigned long long c[4] = {0, 0, 0, 0};
     HIPC(hipMemcpy(c, v->counters_d, sizeof(c), hipMemcpyDeviceToHost));
     out->integrate_ms = v->t_integrate;
     out->assoc_ms = v->t_assoc;
@@ -921,6 +985,9 @@ int semtsdf_get_timing(semtsdf_vol* v, semtsdf_timing* out) {
     out->n_render = v->n_render;
     out->touched = c[0];
     out->gated = c[1];
+    out->bricks = c[3];
+    out->prep_ms = v->t_prep;
+    out->n_prep = v->n_prep;
     return SEMTSDF_OK;
 }
 
@@ -931,9 +998,11 @@ int semtsdf_reset_timing(semtsdf_vol* v) {
     drain(v->ev_integrate);
     drain(v->ev_assoc);
     drain(v->ev_render);
-    v->t_integrate = v->t_assoc = v->t_render = 0;
-    v->n_integrate = v->n_assoc = v->n_render = 0;
+    drain(v->ev_prep);
+    v->t_integrate = v->t_assoc = v->t_render = v->t_prep = 0;
+    v->n_integrate = v->n_assoc = v->n_render = v->n_prep = 0;
     HIPC(hipMemset(v->counters_d, 0, 2 * sizeof(unsigned long long)));
+    HIPC(hipMemset(v->counters_d + 3, 0, sizeof(unsigned long long)));
     return SEMTSDF_OK;
 }
 

@@ -13,19 +13,20 @@ constexpr int kMaxObjects = 32;
 struct VolGeom {
     int dimx, dimy, dimz;      // global dims
     int lz;                    // local z planes (chunks * (chunk + halo))
+    int zs;                    // row stride in voxels: lz rounded up to a multiple of 4 (16-B rows)
     int shard, nshards, chunk, halo;
     float start[3];            // vol_start
     float end[3];              // vol_end
     float voxel[3];
     float mu;
-    uint64_t nvox;             // dimx * dimy * lz (local voxels)
+    uint64_t nvox;             // dimx * dimy * zs (stored voxels, padding planes included)
 };
 
 // Device buffers of one volume.
 struct VolBufs {
     float* sdf;
     int32_t* wt;
-    void* color;       // u8x3 or i32x3, AoS
+    void* color;       // u8x4 or i32x4 per voxel (3 channels + pad, 16-B vectors of 4 voxels)
     uint32_t* hist;    // bin-major [32][nvox]
     int32_t* cls;      // vote mode
     int32_t* cls_cnt;  // vote mode
@@ -34,6 +35,8 @@ struct VolBufs {
 // Per-frame depth pyramid used by the brick culler: max raw depth over tiles of
 // 8, 32 and 128 pixels.
 struct DepthPyramid {
+    float* metres;  // [H][W] depth / depth_scale (IEEE division, tsdf.cu:49), 0 where invalid
+    uint32_t* rgbl; // [H][W] r | g << 8 | b << 16 | label << 24 (one dword gather per gated voxel)
     uint16_t* l0;  // [ceil(H/8)][ceil(W/8)]
     uint16_t* l1;  // [ceil(H/32)][ceil(W/32)]
     uint32_t* l2;  // [ceil(H/128)][ceil(W/128)] (u32 for atomicMax)
@@ -50,12 +53,15 @@ struct IntegrateArgs {
     float gate;
     uint32_t flags;
     int cull;
+    int debug;       // 0 normal; 1 return after the cull; 2 return at entry (timing probes)
     const uint16_t* depth;
     const uint8_t* rgb;
     const uint8_t* mask;    // semantic
     const int32_t* cls;     // vote
     DepthPyramid pyr;
-    unsigned long long* counters;  // [0] touched, [1] gated, [2] bad-label flag
+    unsigned long long* counters;  // [0] touched, [1] gated, [2] bad-label flag, [3] live bricks
+    uint8_t* unit_flags;           // per cull unit: 1 = may hold a touched voxel (cull pass output)
+    int pinhole;                   // K rows are (fx 0 cx; 0 fy cy; 0 0 1)
 };
 
 // Association accumulators (fixed point, scale 2^28, deterministic).
@@ -120,8 +126,13 @@ struct RenderArgs {
 
 // ---- launchers (semtsdf_kernels.hip) ----
 hipError_t launch_fill_volume(const VolGeom& g, const VolBufs& b, uint32_t flags, hipStream_t s);
-hipError_t launch_depth_pyramid(const uint16_t* depth, int w, int h, const DepthPyramid& p, hipStream_t s);
-hipError_t launch_integrate(const IntegrateArgs& a, hipStream_t s);
+hipError_t launch_depth_pyramid(const uint16_t* depth, const uint8_t* rgb, const uint8_t* mask, int w, int h,
+                                float scale, const DepthPyramid& p, hipStream_t s);
+hipError_t launch_color_chunk(const void* src, void* dst, bool to_ref, bool i32, const VolGeom& g, uint64_t v0,
+                              uint64_t nv, hipStream_t s);
+hipError_t launch_cull(const IntegrateArgs& a, hipStream_t s);      // pass 1: live-brick list
+hipError_t launch_integrate(const IntegrateArgs& a, hipStream_t s); // pass 2: persistent integrate
+uint64_t brick_count_max(const VolGeom& g);
 hipError_t launch_mask_stats(const uint8_t* mask, int npx, AssocTables* t, hipStream_t s);
 hipError_t launch_assoc_march(const AssocArgs& a, hipStream_t s);
 hipError_t launch_assoc_decide(const AssocTables* t, AssocDecision* d, int num_objs, float eps,
@@ -130,9 +141,9 @@ hipError_t launch_first_frame_objs(const AssocTables* t, int* num_objs_dev, hipS
 hipError_t launch_relabel(uint8_t* mask, int npx, const AssocDecision* d, hipStream_t s);
 hipError_t launch_render(const RenderArgs& a, hipStream_t s);
 // chunk [v0, v0+nv) of the bin-major histogram <-> voxel-major [nv][32] staging buffer
-hipError_t launch_hist_chunk_to_vm(const uint32_t* bm, uint32_t* vm, uint64_t nvox, uint64_t v0, uint64_t nv,
+hipError_t launch_hist_chunk_to_vm(const uint32_t* bm, uint32_t* vm, const VolGeom& g, uint64_t v0, uint64_t nv,
                                    hipStream_t s);
-hipError_t launch_hist_chunk_to_bm(const uint32_t* vm, uint32_t* bm, uint64_t nvox, uint64_t v0, uint64_t nv,
+hipError_t launch_hist_chunk_to_bm(const uint32_t* vm, uint32_t* bm, const VolGeom& g, uint64_t v0, uint64_t nv,
                                    hipStream_t s);
 
 }  // namespace semtsdf

@@ -100,7 +100,8 @@ hipError_t launch_fill_volume(const VolGeom& g, const VolBufs& b, uint32_t flags
 // depth pyramid: max raw depth over 8/32/128-pixel tiles, for brick culling.
 // One workgroup per 32x32 pixel tile; 256 lanes x 4 pixels.
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restrict__ depth, int w, int h,
+__global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restrict__ depth, const uint8_t* __restrict__ rgb,
+                                                       const uint8_t* __restrict__ mask, int w, int h, float scale,
                                                        DepthPyramid p) {
     __shared__ unsigned s_m[32][8];
     const int tx = blockIdx.x, ty = blockIdx.y;
@@ -112,7 +113,17 @@ __global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restric
     if (yy < h) {
         for (int k = 0; k < 4; ++k) {
             const int xx = tx * 32 + c4 + k;
-            if (xx < w) m = max(m, (unsigned)depth[(size_t)yy * w + xx]);
+            if (xx < w) {
+                const unsigned d = depth[(size_t)yy * w + xx];
+                m = max(m, d);
+                const size_t px = (size_t)yy * w + xx;
+                p.metres[px] = (float)d / scale;  // depth[img] / 5000.f (tsdf.cu:49)
+                if (rgb) {
+                    const unsigned lab = mask ? (unsigned)mask[px] : 0u;
+                    p.rgbl[px] = (unsigned)rgb[px * 3] | ((unsigned)rgb[px * 3 + 1] << 8) |
+                                 ((unsigned)rgb[px * 3 + 2] << 16) | (lab << 24);
+                }
+            }
         }
     }
     s_m[r][t & 7] = m;
@@ -139,30 +150,78 @@ __global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restric
     }
 }
 
-hipError_t launch_depth_pyramid(const uint16_t* depth, int w, int h, const DepthPyramid& p, hipStream_t s) {
+hipError_t launch_depth_pyramid(const uint16_t* depth, const uint8_t* rgb, const uint8_t* mask, int w, int h,
+                                float scale, const DepthPyramid& p, hipStream_t s) {
     hipError_t e = hipMemsetAsync(p.l2, 0, (size_t)p.w2 * p.h2 * sizeof(uint32_t), s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_depth_pyramid, dim3(p.w1, p.h1), dim3(256), 0, s, depth, w, h, p);
+    hipLaunchKernelGGL(k_depth_pyramid, dim3(p.w1, p.h1), dim3(256), 0, s, depth, rgb, mask, w, h, scale, p);
     return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------
 // integrate
 // ------------------------------------------------------------------------------------
-constexpr int BX = 8, BY = 8, BZ = 32;
+// ---- work decomposition ------------------------------------------------------------
+// Cull unit = UX(x) x UY(y) x UZ(z) voxels, tested once per frame by one lane of the cull
+// pass against the frustum and the depth pyramid (a byte flag per unit, no atomics).
+// Integrate work item = one unit, handled by one wavefront: lane = (zq, y) = (lane & 7,
+// lane >> 3) owns planes 4zq..4zq+3 of row y for the UX x-planes, so every state access is
+// one 16-byte vector per lane.  Items are dealt round-robin to persistent waves, so live
+// items spread evenly over the chip and waves never synchronise with each other.
+constexpr int UX = 1, UY = 8, UZ = 32;
 
-// Conservative brick test run by one wave: returns 1 when no voxel of the brick can pass
-// the projection / depth tests of tsdf.cu:46-50 (culling never changes results).
-__device__ int brick_cull(const IntegrateArgs& a, int x0, int y0, int lz0, int lane) {
+// floor(a / b) with the IEEE quotient, through v_rcp when the result is provably the same:
+// |a*rcp(b) - RN(a/b)| < |q| 2^-20, so a q farther than |q| 2^-19 from an integer floors the
+// same way; everything else (near-integers, zeros, NaN/Inf, tiny or huge operands) takes
+// the correctly rounded division.
+__device__ __forceinline__ int floor_div(float a, float b) {
+    const float q = a * __builtin_amdgcn_rcpf(b);
+    const float fq = floorf(q);
+    const float fr = q - fq;
+    const float tol = fabsf(q) * 0x1p-19f;
+    if (fr > tol && fr < 1.0f - tol && fabsf(b) > 1.0e-30f && fabsf(q) < 8.0e6f) return (int)fq;
+    return f2i_rd(a / b);
+}
+
+// (c*w + x) / (w+1) for 0 <= c, x <= 255 via the float reciprocal plus one exact integer
+// correction (quotient <= 255, so the float estimate is within one of it); integer
+// division above w = 65535 where the numerator would leave the exact f32 range.
+__device__ __forceinline__ int avg_div(int num, int den) {
+    if (den > 65536) return num / den;
+    int q = (int)((float)num * __builtin_amdgcn_rcpf((float)den));
+    if ((q + 1) * den <= num) ++q;
+    else if (q * den > num) --q;
+    return q;
+}
+
+// Screen position of camera point q.  With a pinhole K (k1 = k3 = k6 = k7 = 0, k8 = 1) the
+// general dot products reduce exactly (fma(0, a, c) == c up to the sign of a zero, which
+// cannot change the floored pixel), saving 5 of 9 operations.
+__device__ __forceinline__ void screen(const IntegrateArgs& a, float qx, float qy, float qz, float* sx, float* sy,
+                                       float* sz) {
+    if (a.pinhole) {
+        *sx = fmaf(a.K[2], qz, a.K[0] * qx);
+        *sy = fmaf(a.K[5], qz, a.K[4] * qy);
+        *sz = qz;
+    } else {
+        *sx = dot3(a.K[0], a.K[1], a.K[2], qx, qy, qz);
+        *sy = dot3(a.K[3], a.K[4], a.K[5], qx, qy, qz);
+        *sz = dot3(a.K[6], a.K[7], a.K[8], qx, qy, qz);
+    }
+}
+
+// Conservative unit test: returns 1 when no voxel of the unit can pass the projection /
+// depth tests of tsdf.cu:46-50, so culling never changes results.
+__device__ int unit_cull(const IntegrateArgs& a, int x0, int y0, int lz0) {
     const VolGeom& g = a.g;
-    const int x1 = min(x0 + BX - 1, g.dimx - 1);
-    const int y1 = min(y0 + BY - 1, g.dimy - 1);
+    const int x1 = min(x0 + UX - 1, g.dimx - 1);
+    const int y1 = min(y0 + UY - 1, g.dimy - 1);
     const int gz0 = local_to_global_z(g, lz0);
-    int gz1 = local_to_global_z(g, min(lz0 + BZ - 1, g.lz - 1));
-    if (gz0 >= g.dimz) return 1;  // only halo planes beyond the volume
-    gz1 = min(gz1, g.dimz - 1);
+    if (gz0 >= g.dimz) return 1;  // only halo/padding planes beyond the volume
+    const int gz1 = min(local_to_global_z(g, min(lz0 + UZ - 1, g.lz - 1)), g.dimz - 1);
     float umin = 3.0e38f, umax = -3.0e38f, vmin = 3.0e38f, vmax = -3.0e38f;
     float zmin = 3.0e38f, zmax = -3.0e38f, wmin = 3.0e38f, wmax = -3.0e38f;
+#pragma unroll
     for (int c = 0; c < 8; ++c) {
         const float px = fmaf((float)((c & 1) ? x1 : x0), g.voxel[0], g.start[0]);
         const float py = fmaf((float)((c & 2) ? y1 : y0), g.voxel[1], g.start[1]);
@@ -170,9 +229,8 @@ __device__ int brick_cull(const IntegrateArgs& a, int x0, int y0, int lz0, int l
         const float qx = dot3(a.E[0], a.E[1], a.E[2], px, py, pz) + a.E[3];
         const float qy = dot3(a.E[4], a.E[5], a.E[6], px, py, pz) + a.E[7];
         const float qz = dot3(a.E[8], a.E[9], a.E[10], px, py, pz) + a.E[11];
-        const float sx = dot3(a.K[0], a.K[1], a.K[2], qx, qy, qz);
-        const float sy = dot3(a.K[3], a.K[4], a.K[5], qx, qy, qz);
-        const float sz = dot3(a.K[6], a.K[7], a.K[8], qx, qy, qz);
+        float sx, sy, sz;
+        screen(a, qx, qy, qz, &sx, &sy, &sz);
         const float u = sx / sz, v = sy / sz;
         umin = fminf(umin, u); umax = fmaxf(umax, u);
         vmin = fminf(vmin, v); vmax = fmaxf(vmax, v);
@@ -184,175 +242,360 @@ __device__ int brick_cull(const IntegrateArgs& a, int x0, int y0, int lz0, int l
     const float zeps = 1.0e-3f;
     if (!(wmin > zeps) && !(wmax < -zeps)) return 0;
     if (!(umin == umin) || !(vmin == vmin) || !(umax == umax) || !(vmax == vmax)) return 0;
-    // 1-pixel guard band around the projected hull of the brick
     const float W = (float)a.width, H = (float)a.height;
+    // 1-pixel guard band around the projected hull
     if (umax + 1.0f < 0.0f || umin - 1.0f > W || vmax + 1.0f < 0.0f || vmin - 1.0f > H) return 1;
-    int u0 = (int)fmaxf(floorf(umin) - 1.0f, 0.0f);
-    int u1 = (int)fminf(floorf(umax) + 1.0f, W - 1.0f);
-    int v0 = (int)fmaxf(floorf(vmin) - 1.0f, 0.0f);
-    int v1 = (int)fminf(floorf(vmax) + 1.0f, H - 1.0f);
-    if (u0 > u1 || v0 > v1) return 1;          // hull lies entirely in the guard band
-    // pick the finest pyramid level with <= 64 tiles over the footprint
-    const uint16_t* lvl;
-    int ts, lw;
-    const unsigned* lvl2 = nullptr;
-    if (((u1 >> 3) - (u0 >> 3) + 1) * ((v1 >> 3) - (v0 >> 3) + 1) <= 64) {
-        lvl = a.pyr.l0; ts = 3; lw = a.pyr.w0;
-    } else if (((u1 >> 5) - (u0 >> 5) + 1) * ((v1 >> 5) - (v0 >> 5) + 1) <= 64) {
-        lvl = a.pyr.l1; ts = 5; lw = a.pyr.w1;
-    } else {
-        lvl = nullptr; lvl2 = a.pyr.l2; ts = 7; lw = a.pyr.w2;
-    }
-    const int tx0 = u0 >> ts, tx1 = u1 >> ts, ty0 = v0 >> ts, ty1 = v1 >> ts;
-    const int ntx = tx1 - tx0 + 1;
-    const int ntiles = ntx * (ty1 - ty0 + 1);
+    const int u0 = (int)fmaxf(floorf(umin) - 1.0f, 0.0f);
+    const int u1 = (int)fminf(floorf(umax) + 1.0f, W - 1.0f);
+    const int v0 = (int)fmaxf(floorf(vmin) - 1.0f, 0.0f);
+    const int v1 = (int)fminf(floorf(vmax) + 1.0f, H - 1.0f);
+    if (u0 > u1 || v0 > v1) return 1;
+    // max depth over the footprint, on the finest pyramid level with <= 16 tiles
     unsigned m = 0;
-    for (int k = lane; k < ntiles; k += 64) {
-        const int ty = ty0 + k / ntx, tx = tx0 + k % ntx;
-        m = max(m, lvl ? (unsigned)lvl[ty * lw + tx] : lvl2[ty * lw + tx]);
+    if (((u1 >> 3) - (u0 >> 3) + 1) * ((v1 >> 3) - (v0 >> 3) + 1) <= 16) {
+        for (int ty = v0 >> 3; ty <= (v1 >> 3); ++ty)
+            for (int tx = u0 >> 3; tx <= (u1 >> 3); ++tx) m = max(m, (unsigned)a.pyr.l0[ty * a.pyr.w0 + tx]);
+    } else if (((u1 >> 5) - (u0 >> 5) + 1) * ((v1 >> 5) - (v0 >> 5) + 1) <= 16) {
+        for (int ty = v0 >> 5; ty <= (v1 >> 5); ++ty)
+            for (int tx = u0 >> 5; tx <= (u1 >> 5); ++tx) m = max(m, (unsigned)a.pyr.l1[ty * a.pyr.w1 + tx]);
+    } else {
+        for (int ty = v0 >> 7; ty <= (v1 >> 7); ++ty)
+            for (int tx = u0 >> 7; tx <= (u1 >> 7); ++tx) m = max(m, a.pyr.l2[ty * a.pyr.w2 + tx]);
     }
-    for (int off = 32; off > 0; off >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, off, 64));
-    if (m == 0) return 1;                       // every pixel has depth 0
+    if (m == 0) return 1;  // every pixel of the footprint has depth 0
     const float dmax = (float)m / a.depth_scale;
     const float margin = 1.0e-3f + 1.0e-4f * fabsf(zmax);
-    // every voxel has qz >= zmin, so diff <= dmax - zmin; reject when that is <= -mu
+    // every voxel has qz >= zmin, so diff <= dmax - zmin; rejected when that is <= -mu
     if (dmax - zmin < -g.mu - margin) return 1;
     return 0;
 }
 
-template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT>
-__global__ __launch_bounds__(256) void k_integrate(IntegrateArgs a) {
+struct UnitGrid {
+    unsigned nux, nuy, nuz, n;
+};
+
+__host__ __device__ inline UnitGrid unit_grid(const VolGeom& g) {
+    UnitGrid u;
+    u.nux = (unsigned)(g.dimx + UX - 1) / UX;
+    u.nuy = (unsigned)(g.dimy + UY - 1) / UY;
+    u.nuz = (unsigned)(g.lz + UZ - 1) / UZ;
+    u.n = u.nux * u.nuy * u.nuz;
+    return u;
+}
+
+// Pass 1: one lane per unit.  flags[u] = 1 when the unit may hold a touched voxel.
+__global__ __launch_bounds__(256) void k_cull_units(IntegrateArgs a, UnitGrid ug) {
+    const unsigned u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= ug.n) return;
+    const int ux = (int)(u % ug.nux), uy = (int)((u / ug.nux) % ug.nuy), uz = (int)(u / (ug.nux * ug.nuy));
+    const int live = a.cull ? !unit_cull(a, ux * UX, uy * UY, uz * UZ) : 1;
+    a.unit_flags[u] = (uint8_t)live;
+}
+
+__global__ __launch_bounds__(256) void k_count_live(const uint8_t* __restrict__ flags, unsigned n,
+                                                    unsigned long long* counters) {
+    unsigned c = 0;
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) c += flags[i];
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(counters + 3, (unsigned long long)c);
+}
+
+hipError_t launch_cull(const IntegrateArgs& a, hipStream_t s) {
+    const UnitGrid ug = unit_grid(a.g);
+    hipLaunchKernelGGL(k_cull_units, dim3((ug.n + 255) / 256), dim3(256), 0, s, a, ug);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && a.counters && (a.flags & 0x80000000u))
+        hipLaunchKernelGGL(k_count_live, dim3(64), dim3(256), 0, s, a.unit_flags, ug.n, a.counters);
+    return e == hipSuccess ? hipGetLastError() : e;
+}
+
+uint64_t brick_count_max(const VolGeom& g) { return unit_grid(g).n; }
+
+// Pass 2: persistent wavefronts over units.  Branch-free classification and update
+// (selects instead of divergent ifs) keep the scalar/branch overhead per item low; the only
+// divergent branches left guard the rare exact-division fallback, the gated colour /
+// histogram path and the stores.
+template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT, bool SHARD, bool PIN>
+__global__ __launch_bounds__(256) void k_integrate(IntegrateArgs a, UnitGrid ug) {
     const VolGeom& g = a.g;
-    const int x0 = blockIdx.x * BX, y0 = blockIdx.y * BY, lz0 = blockIdx.z * BZ;
-    const int tid = threadIdx.x;
-    if (a.cull) {
-        __shared__ int s_skip;
-        if (tid < 64) {
-            const int sk = brick_cull(a, x0, y0, lz0, tid);
-            if (tid == 0) s_skip = sk;
-        }
-        __syncthreads();
-        if (s_skip) return;
-    }
-    const int l = lz0 + (tid & (BZ - 1));
-    const int gy = y0 + (tid >> 5);
-    unsigned n_touch = 0, n_gate = 0, bad = 0;
-    bool active = (l < g.lz) && (gy < g.dimy);
-    int gz = 0;
-    if (active) {
-        gz = local_to_global_z(g, l);
-        active = gz < g.dimz;
-    }
-    if (active) {
-        const float py = fmaf((float)gy, g.voxel[1], g.start[1]);
-        const float pz = fmaf((float)gz, g.voxel[2], g.start[2]);
-        const uint64_t plane = (uint64_t)g.dimy * (uint64_t)g.lz;
-        const uint64_t base = (uint64_t)gy * (uint64_t)g.lz + (uint64_t)l;
-        const int xe = min(x0 + BX, g.dimx);
-        for (int gx = x0; gx < xe; ++gx) {
-            const float px = fmaf((float)gx, g.voxel[0], g.start[0]);
-            float qz;
-            int ix, iy;
-            project_voxel(a.E, a.K, px, py, pz, &qz, &ix, &iy);
-            if (ix < 0 || ix >= a.width || iy < 0 || iy >= a.height) continue;
-            const int img = iy * a.width + ix;
-            const unsigned d = a.depth[img];
-            if (d == 0) continue;
-            float diff = (float)d / a.depth_scale - qz;
-            if (diff <= -g.mu) continue;
-            if (diff > g.mu) diff = g.mu;
-            diff = diff / g.mu;
-            const uint64_t v = (uint64_t)gx * plane + base;
-            const int w = a.b.wt[v];
-            const float s = a.b.sdf[v];
-            a.b.sdf[v] = fmaf(s, (float)w, diff) / (float)(w + 1);
-            if (COUNT) ++n_touch;
-            if (!GATE || diff < a.gate) {
-                if (COUNT) ++n_gate;
-                const uint8_t* rgb = a.rgb + (size_t)img * 3;
-                if (CI32) {
-                    int32_t* c = reinterpret_cast<int32_t*>(a.b.color) + v * 3;
-                    c[0] = (c[0] * w + (int)rgb[0]) / (w + 1);
-                    c[1] = (c[1] * w + (int)rgb[1]) / (w + 1);
-                    c[2] = (c[2] * w + (int)rgb[2]) / (w + 1);
+    const int lane = threadIdx.x & 63;
+    const unsigned wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+    const unsigned nwaves = gridDim.x * (blockDim.x >> 6);
+    const uint64_t plane = (uint64_t)g.dimy * (uint64_t)g.zs;
+    unsigned n_touch = 0, n_gate = 0;
+    // The wave's units are wave, wave + nwaves, ...; their flags are fetched 64 at a time
+    // (one per lane) and the live ones are visited through the ballot mask.
+    for (unsigned first = wave; first < ug.n; first += 64u * nwaves) {
+        const unsigned mine = first + (unsigned)lane * nwaves;
+        const bool lv = mine < ug.n && a.unit_flags[mine];
+        unsigned long long todo = __ballot(lv);
+        while (todo) {
+            const int kk = __ffsll((long long)todo) - 1;
+            todo &= todo - 1ull;
+            const unsigned u = first + (unsigned)kk * nwaves;
+            const unsigned uxy = u % (ug.nux * ug.nuy);
+            const int x = (int)(uxy % ug.nux);
+            const int y = (int)(uxy / ug.nux) * UY + (lane >> 3);
+            const int l0 = (int)(u / (ug.nux * ug.nuy)) * UZ + (lane & 7) * 4;
+            const bool row_ok = (y < g.dimy) && (l0 < g.lz);
+            const float px = fmaf((float)x, g.voxel[0], g.start[0]);
+            const float py = fmaf((float)y, g.voxel[1], g.start[1]);
+            const uint64_t v = (uint64_t)x * plane + (uint64_t)y * (uint64_t)g.zs + (uint64_t)l0;
+
+            // ---- project the lane's 4 voxels (tsdf.cu:30-44)
+            int img[4];
+            float qz[4];
+            unsigned slow = 0;
+            float sxv[4], syv[4], szv[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                int gz = l0 + k;
+                bool zok = row_ok && (l0 + k < g.lz);
+                if (SHARD) {
+                    gz = local_to_global_z(g, l0 + k);
+                    zok = zok && gz < g.dimz;
+                }
+                const float pz = fmaf((float)gz, g.voxel[2], g.start[2]);
+                const float qx = dot3(a.E[0], a.E[1], a.E[2], px, py, pz) + a.E[3];
+                const float qy = dot3(a.E[4], a.E[5], a.E[6], px, py, pz) + a.E[7];
+                qz[k] = dot3(a.E[8], a.E[9], a.E[10], px, py, pz) + a.E[11];
+                float sx, sy, sz;
+                if (PIN) {
+                    sx = fmaf(a.K[2], qz[k], a.K[0] * qx);
+                    sy = fmaf(a.K[5], qz[k], a.K[4] * qy);
+                    sz = qz[k];
                 } else {
-                    uint8_t* c = reinterpret_cast<uint8_t*>(a.b.color) + v * 3;
-                    c[0] = (uint8_t)(((int)c[0] * w + (int)rgb[0]) / (w + 1));
-                    c[1] = (uint8_t)(((int)c[1] * w + (int)rgb[1]) / (w + 1));
-                    c[2] = (uint8_t)(((int)c[2] * w + (int)rgb[2]) / (w + 1));
+                    sx = dot3(a.K[0], a.K[1], a.K[2], qx, qy, qz[k]);
+                    sy = dot3(a.K[3], a.K[4], a.K[5], qx, qy, qz[k]);
+                    sz = dot3(a.K[6], a.K[7], a.K[8], qx, qy, qz[k]);
+                }
+                // floor(sx/sz), floor(sy/sz) through the reciprocal (see floor_div); lanes
+                // whose quotient is too close to an integer are redone exactly below
+                const float r = __builtin_amdgcn_rcpf(sz);
+                const float qu = sx * r, qv = sy * r;
+                const float fu = floorf(qu), fvv = floorf(qv);
+                const float tu = fabsf(qu) * 0x1p-19f, tv = fabsf(qv) * 0x1p-19f;
+                const bool fast = (qu - fu > tu) && (qu - fu < 1.0f - tu) && (qv - fvv > tv) &&
+                                  (qv - fvv < 1.0f - tv) && fabsf(sz) > 1.0e-30f && fabsf(qu) < 8.0e6f &&
+                                  fabsf(qv) < 8.0e6f;
+                const int ix = (int)fu, iy = (int)fvv;
+                const bool in = zok && ix >= 0 && ix < a.width && iy >= 0 && iy < a.height;
+                img[k] = in ? iy * a.width + ix : -1;
+                if (zok && !fast) slow |= 1u << k;
+                sxv[k] = sx; syv[k] = sy; szv[k] = sz;
+            }
+            if (slow) {  // rare: exact IEEE quotients
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (!(slow & (1u << k))) continue;
+                    const int ix = f2i_rd(sxv[k] / szv[k]), iy = f2i_rd(syv[k] / szv[k]);
+                    img[k] = (ix >= 0 && ix < a.width && iy >= 0 && iy < a.height) ? iy * a.width + ix : -1;
+                }
+            }
+            // ---- depth gather (one dword per voxel from the metres image)
+            float dm[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) dm[k] = a.pyr.metres[img[k] >= 0 ? img[k] : 0];
+            // ---- classify (tsdf.cu:48-52), branch-free
+            float fv[4];
+            unsigned tmask = 0, gmask = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float d = img[k] >= 0 ? dm[k] : 0.0f;
+                float diff = d - qz[k];
+                const bool t = (d != 0.0f) && (diff > -g.mu);
+                diff = (diff > g.mu) ? g.mu : diff;
+                fv[k] = diff / g.mu;
+                tmask |= (t ? 1u : 0u) << k;
+                gmask |= ((t && (!GATE || fv[k] < a.gate)) ? 1u : 0u) << k;
+            }
+            if (COUNT) {
+                n_touch += __popc(tmask);
+                n_gate += __popc(gmask);
+            }
+            if (a.debug == 3) {  // timing probe: classification only, no state traffic
+                asm volatile("" ::"v"(fv[0] + fv[1] + fv[2] + fv[3]), "v"(tmask), "v"(gmask));
+                continue;
+            }
+            if (a.debug == 4) gmask = 0;  // timing probe: no colour/histogram traffic
+            if (!tmask) continue;
+            // ---- state loads: one 16-B vector per array for the 4 voxels
+            const float4 s4 = *reinterpret_cast<const float4*>(a.b.sdf + v);
+            const int4 w4 = *reinterpret_cast<const int4*>(a.b.wt + v);
+            int4 vc4, vn4;
+            int vin[4];
+            if (VOTE) {
+                vc4 = *reinterpret_cast<const int4*>(a.b.cls + v);
+                vn4 = *reinterpret_cast<const int4*>(a.b.cls_cnt + v);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) vin[k] = a.cls[img[k] >= 0 ? img[k] : 0];
+            }
+            uint4 c8 = make_uint4(0, 0, 0, 0);
+            int4 c32[4];
+            unsigned pix[4] = {0, 0, 0, 0};
+            if (gmask) {
+                if (CI32) {
+                    const int4* c = reinterpret_cast<const int4*>(a.b.color) + v;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) c32[k] = c[k];
+                } else {
+                    c8 = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint32_t*>(a.b.color) + v);
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) pix[k] = a.pyr.rgbl[img[k] >= 0 ? img[k] : 0];
+            }
+            // ---- update (tsdf.cu:56, 68), branch-free selects
+            const float so[4] = {s4.x, s4.y, s4.z, s4.w};
+            const int wo[4] = {w4.x, w4.y, w4.z, w4.w};
+            float sn[4];
+            int wn[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const bool t = (tmask >> k) & 1u;
+                const float upd = fmaf(so[k], (float)wo[k], fv[k]) / (float)(wo[k] + 1);
+                sn[k] = t ? upd : so[k];
+                wn[k] = wo[k] + (t ? 1 : 0);
+            }
+            *reinterpret_cast<float4*>(a.b.sdf + v) = make_float4(sn[0], sn[1], sn[2], sn[3]);
+            *reinterpret_cast<int4*>(a.b.wt + v) = make_int4(wn[0], wn[1], wn[2], wn[3]);
+            if (gmask) {  // tsdf.cu:57-62
+                if (CI32) {
+                    int4* c = reinterpret_cast<int4*>(a.b.color) + v;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const bool gk = (gmask >> k) & 1u;
+                        const int wi = wo[k];
+                        const int r0 = pix[k] & 0xFF, r1 = (pix[k] >> 8) & 0xFF, r2 = (pix[k] >> 16) & 0xFF;
+                        int4 n = c32[k];
+                        n.x = avg_div(n.x * wi + r0, wi + 1);
+                        n.y = avg_div(n.y * wi + r1, wi + 1);
+                        n.z = avg_div(n.z * wi + r2, wi + 1);
+                        c32[k] = gk ? n : c32[k];
+                    }
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) c[k] = c32[k];
+                } else {
+                    unsigned cw[4] = {c8.x, c8.y, c8.z, c8.w};
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const bool gk = (gmask >> k) & 1u;
+                        const int wi = wo[k];
+                        const unsigned o = cw[k];
+                        const unsigned n0 = (unsigned)avg_div((int)(o & 0xFF) * wi + (int)(pix[k] & 0xFF), wi + 1);
+                        const unsigned n1 =
+                            (unsigned)avg_div((int)((o >> 8) & 0xFF) * wi + (int)((pix[k] >> 8) & 0xFF), wi + 1);
+                        const unsigned n2 =
+                            (unsigned)avg_div((int)((o >> 16) & 0xFF) * wi + (int)((pix[k] >> 16) & 0xFF), wi + 1);
+                        const unsigned nw = (n0 & 0xFF) | ((n1 & 0xFF) << 8) | ((n2 & 0xFF) << 16);
+                        cw[k] = gk ? nw : o;
+                    }
+                    *reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(a.b.color) + v) =
+                        make_uint4(cw[0], cw[1], cw[2], cw[3]);
                 }
                 if (SEM) {
-                    const unsigned lab = a.mask[img];
-                    if (lab < (unsigned)kMaxObjects) {
-                        a.b.hist[(uint64_t)lab * g.nvox + v] += 1u;
-                    } else {
-                        bad = 1;
+                    // tsdf.cu:61.  One lane owns the voxel, so a no-return atomic add is the
+                    // plain increment without a dependent load round trip.
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const unsigned lab = pix[k] >> 24;
+                        if (((gmask >> k) & 1u) && lab < (unsigned)kMaxObjects && a.debug != 6)
+                            atomicAdd(a.b.hist + (uint64_t)lab * g.nvox + v + k, 1u);
                     }
+                    unsigned bad = 0;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) bad |= ((gmask >> k) & 1u) && (pix[k] >> 24) >= (unsigned)kMaxObjects;
+                    if (bad) atomicOr(reinterpret_cast<unsigned*>(a.counters + 2), 1u);
                 }
             }
-            a.b.wt[v] = w + 1;
-            if (VOTE) {
-                const int lab = a.cls[img];
-                const int cnt = a.b.cls_cnt[v];
-                if (cnt == 0) {
-                    a.b.cls[v] = lab;
-                    a.b.cls_cnt[v] = 1;
-                } else if (a.b.cls[v] == lab) {
-                    a.b.cls_cnt[v] = cnt + 1;
-                } else {
-                    a.b.cls_cnt[v] = cnt - 1;
+            if (VOTE) {  // TSDF_Python/tsdf.cu:48-57
+                int vc[4] = {vc4.x, vc4.y, vc4.z, vc4.w}, vn[4] = {vn4.x, vn4.y, vn4.z, vn4.w};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (!((tmask >> k) & 1u)) continue;
+                    if (vn[k] == 0) {
+                        vc[k] = vin[k];
+                        vn[k] = 1;
+                    } else if (vc[k] == vin[k]) {
+                        vn[k] += 1;
+                    } else {
+                        vn[k] -= 1;
+                    }
                 }
+                *reinterpret_cast<int4*>(a.b.cls + v) = make_int4(vc[0], vc[1], vc[2], vc[3]);
+                *reinterpret_cast<int4*>(a.b.cls_cnt + v) = make_int4(vn[0], vn[1], vn[2], vn[3]);
             }
         }
     }
-    if (SEM && bad) atomicOr(reinterpret_cast<unsigned*>(a.counters + 2), 1u);
     if (COUNT) {
-        __shared__ unsigned s_cnt[2];
-        if (tid < 2) s_cnt[tid] = 0;
-        __syncthreads();
-        if (n_touch) atomicAdd(&s_cnt[0], n_touch);
-        if (n_gate) atomicAdd(&s_cnt[1], n_gate);
-        __syncthreads();
-        if (tid == 0) {
-            if (s_cnt[0]) atomicAdd(a.counters + 0, (unsigned long long)s_cnt[0]);
-            if (s_cnt[1]) atomicAdd(a.counters + 1, (unsigned long long)s_cnt[1]);
+        unsigned long long t = n_touch, gg = n_gate;
+        for (int off = 32; off > 0; off >>= 1) {
+            t += __shfl_xor(t, off, 64);
+            gg += __shfl_xor(gg, off, 64);
+        }
+        if (lane == 0) {
+            if (t) atomicAdd(a.counters + 0, t);
+            if (gg) atomicAdd(a.counters + 1, gg);
         }
     }
 }
 
-template <bool SEM, bool GATE, bool CI32, bool VOTE>
-static hipError_t launch_integrate_t(const IntegrateArgs& a, bool count, dim3 grid, hipStream_t s) {
-    if (count)
-        hipLaunchKernelGGL((k_integrate<SEM, GATE, CI32, VOTE, true>), grid, dim3(256), 0, s, a);
-    else
-        hipLaunchKernelGGL((k_integrate<SEM, GATE, CI32, VOTE, false>), grid, dim3(256), 0, s, a);
+// Persistent grid sized to exactly the resident capacity (blocks/CU from the occupancy
+// query x CUs): an oversubscribed persistent grid leaves a tail of late blocks.
+template <typename K>
+static unsigned resident_grid(K kernel) {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 1024;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 1024;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 256, 0) != hipSuccess || per < 1) per = 1;
+    return (unsigned)(cus * per);
+}
+
+template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT, bool SHARD, bool PIN>
+static hipError_t launch_integrate_k(const IntegrateArgs& a, hipStream_t s) {
+    static const unsigned grid = resident_grid(k_integrate<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>);
+    hipLaunchKernelGGL((k_integrate<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>), dim3(grid), dim3(256), 0, s, a,
+                       unit_grid(a.g));
     return hipGetLastError();
 }
 
+template <bool SEM, bool GATE, bool CI32, bool VOTE>
+static hipError_t launch_integrate_t(const IntegrateArgs& a, bool count, hipStream_t s) {
+    const bool shard = a.g.nshards > 1, pin = a.pinhole != 0;
+    if (count) {  // measurement pass: pinhole only is not assumed
+        if (shard) return launch_integrate_k<SEM, GATE, CI32, VOTE, true, true, false>(a, s);
+        return launch_integrate_k<SEM, GATE, CI32, VOTE, true, false, false>(a, s);
+    }
+    if (shard) {
+        if (pin) return launch_integrate_k<SEM, GATE, CI32, VOTE, false, true, true>(a, s);
+        return launch_integrate_k<SEM, GATE, CI32, VOTE, false, true, false>(a, s);
+    }
+    if (pin) return launch_integrate_k<SEM, GATE, CI32, VOTE, false, false, true>(a, s);
+    return launch_integrate_k<SEM, GATE, CI32, VOTE, false, false, false>(a, s);
+}
+
 hipError_t launch_integrate(const IntegrateArgs& a, hipStream_t s) {
-    const dim3 grid((a.g.dimx + BX - 1) / BX, (a.g.dimy + BY - 1) / BY, (a.g.lz + BZ - 1) / BZ);
     const bool count = a.counters != nullptr && (a.flags & 0x80000000u);
     const bool sem = a.flags & 0x1u, gate = a.flags & 0x2u, ci32 = a.flags & 0x4u, vote = a.flags & 0x8u;
     // Instantiated mode combinations: SfM semantic (u8 colour, gated), TSDF+colour (NumPy
     // rule: i32 colour, ungated), TSDF_Python vote, plus their neighbours.
     if (vote) {
-        if (ci32) return launch_integrate_t<false, false, true, true>(a, count, grid, s);
-        return launch_integrate_t<false, false, false, true>(a, count, grid, s);
+        if (ci32) return launch_integrate_t<false, false, true, true>(a, count, s);
+        return launch_integrate_t<false, false, false, true>(a, count, s);
     }
     if (sem) {
         if (gate) {
-            if (ci32) return launch_integrate_t<true, true, true, false>(a, count, grid, s);
-            return launch_integrate_t<true, true, false, false>(a, count, grid, s);
+            if (ci32) return launch_integrate_t<true, true, true, false>(a, count, s);
+            return launch_integrate_t<true, true, false, false>(a, count, s);
         }
-        if (ci32) return launch_integrate_t<true, false, true, false>(a, count, grid, s);
-        return launch_integrate_t<true, false, false, false>(a, count, grid, s);
+        if (ci32) return launch_integrate_t<true, false, true, false>(a, count, s);
+        return launch_integrate_t<true, false, false, false>(a, count, s);
     }
     if (gate) {
-        if (ci32) return launch_integrate_t<false, true, true, false>(a, count, grid, s);
-        return launch_integrate_t<false, true, false, false>(a, count, grid, s);
+        if (ci32) return launch_integrate_t<false, true, true, false>(a, count, s);
+        return launch_integrate_t<false, true, false, false>(a, count, s);
     }
-    if (ci32) return launch_integrate_t<false, false, true, false>(a, count, grid, s);
-    return launch_integrate_t<false, false, false, false>(a, count, grid, s);
+    if (ci32) return launch_integrate_t<false, false, true, false>(a, count, s);
+    return launch_integrate_t<false, false, false, false>(a, count, s);
 }
 
 // ------------------------------------------------------------------------------------
@@ -378,10 +621,10 @@ __device__ __forceinline__ Tri tri_setup(const VolGeom& g, float px, float py, f
     const int xc = min(max(x, 0), g.dimx - 1), yc = min(max(y, 0), g.dimy - 1), zc = min(max(z, 0), g.dimz - 1);
     const int xn = min(max(x + 1, 0), g.dimx - 1), yn = min(max(y + 1, 0), g.dimy - 1),
               zn = min(max(z + 1, 0), g.dimz - 1);
-    const uint64_t plane = (uint64_t)g.dimy * (uint64_t)g.lz;
-    t.i000 = (uint64_t)xc * plane + (uint64_t)yc * g.lz + (uint64_t)zc;
+    const uint64_t plane = (uint64_t)g.dimy * (uint64_t)g.zs;
+    t.i000 = (uint64_t)xc * plane + (uint64_t)yc * g.zs + (uint64_t)zc;
     t.dx = (uint64_t)(xn - xc) * plane;
-    t.dy = (uint64_t)(yn - yc) * (uint64_t)g.lz;
+    t.dy = (uint64_t)(yn - yc) * (uint64_t)g.zs;
     t.dz = (uint32_t)(zn - zc);
     return t;
 }
@@ -709,9 +952,9 @@ __global__ __launch_bounds__(256) void k_render(RenderArgs a) {
         } else {
             float cc[3];
             for (int ch = 0; ch < 3; ++ch) {
-                // colour planes are AoS [v*3 + ch]: sample with stride 3
-                const uint64_t i000 = tr.i000 * 3 + ch;
-                const uint64_t sx = tr.dx * 3, sy = tr.dy * 3, sz = (uint64_t)tr.dz * 3;
+                // colour is stored padded to 4 channels: [v*4 + ch]
+                const uint64_t i000 = tr.i000 * 4 + ch;
+                const uint64_t sx = tr.dx * 4, sy = tr.dy * 4, sz = (uint64_t)tr.dz * 4;
                 float d[8];
                 for (int k = 0; k < 8; ++k) {
                     const uint64_t off = ((k & 4) ? sx : 0) + ((k & 2) ? sy : 0) + ((k & 1) ? sz : 0);
@@ -742,37 +985,81 @@ hipError_t launch_render(const RenderArgs& a, hipStream_t s) {
 // histogram layout conversion (bin-major device <-> voxel-major reference export)
 // ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_hist_to_vm(const uint32_t* __restrict__ bm, uint32_t* __restrict__ vm,
-                                                    uint64_t nvox, uint64_t v0, uint64_t nv) {
-    // vm is a chunk [nv][32] for voxels v0 .. v0+nv
+                                                    uint64_t nvox, uint32_t lz, uint32_t zs, uint64_t v0, uint64_t nv) {
+    // vm is a chunk [nv][32] of logical voxels v0 .. v0+nv (rows of lz planes)
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv * kMaxObjects;
          i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t v = i / kMaxObjects, k = i % kMaxObjects;
-        vm[i] = bm[k * nvox + v0 + v];
+        const uint64_t v = v0 + i / kMaxObjects, k = i % kMaxObjects;
+        vm[i] = bm[k * nvox + (v / lz) * zs + v % lz];
     }
 }
 
 __global__ __launch_bounds__(256) void k_hist_to_bm(const uint32_t* __restrict__ vm, uint32_t* __restrict__ bm,
-                                                    uint64_t nvox, uint64_t v0, uint64_t nv) {
+                                                    uint64_t nvox, uint32_t lz, uint32_t zs, uint64_t v0, uint64_t nv) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv * kMaxObjects;
          i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t k = i / nv, v = i % nv;
-        bm[k * nvox + v0 + v] = vm[v * kMaxObjects + k];
+        const uint64_t k = i / nv, v = v0 + i % nv;
+        bm[k * nvox + (v / lz) * zs + v % lz] = vm[(v - v0) * kMaxObjects + k];
     }
 }
 
-hipError_t launch_hist_chunk_to_vm(const uint32_t* bm, uint32_t* vm, uint64_t nvox, uint64_t v0, uint64_t nv,
+hipError_t launch_hist_chunk_to_vm(const uint32_t* bm, uint32_t* vm, const VolGeom& g, uint64_t v0, uint64_t nv,
                                    hipStream_t s) {
     uint64_t blocks = (nv * kMaxObjects + 255) / 256;
     if (blocks > 16384) blocks = 16384;
-    hipLaunchKernelGGL(k_hist_to_vm, dim3((unsigned)blocks), dim3(256), 0, s, bm, vm, nvox, v0, nv);
+    hipLaunchKernelGGL(k_hist_to_vm, dim3((unsigned)blocks), dim3(256), 0, s, bm, vm, g.nvox, (uint32_t)g.lz,
+                       (uint32_t)g.zs, v0, nv);
     return hipGetLastError();
 }
 
-hipError_t launch_hist_chunk_to_bm(const uint32_t* vm, uint32_t* bm, uint64_t nvox, uint64_t v0, uint64_t nv,
+hipError_t launch_hist_chunk_to_bm(const uint32_t* vm, uint32_t* bm, const VolGeom& g, uint64_t v0, uint64_t nv,
                                    hipStream_t s) {
     uint64_t blocks = (nv * kMaxObjects + 255) / 256;
     if (blocks > 16384) blocks = 16384;
-    hipLaunchKernelGGL(k_hist_to_bm, dim3((unsigned)blocks), dim3(256), 0, s, vm, bm, nvox, v0, nv);
+    hipLaunchKernelGGL(k_hist_to_bm, dim3((unsigned)blocks), dim3(256), 0, s, vm, bm, g.nvox, (uint32_t)g.lz,
+                       (uint32_t)g.zs, v0, nv);
+    return hipGetLastError();
+}
+
+// colour: device storage is padded to 4 channels (u8x4 / i32x4), the reference layout has 3
+template <typename T>
+__global__ __launch_bounds__(256) void k_color_to_ref(const T* __restrict__ dev, T* __restrict__ ref, uint32_t lz,
+                                                      uint32_t zs, uint64_t v0, uint64_t nv) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv * 3; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t v = v0 + i / 3, c = i % 3;
+        ref[i] = dev[((v / lz) * zs + v % lz) * 4 + c];
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_color_from_ref(const T* __restrict__ ref, T* __restrict__ dev, uint32_t lz,
+                                                        uint32_t zs, uint64_t v0, uint64_t nv) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv * 3; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t v = v0 + i / 3, c = i % 3;
+        dev[((v / lz) * zs + v % lz) * 4 + c] = ref[i];
+    }
+}
+
+hipError_t launch_color_chunk(const void* src, void* dst, bool to_ref, bool i32, const VolGeom& g, uint64_t v0,
+                              uint64_t nv, hipStream_t s) {
+    uint64_t blocks = (nv * 3 + 255) / 256;
+    if (blocks > 16384) blocks = 16384;
+    const dim3 gr((unsigned)blocks), bl(256);
+    if (i32) {
+        if (to_ref)
+            hipLaunchKernelGGL(k_color_to_ref<int32_t>, gr, bl, 0, s, (const int32_t*)src, (int32_t*)dst, (uint32_t)g.lz,
+                               (uint32_t)g.zs, v0, nv);
+        else
+            hipLaunchKernelGGL(k_color_from_ref<int32_t>, gr, bl, 0, s, (const int32_t*)src, (int32_t*)dst,
+                               (uint32_t)g.lz, (uint32_t)g.zs, v0, nv);
+    } else {
+        if (to_ref)
+            hipLaunchKernelGGL(k_color_to_ref<uint8_t>, gr, bl, 0, s, (const uint8_t*)src, (uint8_t*)dst, (uint32_t)g.lz,
+                               (uint32_t)g.zs, v0, nv);
+        else
+            hipLaunchKernelGGL(k_color_from_ref<uint8_t>, gr, bl, 0, s, (const uint8_t*)src, (uint8_t*)dst,
+                               (uint32_t)g.lz, (uint32_t)g.zs, v0, nv);
+    }
     return hipGetLastError();
 }
 

@@ -100,6 +100,9 @@ class Timing(C.Structure):
         ("n_render", C.c_uint64),
         ("touched", C.c_uint64),
         ("gated", C.c_uint64),
+        ("bricks", C.c_uint64),
+        ("prep_ms", C.c_double),
+        ("n_prep", C.c_uint64),
     ]
 
 

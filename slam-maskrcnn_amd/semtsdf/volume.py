@@ -82,7 +82,7 @@ class Volume:
         self.W, self.H = params.width, params.height
         st = self.state()
         self.local_dim = tuple(st.local_dim)
-        self.nvox = int(st.local_voxels)
+        self.nvox = int(st.local_voxels)  # reference layout (dense rows of local_dim[2] planes)
 
     # ---- lifecycle
     @property
