@@ -48,7 +48,7 @@ def lib():
         _lib = C.CDLL(LIB)
         P = C.c_void_p
         _lib.oracle_integrate.argtypes = [P, P, P, P, C.c_int, C.c_int, C.c_uint32, P, P, P, P, P, P, P, P, P, P,
-                                          C.c_int, C.c_int, P]
+                                          C.c_int, C.c_int, P, P, C.c_int]
         _lib.oracle_integrate.restype = None
         _lib.oracle_march_probs.argtypes = [P, P, P, P, C.c_int, C.c_int, P, P, C.c_float, P, P, C.c_int, C.c_int]
         _lib.oracle_march_probs.restype = None
@@ -101,8 +101,8 @@ def k9(K16):
 class OState:
     """Reference-layout volume state for the C oracle."""
 
-    def __init__(self, dims, mu, semantic=False, color_i32=False, vote=False):
-        n = int(np.prod(dims))
+    def __init__(self, dims, mu, semantic=False, color_i32=False, vote=False, lz=None):
+        n = int(dims[0]) * int(dims[1]) * int(dims[2] if lz is None else lz)
         self.sdf = np.full(n, np.float32(mu), np.float32)
         self.wt = np.zeros(n, np.int32)
         self.color = np.zeros(n * 3, np.int32 if color_i32 else np.uint8)
@@ -111,15 +111,19 @@ class OState:
         self.cls_cnt = np.zeros(n, np.int32) if vote else None
 
 
-def integrate(g: OGeom, st: OState, K16, E16, depth, rgb, mask=None, cls=None, flags=0x3, x_range=None):
+def integrate(g: OGeom, st: OState, K16, E16, depth, rgb, mask=None, cls=None, flags=0x3, x_range=None, zmap=None):
+    """zmap: global z of each local plane (a Z-slab shard); st must then be sized
+    dims[0] x dims[1] x len(zmap)."""
     H, W = depth.shape[:2]
     x0, x1 = (0, int(g.dims[0])) if x_range is None else x_range
     counts = np.zeros(3, np.uint64)
+    zm = None if zmap is None else np.ascontiguousarray(zmap, np.int32)
     lib().oracle_integrate(_p(g.dims), _p(g.geo), _p(k9(K16)), _p(np.ascontiguousarray(E16, np.float32).reshape(16)),
                            W, H, flags, _p(st.sdf), _p(st.wt), _p(st.color), _p(st.hist), _p(st.cls), _p(st.cls_cnt),
                            _p(np.ascontiguousarray(depth, np.uint16)), _p(np.ascontiguousarray(rgb, np.uint8)),
                            _p(None if mask is None else np.ascontiguousarray(mask, np.uint8)),
-                           _p(None if cls is None else np.ascontiguousarray(cls, np.int32)), x0, x1, _p(counts))
+                           _p(None if cls is None else np.ascontiguousarray(cls, np.int32)), x0, x1, _p(counts),
+                           _p(zm), 0 if zm is None else int(zm.size))
     return counts
 
 

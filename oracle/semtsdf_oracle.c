@@ -71,16 +71,22 @@ static ogeom mk_geom(const int32_t* dims, const float* geo) {
 void oracle_integrate(const int32_t* dims, const float* geo, const float* K9, const float* E16, int width,
                       int height, uint32_t flags, float* sdf, int32_t* wt, void* color, uint32_t* hist,
                       int32_t* cls, int32_t* cls_cnt, const uint16_t* depth, const uint8_t* rgb,
-                      const uint8_t* mask, const int32_t* cls_in, int x_begin, int x_end, uint64_t* counts) {
+                      const uint8_t* mask, const int32_t* cls_in, int x_begin, int x_end, uint64_t* counts,
+                      const int32_t* zmap, int lz) {
+    /* zmap: global z of each of the lz local planes (a Z-slab shard); NULL =
+       the whole volume.  State arrays are [dims[0]][dims[1]][lz]. */
     const ogeom g = mk_geom(dims, geo);
+    if (!zmap) lz = g.dz;
     const int sem = flags & 1, gate = flags & 2, ci32 = flags & 4, vote = flags & 8;
     uint64_t n_touch = 0, n_gate = 0, n_bad = 0;
     for (int x = x_begin; x < x_end; ++x) {
         const float px = fmaf((float)x, g.voxel[0], g.start[0]);
         for (int y = 0; y < g.dy; ++y) {
             const float py = fmaf((float)y, g.voxel[1], g.start[1]);
-            for (int z = 0; z < g.dz; ++z) {
-                const float pz = fmaf((float)z, g.voxel[2], g.start[2]);
+            for (int z = 0; z < lz; ++z) {
+                const int gz = zmap ? zmap[z] : z;
+                if (gz >= g.dz) continue;
+                const float pz = fmaf((float)gz, g.voxel[2], g.start[2]);
                 /* proj = extrinsic2init[0:3] . (p, 1)   (tsdf.cu:31-34) */
                 const float qx = o_dot3(E16[0], E16[1], E16[2], px, py, pz) + E16[3];
                 const float qy = o_dot3(E16[4], E16[5], E16[6], px, py, pz) + E16[7];
@@ -99,7 +105,7 @@ void oracle_integrate(const int32_t* dims, const float* geo, const float* K9, co
                 if (diff <= -g.mu) continue;
                 if (diff > g.mu) diff = g.mu;
                 diff = diff / g.mu;
-                const size_t v = ((size_t)x * g.dy + y) * g.dz + z;
+                const size_t v = ((size_t)x * g.dy + y) * lz + z;
                 const int w = wt[v];
                 /* running mean with unit weight (tsdf.cu:56) */
                 sdf[v] = fmaf(sdf[v], (float)w, diff) / (float)(w + 1);

@@ -828,6 +828,7 @@ int semtsdf_raycast_dev(semtsdf_vol* v, const float s2w[16], const float c[3], i
 // device storage (rows padded to zs planes).  eb = bytes per voxel.
 static hipError_t copy_rows(const semtsdf_vol* v, void* dst, const void* src, size_t eb, bool to_host, hipStream_t s) {
     const size_t rows = (size_t)v->g.dimx * v->g.dimy;
+    if (v->g.lz == 0) return hipSuccess;
     const size_t w = (size_t)v->g.lz * eb, pitch_dev = (size_t)v->g.zs * eb;
     if (v->g.lz == v->g.zs)
         return hipMemcpyAsync(dst, src, rows * w, to_host ? hipMemcpyDeviceToHost : hipMemcpyHostToDevice, s);
@@ -840,6 +841,7 @@ static int color_xfer(semtsdf_vol* v, void* host, bool to_host, hipStream_t s) {
     const bool i32 = v->p.flags & SEMTSDF_F_COLOR_I32;
     const size_t es = i32 ? 4 : 1;
     const uint64_t n = (uint64_t)v->g.dimx * v->g.dimy * v->g.lz;
+    if (n == 0) return SEMTSDF_OK;
     const uint64_t chunk = std::min<uint64_t>(n, 1ull << 24);
     void* stage = nullptr;
     HIPC(hipMalloc(&stage, chunk * 3 * es));
@@ -876,17 +878,17 @@ int semtsdf_download(semtsdf_vol* v, float* sdf, int32_t* wt, void* color, uint3
         if (rc) return rc;
     }
     if (cls) {
-        if (!v->b.cls) return fail(SEMTSDF_ERR_STATE, "not a VOTE volume");
+        if (!(v->p.flags & SEMTSDF_F_VOTE)) return fail(SEMTSDF_ERR_STATE, "not a VOTE volume");
         HIPC(copy_rows(v, cls, v->b.cls, 4, true, s));
     }
     if (cls_cnt) {
-        if (!v->b.cls_cnt) return fail(SEMTSDF_ERR_STATE, "not a VOTE volume");
+        if (!(v->p.flags & SEMTSDF_F_VOTE)) return fail(SEMTSDF_ERR_STATE, "not a VOTE volume");
         HIPC(copy_rows(v, cls_cnt, v->b.cls_cnt, 4, true, s));
     }
     if (hist) {
-        if (!v->b.hist) return fail(SEMTSDF_ERR_STATE, "not a SEMANTIC volume");
+        if (!(v->p.flags & SEMTSDF_F_SEMANTIC)) return fail(SEMTSDF_ERR_STATE, "not a SEMANTIC volume");
         const uint64_t n = (uint64_t)v->g.dimx * v->g.dimy * v->g.lz;
-        const uint64_t chunk = std::min<uint64_t>(n, 1ull << 22);  // 4M voxels = 512 MiB staging
+        const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(n, 1ull << 22));  // <= 512 MiB staging
         uint32_t* stage = nullptr;
         HIPC(hipMalloc(&stage, chunk * kMaxObjects * 4));
         for (uint64_t v0 = 0; v0 < n; v0 += chunk) {
@@ -918,17 +920,17 @@ int semtsdf_upload(semtsdf_vol* v, const float* sdf, const int32_t* wt, const vo
         if (rc) return rc;
     }
     if (cls) {
-        if (!v->b.cls) return fail(SEMTSDF_ERR_STATE, "not a VOTE volume");
+        if (!(v->p.flags & SEMTSDF_F_VOTE)) return fail(SEMTSDF_ERR_STATE, "not a VOTE volume");
         HIPC(copy_rows(v, v->b.cls, cls, 4, false, s));
     }
     if (cls_cnt) {
-        if (!v->b.cls_cnt) return fail(SEMTSDF_ERR_STATE, "not a VOTE volume");
+        if (!(v->p.flags & SEMTSDF_F_VOTE)) return fail(SEMTSDF_ERR_STATE, "not a VOTE volume");
         HIPC(copy_rows(v, v->b.cls_cnt, cls_cnt, 4, false, s));
     }
     if (hist) {
-        if (!v->b.hist) return fail(SEMTSDF_ERR_STATE, "not a SEMANTIC volume");
+        if (!(v->p.flags & SEMTSDF_F_SEMANTIC)) return fail(SEMTSDF_ERR_STATE, "not a SEMANTIC volume");
         const uint64_t n = (uint64_t)v->g.dimx * v->g.dimy * v->g.lz;
-        const uint64_t chunk = std::min<uint64_t>(n, 1ull << 22);
+        const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(n, 1ull << 22));
         uint32_t* stage = nullptr;
         HIPC(hipMalloc(&stage, chunk * kMaxObjects * 4));
         for (uint64_t v0 = 0; v0 < n; v0 += chunk) {

@@ -302,6 +302,7 @@ __global__ __launch_bounds__(256) void k_count_live(const uint8_t* __restrict__ 
 
 hipError_t launch_cull(const IntegrateArgs& a, hipStream_t s) {
     const UnitGrid ug = unit_grid(a.g);
+    if (ug.n == 0) return hipSuccess;  // a shard that owns no chunk
     hipLaunchKernelGGL(k_cull_units, dim3((ug.n + 255) / 256), dim3(256), 0, s, a, ug);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && a.counters && (a.flags & 0x80000000u))
@@ -405,7 +406,7 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateArgs a, UnitGrid ug)
                 float diff = d - qz[k];
                 const bool t = (d != 0.0f) && (diff > -g.mu);
                 diff = (diff > g.mu) ? g.mu : diff;
-                fv[k] = diff / g.mu;
+                fv[k] = (a.debug == 7) ? diff * __builtin_amdgcn_rcpf(g.mu) : diff / g.mu;
                 tmask |= (t ? 1u : 0u) << k;
                 gmask |= ((t && (!GATE || fv[k] < a.gate)) ? 1u : 0u) << k;
             }
@@ -452,7 +453,8 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateArgs a, UnitGrid ug)
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const bool t = (tmask >> k) & 1u;
-                const float upd = fmaf(so[k], (float)wo[k], fv[k]) / (float)(wo[k] + 1);
+                const float upd = (a.debug == 7) ? fmaf(so[k], (float)wo[k], fv[k]) * __builtin_amdgcn_rcpf((float)(wo[k] + 1))
+                                                 : fmaf(so[k], (float)wo[k], fv[k]) / (float)(wo[k] + 1);
                 sn[k] = t ? upd : so[k];
                 wn[k] = wo[k] + (t ? 1 : 0);
             }
@@ -552,7 +554,10 @@ static unsigned resident_grid(K kernel) {
 
 template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT, bool SHARD, bool PIN>
 static hipError_t launch_integrate_k(const IntegrateArgs& a, hipStream_t s) {
-    static const unsigned grid = resident_grid(k_integrate<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>);
+    if (unit_grid(a.g).n == 0) return hipSuccess;
+    static const unsigned grid0 = resident_grid(k_integrate<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>);
+    unsigned grid = grid0;
+    if (a.debug >= 100) grid = grid0 * (unsigned)(a.debug - 100) / 8u;  // timing probe: fraction of residency
     hipLaunchKernelGGL((k_integrate<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>), dim3(grid), dim3(256), 0, s, a,
                        unit_grid(a.g));
     return hipGetLastError();

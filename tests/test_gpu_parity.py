@@ -256,3 +256,51 @@ def test_error_paths(S, stream):
         vol.associate(np.ascontiguousarray(frames[1].mask.copy()), np.eye(4, dtype=np.float32))
     assert e.value.code == L.ERR_STATE  # n_obs == 0 (tsdf.cu:426)
     vol.close()
+
+
+@pytest.mark.parametrize("nshards,chunk", [(2, 8), (3, 5), (4, 16)])
+def test_sharded_handles_equal_single_volume(S, oracle, stream, nshards, chunk):
+    """Z-slab shards on one device: the gathered owned planes equal the
+    single-handle volume bit for bit, halo planes equal their owners, and each shard
+    equals the C oracle run on the same local plane map."""
+    from semtsdf.shard import ShardLayout
+
+    st, frames = stream
+    semtsdf, L = S
+    dims = (40, 36, 48)
+    p, vol, g, ost = make(S, oracle, dims, frames[0], 0x3)
+    shards = []
+    for sidx in range(nshards):
+        q = semtsdf.default_params(64, KI, 640, 480)
+        for fld in ("dim", "vol_start", "vol_end", "voxel", "K", "Kinv"):
+            getattr(q, fld)[:] = getattr(p, fld)[:]
+        q.mu, q.flags = p.mu, p.flags
+        q.z_nshards, q.z_shard, q.z_chunk = nshards, sidx, chunk
+        shards.append(semtsdf.Volume(q, 0))
+    lay = ShardLayout(dims[2], nshards, chunk)
+    for k in range(1, 4):
+        fr = frames[k]
+        E = (fr.w2c @ frames[0].c2w).astype(np.float32)
+        vol.integrate(fr.depth, fr.rgb, fr.gt_ids, E)
+        for sh in shards:
+            sh.integrate(fr.depth, fr.rgb, fr.gt_ids, E)
+    full = vol.download(hist=True)
+    locs = [sh.download(hist=True) for sh in shards]
+    for key, extra in (("sdf", ()), ("wt", ()), ("color", (3,)), ("hist", (32,))):
+        parts = [lc[key].reshape((dims[0], dims[1], -1) + extra) for lc in locs]
+        got = lay.gather(parts, dims[0], dims[1])
+        ref = full[key].reshape((dims[0], dims[1], dims[2]) + extra)
+        assert np.array_equal(got.view(np.uint8), ref.view(np.uint8)), key
+        assert lay.check_halo(parts), key
+    # one shard against the oracle with the same local plane map
+    zmap = lay.local_to_global(1)
+    ost1 = oracle.OState(list(dims), p.mu, semantic=True, lz=zmap.size)
+    for k in range(1, 4):
+        fr = frames[k]
+        E = (fr.w2c @ frames[0].c2w).astype(np.float32)
+        oracle.integrate(g, ost1, list(p.K), E, fr.depth, fr.rgb, fr.gt_ids, flags=0x3, zmap=zmap)
+    assert np.array_equal(locs[1]["sdf"].view(np.uint32), ost1.sdf.view(np.uint32))
+    assert np.array_equal(locs[1]["hist"], ost1.hist)
+    for sh in shards:
+        sh.close()
+    vol.close()
