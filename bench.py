@@ -5,8 +5,10 @@ One step = one frame of the per-frame integrate (src/SfM_CUDA/tsdf.cu:18-70 sema
 SDF + gated colour + 32-bin instance histogram) over the whole volume, inputs resident
 in HBM.  N=1 runs configuration C3 (512^3 semantic, synthetic 640x480 stream with masks).
 N>1 ranks (torchrun, one process per GPU) each own an interleaved Z-slab shard of a
-512 x 512 x (512 N) volume, so every GPU integrates 512^3 voxels per frame (weak
-scaling; Z-slab sharding needs no collective for integrate).
+512 x 512 x (512 N) volume covering the same physical box (the SfM placement divides
+each axis by its own dim, so z resolution grows N-fold) -- every GPU owns 512^3 voxels
+and sees the same share of the surface band per frame (weak scaling; Z-slab sharding
+needs no collective for integrate).
 
 value = voxels integrated by all ranks / max-over-ranks wall time of the K timed steps.
 Extra fields: frames/s of the full per-frame pipeline (association raycast + relabel +
@@ -36,98 +38,154 @@ def log(*a):
 
 
 def dist_setup(n_gpus):
+    """One process per GPU (torch.distributed.run).  The data path has no collective (each
+    rank integrates its own Z-slab shard); the process group only carries the barrier and
+    the max/sum of the timings.  Backend: RCCL ("nccl") by default; BENCH_DIST_BACKEND=gloo
+    rehearses N ranks on fewer GPUs (device = LOCAL_RANK % device count)."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != n_gpus:
-        if world == 1 and n_gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    if world == 1 and n_gpus > 1:
+        raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    device = local
     pg = None
     if world > 1:
         import torch
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://")
+        backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+        ndev = torch.cuda.device_count()
+        device = local % max(ndev, 1) if backend == "gloo" else local
+        torch.cuda.set_device(device)
+        dist.init_process_group(backend, init_method="env://")
         pg = dist
-    return rank, world, local, pg
+    return rank, world, device, pg
 
 
-def barrier(pg, local):
+def _reduce(pg, device, x: float, op) -> float:
+    if pg is None:
+        return x
+    import torch
+
+    on_gpu = pg.get_backend() == "nccl"
+    t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{device}" if on_gpu else "cpu")
+    pg.all_reduce(t, op=op)
+    return float(t.item())
+
+
+def barrier(pg, device):
     if pg is not None:
         import torch
 
-        pg.barrier(device_ids=[local])
+        if pg.get_backend() == "nccl":
+            pg.barrier(device_ids=[device])
+        else:
+            pg.barrier()
         torch.cuda.synchronize()
 
 
-def max_over_ranks(pg, local, x: float) -> float:
-    if pg is None:
-        return x
-    import torch
-
-    t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
-    pg.all_reduce(t, op=pg.ReduceOp.MAX)
-    return float(t.item())
+def max_over_ranks(pg, device, x: float) -> float:
+    return x if pg is None else _reduce(pg, device, x, pg.ReduceOp.MAX)
 
 
-def sum_over_ranks(pg, local, x: float) -> float:
-    if pg is None:
-        return x
-    import torch
-
-    t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
-    pg.all_reduce(t, op=pg.ReduceOp.SUM)
-    return float(t.item())
+def sum_over_ranks(pg, device, x: float) -> float:
+    return x if pg is None else _reduce(pg, device, x, pg.ReduceOp.SUM)
 
 
-def cpu_baseline(frames, p, f0, x_planes=64, slabs=3):
-    """NumPy restatement of tsdf.py:78-120 (+ SfM gate/histogram), 1 core, over a bounded
-    sample: `slabs` x `x_planes` x-planes of the 512^3 volume, one frame each."""
+def _cpu_slab_worker(job):
+    """Integrate one x-slab of the volume with the NumPy restatement (1 BLAS thread).
+    Returns (voxel-updates, seconds)."""
+    frame, p_geo, x0, x_planes = job
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     try:
         from threadpoolctl import threadpool_limits
+        ctx = threadpool_limits(limits=1)
     except Exception:  # pragma: no cover
-        threadpool_limits = None
-    D = p.dim[0]
-    Dy, Dz = p.dim[1], p.dim[2]
-    assert D == Dy == Dz, "the CPU baseline runs on the cubic N=1 volume"
+        ctx = None
+    depth, rgb, mask, E = frame
+    D, Dy, Dz, vs, vx, mu = p_geo
     K = np.eye(4, dtype=np.float32)
     K[(0, 1, 0, 1), (0, 1, 2, 2)] = KI
-    vs = np.array(p.vol_start[:], np.float64)
-    vx = np.array(p.voxel[:], np.float64)
-    mu = float(p.mu)
     n = x_planes * Dy * Dz
     sdf = np.full(n, np.float32(mu), np.float32)
     wt = np.zeros(n, np.int32)
     col = np.zeros((n, 3), np.uint8)
     hist = np.zeros((n, 32), np.uint32)
-    total_vox = 0
-    t_total = 0.0
-    ctx = threadpool_limits(limits=1) if threadpool_limits else None
-    try:
-        for s in range(slabs):
-            fr = frames[(s % len(frames))]
-            E = (fr.w2c @ f0.c2w).astype(np.float64)
-            x0 = (D // 2 - x_planes // 2 + (s - slabs // 2) * x_planes) % max(D - x_planes, 1)
-            # shift the origin so the slab [x0, x0+x_planes) is processed in a local buffer
-            vs_s = vs.copy()
-            vs_s[0] = vs[0] + x0 * vx[0]
-            sdf[:] = np.float32(mu)
-            wt[:] = 0
+    vs_s = np.array(vs, np.float64)
+    vs_s[0] = vs[0] + x0 * vx[0]  # the slab [x0, x0 + x_planes) in a local buffer
+    t0 = time.perf_counter()
+    O.numpy_integrate(sdf, wt, col, D, vs_s, vx, mu, K, E, depth, rgb, x_range=(0, x_planes),
+                      semantic=True, gate=0.99, mask=mask, hist=hist)
+    dt = time.perf_counter() - t0
+    if ctx is not None:
+        ctx.__exit__(None, None, None)
+    return n, dt
+
+
+def cpu_baseline(frames, p, f0, x_planes=64, slabs=10, workers=1):
+    """NumPy restatement of tsdf.py:78-120 (+ SfM gate/histogram) over a bounded sample of
+    the 512^3 workload: `slabs` x-slabs of `x_planes` planes around the volume centre, one
+    frame each.  workers=1: one core, time = sum of the slab times.  workers>1: x-slab
+    multiprocessing (fork; the children only run NumPy), time = wall time of the pool."""
+    D, Dy, Dz = p.dim[0], p.dim[1], p.dim[2]
+    assert D == Dy == Dz, "the CPU baseline runs on the cubic N=1 volume"
+    geo = (D, Dy, Dz, tuple(p.vol_start[:]), tuple(float(v) for v in p.voxel[:]), float(p.mu))
+    jobs = []
+    for s in range(slabs):
+        fr = frames[s % len(frames)]
+        E = (fr.w2c @ f0.c2w).astype(np.float64)
+        x0 = (D // 2 - x_planes // 2 + (s - slabs // 2) * x_planes) % max(D - x_planes, 1)
+        jobs.append(((fr.depth, fr.rgb, fr.mask, E), geo, x0, x_planes))
+    if workers <= 1:
+        res = [_cpu_slab_worker(j) for j in jobs]
+        total = sum(r[0] for r in res)
+        t = sum(r[1] for r in res)
+    else:
+        import multiprocessing as mp
+
+        with mp.get_context("fork").Pool(workers) as pool:
             t0 = time.perf_counter()
-            O.numpy_integrate(sdf, wt, col, D, vs_s, vx, mu, K, E, fr.depth, fr.rgb, x_range=(0, x_planes),
-                              semantic=True, gate=0.99, mask=fr.mask, hist=hist)
-            t_total += time.perf_counter() - t0
-            total_vox += n
-    finally:
-        if ctx is not None:
-            ctx.__exit__(None, None, None)
-    return {"value": total_vox / t_total / 1e6, "unit": "Mvoxel-updates/s", "cores": 1, "kind": "port",
-            "sample": f"{slabs} x {x_planes} x-planes of the {D}^3 volume ({total_vox} voxel-updates, "
-                      f"{t_total:.1f} s), NumPy restatement of tsdf.py:78-120 + SfM gate/histogram, "
-                      f"1 BLAS thread"}
+            res = pool.map(_cpu_slab_worker, jobs, chunksize=1)
+            t = time.perf_counter() - t0
+        total = sum(r[0] for r in res)
+    return {"value": total / t / 1e6, "unit": "Mvoxel-updates/s", "cores": int(workers), "kind": "port",
+            "sample": f"{slabs} x-slabs of {x_planes} planes of the {D}^3 volume, one synthetic frame each "
+                      f"({total} voxel-updates, {t:.1f} s{' wall' if workers > 1 else ''}), NumPy restatement of "
+                      f"tsdf.py:78-120 + SfM gate/histogram, 1 BLAS thread per "
+                      f"{'worker' if workers > 1 else 'process'}"}
+
+
+def host_cores() -> int:
+    """Cores this job may use on the host (the GPU box caps the share via OMP_NUM_THREADS)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except Exception:  # pragma: no cover
+        n = os.cpu_count() or 1
+    cap = os.environ.get("OMP_NUM_THREADS")
+    if cap and cap.isdigit():
+        n = min(n, int(cap))
+    return max(1, n)
+
+
+def copy_bandwidth(device: int, nbytes: int = 1 << 30) -> float:
+    """Achievable HBM bandwidth (GB/s, read + write) of a device-to-device copy, for context
+    beside the 8 TB/s spec peak."""
+    import torch
+
+    a = torch.empty(nbytes // 4, dtype=torch.float32, device=f"cuda:{device}").fill_(1.0)
+    b = torch.empty_like(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    best = 1e9
+    for _ in range(5):
+        e0.record()
+        b.copy_(a)
+        e1.record()
+        e1.synchronize()
+        best = min(best, e0.elapsed_time(e1))
+    del a, b
+    torch.cuda.empty_cache()
+    return 2.0 * nbytes / (best * 1e-3) / 1e9
 
 
 def main():
@@ -142,7 +200,8 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true")
     ap.add_argument("--no-cull", action="store_true", help="debug: disable brick culling")
     ap.add_argument("--cpu-planes", type=int, default=64)
-    ap.add_argument("--cpu-slabs", type=int, default=3)
+    ap.add_argument("--cpu-slabs", type=int, default=10)
+    ap.add_argument("--cpu-workers", type=int, default=0, help="N-core CPU baseline workers (0 = host cores)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="per-launch HBM bytes of the integrate kernel from rocprofv3 PMC (see profiles/)")
     args = ap.parse_args()
@@ -170,6 +229,17 @@ def main():
         p.z_nshards = world
         p.z_shard = rank
         p.z_chunk = args.z_chunk
+    # CPU baseline first: the forked N-core workers then start from a process that has not
+    # touched the GPU yet.
+    cpu = cpu_n = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(frames, p, f0, args.cpu_planes, args.cpu_slabs, 1)
+        nw = args.cpu_workers or host_cores()
+        if nw > 1:
+            cpu_n = cpu_baseline(frames, p, f0, args.cpu_planes, max(args.cpu_slabs, nw), nw)
+        log(f"[bench] cpu baseline 1 core {cpu['value']:.1f} Mvox/s"
+            + (f", {nw} cores {cpu_n['value']:.1f} Mvox/s" if cpu_n else ""))
+
     vol = semtsdf.Volume(p, local)
     st0 = vol.state()
     voxels_per_rank = D * D * D  # owned voxels (halo planes are integrated redundantly, not counted)
@@ -278,9 +348,9 @@ def main():
         obuf.free()
         mwork.free()
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(frames, p, f0, args.cpu_planes, args.cpu_slabs)
+    copy_bw = None
+    if rank == 0 and not args.no_pipeline:
+        copy_bw = copy_bandwidth(local)
 
     if rank == 0:
         rec = {
@@ -321,6 +391,8 @@ def main():
                 "algorithmic_bytes_per_launch": int(bytes_per_launch),
             },
             "cpu_baseline": cpu,
+            "cpu_baseline_ncores": cpu_n,
+            "hbm_copy_gbs": round(copy_bw, 1) if copy_bw else None,
             "pipeline": pipeline,
         }
         print(json.dumps(rec), flush=True)

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SEMTSDF_ABI_VERSION 1
+#define SEMTSDF_ABI_VERSION 2
 #define SEMTSDF_MAX_OBJECTS 32 /* tsdf.cuh:4 */
 
 /* ---- status codes ------------------------------------------------------------ */
@@ -184,6 +184,32 @@ int semtsdf_raycast(semtsdf_vol* v, const float s2w[16], const float c[3], int m
                     uint8_t* out_bgr, float* out_t, void* stream);
 int semtsdf_raycast_dev(semtsdf_vol* v, const float s2w[16], const float c[3], int mode,
                         uint8_t* out_bgr_d, float* out_t_d, void* stream);
+
+/* ---- Z-sharded raycast (replaces the single-GPU back_proj_kernel
+ * tsdf.cu:72-135 and show_tsdf_kernel viewer.cu:17-86 when the volume is split across GPUs)
+ * Every shard of a group runs the same call sequence.  Between calls the host all-gathers
+ * the per-pixel `send` records (record_bytes each) of all shards, in shard order, into
+ * `gathered` (z_nshards * record_bytes, device memory):
+ *   begin(kind, cam, c, &rec, &nsteps)
+ *   for s in 0..nsteps-1:  step(s, s ? gathered : NULL, send);  all-gather send -> gathered
+ *   kind RENDER_*:  render_finish(gathered, out_bgr, out_t)   -- all-gathered composite
+ *   kind RAY_ASSOC: assoc_partial(gathered, mask, partial);    all-reduce(SUM) partial;
+ *                   assoc_apply(reduced, mask, stats)         -- decide + relabel
+ * The result is bit-identical to the single-volume raycast / association. */
+#define SEMTSDF_RAY_ASSOC 2
+#define SEMTSDF_ASSOC_PARTIAL_LEN 3168 /* int64 words: 32x32 t1, t3; 32 t2, c1, c2; 32x32 c3 */
+int semtsdf_shard_ray_begin(semtsdf_vol* v, int kind, const float cam[16], const float c[3],
+                            size_t* record_bytes, int* nsteps);
+int semtsdf_shard_ray_step(semtsdf_vol* v, int step, const void* gathered_d, void* send_d, void* stream);
+int semtsdf_shard_render_finish(semtsdf_vol* v, const void* gathered_d, uint8_t* out_bgr_d, float* out_t_d,
+                                void* stream);
+int semtsdf_shard_assoc_partial(semtsdf_vol* v, const void* gathered_d, const uint8_t* mask_d,
+                                int64_t* partial_d, void* stream);
+int semtsdf_shard_assoc_apply(semtsdf_vol* v, const int64_t* reduced_d, uint8_t* mask_d,
+                              semtsdf_assoc_stats* stats, void* stream);
+/* parse_frame for a sharded handle: the host runs the association protocol above (when
+ * n_obs > 0), then integrate_dev, then note_integrated (n_obs++, first-frame object count). */
+int semtsdf_shard_note_integrated(semtsdf_vol* v, const uint8_t* mask_d, void* stream);
 
 /* ---- state transfer (parity, checkpoint/resume) ------------------------------------------
  * Reference layouts, local storage (for an unsharded handle: the whole volume).  Any

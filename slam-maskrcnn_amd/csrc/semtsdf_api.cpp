@@ -87,6 +87,11 @@ struct semtsdf_vol {
     unsigned long long* counters_d = nullptr;
     uint8_t* unit_flags_d = nullptr;
     AssocDecision* decision_h = nullptr;  // pinned
+    // Z-sharded raycast protocol (allocated on first use)
+    void* ray_state_d = nullptr;   // ShardRayState arrays, 6 x npx x 4 B
+    MarchCamera ray_cam{};
+    int ray_kind = -1;
+    int ray_next = 0;              // next expected step
     uint32_t n_obs = 0;
     // instrumentation
     int instr = 0;
@@ -115,7 +120,7 @@ void free_all(semtsdf_vol* v) {
     void* ptrs[] = {v->b.sdf, v->b.wt, v->b.color, v->b.hist, v->b.cls, v->b.cls_cnt, v->depth_d, v->rgb_d,
                     v->mask_d, v->cls_d, v->pyr.metres, v->pyr.rgbl, v->pyr.l0, v->pyr.l1, v->pyr.l2, v->tables_d, v->decision_d,
                     v->num_objs_d, v->probs_d, v->box_d, v->palette_d, v->render_d, v->render_t_d,
-                    v->counters_d, v->unit_flags_d};
+                    v->counters_d, v->unit_flags_d, v->ray_state_d};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (v->decision_h) (void)hipHostFree(v->decision_h);
@@ -750,6 +755,160 @@ int semtsdf_parse_frame_dev(semtsdf_vol* v, const uint16_t* depth_d, const uint8
     }
     int rc = integrate_impl(v, depth_d, rgb_d, sem ? mask_d : nullptr, nullptr, E, s);
     if (rc) return rc;
+    v->n_obs++;
+    return SEMTSDF_OK;
+}
+
+// ---- Z-sharded raycast protocol ------------------------------------------------------
+static ShardRayArgs shard_args(semtsdf_vol* v) {
+    ShardRayArgs a{};
+    a.g = v->g;
+    a.b = v->b;
+    a.cam = v->ray_cam;
+    a.width = v->p.width;
+    a.height = v->p.height;
+    a.kind = v->ray_kind;
+    const size_t n = npx(v);
+    char* base = (char*)v->ray_state_d;
+    a.st.k = (int*)(base);
+    a.st.fk = (float*)(base + 4 * n);
+    a.st.j = (int*)(base + 8 * n);
+    a.st.fj = (float*)(base + 12 * n);
+    a.st.fp = (float*)(base + 16 * n);
+    a.st.t = (float*)(base + 20 * n);
+    a.color_i32 = (v->p.flags & SEMTSDF_F_COLOR_I32) ? 1 : 0;
+    a.palette = v->palette_d;
+    a.n_obs = (float)v->n_obs;
+    a.eps = v->p.prior_mrcnn_err_rate;
+    a.box_thresh = v->p.box_thresh;
+    return a;
+}
+
+int semtsdf_shard_ray_begin(semtsdf_vol* v, int kind, const float cam[16], const float c[3], size_t* record_bytes,
+                            int* nsteps) {
+    if (!v || !cam) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    if (kind != SEMTSDF_RENDER_LABEL && kind != SEMTSDF_RENDER_COLOR && kind != SEMTSDF_RAY_ASSOC)
+        return fail(SEMTSDF_ERR_INVALID, "bad ray kind %d", kind);
+    if (kind != SEMTSDF_RAY_ASSOC && !c) return fail(SEMTSDF_ERR_INVALID, "render needs the camera centre");
+    if ((kind == SEMTSDF_RENDER_LABEL || kind == SEMTSDF_RAY_ASSOC) && !(v->p.flags & SEMTSDF_F_SEMANTIC))
+        return fail(SEMTSDF_ERR_STATE, "label render / association needs a SEMANTIC volume");
+    if (kind == SEMTSDF_RAY_ASSOC && v->n_obs == 0)
+        return fail(SEMTSDF_ERR_STATE, "association needs n_obs > 0 (tsdf.cu:426)");
+    HIPC(hipSetDevice(v->device));
+    if (!v->ray_state_d) {
+        int rc = dev_alloc(v, &v->ray_state_d, 24 * npx(v));
+        if (rc) return rc;
+    }
+    if (kind == SEMTSDF_RAY_ASSOC) {
+        v->ray_cam = assoc_camera(v, cam);
+    } else {
+        MarchCamera m{};
+        for (int i = 0; i < 12; ++i) m.s2w[i] = cam[i];
+        m.o[0] = c[0]; m.o[1] = c[1]; m.o[2] = c[2];
+        m.use_s2w = 1;
+        v->ray_cam = m;
+    }
+    v->ray_kind = kind;
+    v->ray_next = 0;
+    if (record_bytes) *record_bytes = 8 * npx(v);
+    if (nsteps) *nsteps = kind == SEMTSDF_RAY_ASSOC ? 3 : 4;
+    return SEMTSDF_OK;
+}
+
+int semtsdf_shard_ray_step(semtsdf_vol* v, int step, const void* gathered_d, void* send_d, void* stream) {
+    if (!v || !send_d) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    if (v->ray_kind < 0) return fail(SEMTSDF_ERR_STATE, "shard_ray_begin was not called");
+    const int nsteps = v->ray_kind == SEMTSDF_RAY_ASSOC ? 3 : 4;
+    if (step != v->ray_next || step >= nsteps)
+        return fail(SEMTSDF_ERR_STATE, "ray step %d out of order (expected %d of %d)", step, v->ray_next, nsteps);
+    if (step > 0 && !gathered_d) return fail(SEMTSDF_ERR_INVALID, "step %d needs the gathered records", step);
+    HIPC(hipSetDevice(v->device));
+    hipStream_t s = pick(v, stream);
+    ShardRayArgs a = shard_args(v);
+    a.step = step;
+    a.gathered = (const int2*)gathered_d;
+    a.send = (int2*)send_d;
+    EventPair ep;
+    timing_begin(v, v->ray_kind == SEMTSDF_RAY_ASSOC ? v->ev_assoc : v->ev_render, s, &ep);
+    if (step < 3) HIPC(launch_shard_ray_step(a, s));
+    else HIPC(launch_shard_render_final(a, s));
+    timing_end(v, v->ray_kind == SEMTSDF_RAY_ASSOC ? v->ev_assoc : v->ev_render, s, &ep);
+    v->ray_next = step + 1;
+    return SEMTSDF_OK;
+}
+
+int semtsdf_shard_render_finish(semtsdf_vol* v, const void* gathered_d, uint8_t* out_bgr_d, float* out_t_d,
+                                void* stream) {
+    if (!v || !gathered_d || !out_bgr_d) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    if (v->ray_kind != SEMTSDF_RENDER_LABEL && v->ray_kind != SEMTSDF_RENDER_COLOR)
+        return fail(SEMTSDF_ERR_STATE, "no render in progress");
+    if (v->ray_next != 4) return fail(SEMTSDF_ERR_STATE, "render_finish before step 3");
+    HIPC(hipSetDevice(v->device));
+    hipStream_t s = pick(v, stream);
+    ShardRayArgs a = shard_args(v);
+    a.gathered = (const int2*)gathered_d;
+    a.out_bgr = out_bgr_d;
+    a.out_t = out_t_d;
+    HIPC(launch_shard_render_finish(a, s));
+    v->ray_kind = -1;
+    v->n_render++;
+    return SEMTSDF_OK;
+}
+
+int semtsdf_shard_assoc_partial(semtsdf_vol* v, const void* gathered_d, const uint8_t* mask_d, int64_t* partial_d,
+                                void* stream) {
+    if (!v || !gathered_d || !mask_d || !partial_d) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    if (v->ray_kind != SEMTSDF_RAY_ASSOC || v->ray_next != 3)
+        return fail(SEMTSDF_ERR_STATE, "assoc_partial needs the three association steps first");
+    HIPC(hipSetDevice(v->device));
+    hipStream_t s = pick(v, stream);
+    ShardRayArgs a = shard_args(v);
+    a.gathered = (const int2*)gathered_d;
+    a.mask = mask_d;
+    a.partial = (long long*)partial_d;
+    EventPair ep;
+    timing_begin(v, v->ev_assoc, s, &ep);
+    HIPC(hipMemsetAsync(partial_d, 0, sizeof(int64_t) * SEMTSDF_ASSOC_PARTIAL_LEN, s));
+    HIPC(launch_shard_assoc_partial(a, s));
+    timing_end(v, v->ev_assoc, s, &ep);
+    v->ray_kind = -1;
+    return SEMTSDF_OK;
+}
+
+int semtsdf_shard_assoc_apply(semtsdf_vol* v, const int64_t* reduced_d, uint8_t* mask_d, semtsdf_assoc_stats* stats,
+                              void* stream) {
+    if (!v || !reduced_d || !mask_d) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    HIPC(hipSetDevice(v->device));
+    hipStream_t s = pick(v, stream);
+    EventPair ep;
+    timing_begin(v, v->ev_assoc, s, &ep);
+    HIPC(hipMemsetAsync(v->tables_d, 0, sizeof(AssocTables), s));
+    HIPC(hipMemsetAsync(&v->tables_d->first_px[0], 0xFF, sizeof(unsigned) * 256, s));
+    HIPC(launch_mask_stats(mask_d, (int)npx(v), v->tables_d, s));
+    HIPC(launch_tables_from_partial((const long long*)reduced_d, v->tables_d, s));
+    HIPC(launch_assoc_decide(v->tables_d, v->decision_d, 0, v->p.prior_mrcnn_err_rate, v->num_objs_d, s));
+    HIPC(launch_relabel(mask_d, (int)npx(v), v->decision_d, s));
+    timing_end(v, v->ev_assoc, s, &ep);
+    v->n_assoc++;
+    if (stats) {
+        HIPC(hipMemcpyAsync(v->decision_h, v->decision_d, sizeof(AssocDecision), hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+        decision_to_stats(*v->decision_h, stats);
+    }
+    return SEMTSDF_OK;
+}
+
+int semtsdf_shard_note_integrated(semtsdf_vol* v, const uint8_t* mask_d, void* stream) {
+    if (!v) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    HIPC(hipSetDevice(v->device));
+    hipStream_t s = pick(v, stream);
+    if (v->n_obs == 0 && (v->p.flags & SEMTSDF_F_SEMANTIC)) {
+        if (!mask_d) return fail(SEMTSDF_ERR_INVALID, "semantic volume needs a mask");
+        HIPC(hipMemsetAsync(v->tables_d, 0, sizeof(AssocTables), s));
+        HIPC(hipMemsetAsync(&v->tables_d->first_px[0], 0xFF, sizeof(unsigned) * 256, s));
+        HIPC(launch_mask_stats(mask_d, (int)npx(v), v->tables_d, s));
+        HIPC(launch_first_frame_objs(v->tables_d, v->num_objs_d, s));
+    }
     v->n_obs++;
     return SEMTSDF_OK;
 }

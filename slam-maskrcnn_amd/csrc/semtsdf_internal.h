@@ -124,7 +124,43 @@ struct RenderArgs {
     float* out_t;
 };
 
+// Z-sharded raycast protocol (k_shard_* in semtsdf_kernels.hip): per-pixel march state.
+struct ShardRayState {
+    int* k;      // global coarse event index, -1 = miss
+    float* fk;   // sample value at the coarse event
+    int* j;      // fine hit index (0 = hit in the coarse phase)
+    float* fj;   // sample value at the fine hit
+    float* fp;   // sample value before the hit
+    float* t;    // refined hit t, -1 = miss
+};
+
+constexpr int kAssocPartialLen = 3 * kMaxObjects * kMaxObjects + 3 * kMaxObjects;  // int64 words
+
+struct ShardRayArgs {
+    VolGeom g;
+    VolBufs b;
+    MarchCamera cam;
+    int width, height;
+    int kind;                 // 0 label render, 1 colour render, 2 association
+    int step;                 // 0..2 (k_shard_ray_step)
+    const int2* gathered;     // [nshards][npx] records of the previous step
+    int2* send;               // [npx] this shard's records
+    ShardRayState st;
+    int color_i32;
+    const uint8_t* palette;
+    uint8_t* out_bgr;
+    float* out_t;
+    const uint8_t* mask;
+    float n_obs, eps, box_thresh;
+    long long* partial;       // [kAssocPartialLen]
+};
+
 // ---- launchers (semtsdf_kernels.hip) ----
+hipError_t launch_shard_ray_step(const ShardRayArgs& a, hipStream_t s);
+hipError_t launch_shard_render_final(const ShardRayArgs& a, hipStream_t s);
+hipError_t launch_shard_render_finish(const ShardRayArgs& a, hipStream_t s);
+hipError_t launch_shard_assoc_partial(const ShardRayArgs& a, hipStream_t s);
+hipError_t launch_tables_from_partial(const long long* reduced, AssocTables* t, hipStream_t s);
 hipError_t launch_fill_volume(const VolGeom& g, const VolBufs& b, uint32_t flags, hipStream_t s);
 hipError_t launch_depth_pyramid(const uint16_t* depth, const uint8_t* rgb, const uint8_t* mask, int w, int h,
                                 float scale, const DepthPyramid& p, hipStream_t s);

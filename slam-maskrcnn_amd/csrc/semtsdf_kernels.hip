@@ -56,6 +56,20 @@ __device__ __forceinline__ int local_to_global_z(const VolGeom& g, int l) {
     return (c * g.nshards + g.shard) * g.chunk + w;
 }
 
+// Local plane of a global plane owned by this shard (inverse of local_to_global_z).
+__device__ __forceinline__ int global_to_local_z(const VolGeom& g, int z) {
+    const int c = z / g.chunk;
+    return (c / g.nshards) * (g.chunk + g.halo) + (z - c * g.chunk);
+}
+
+// Shard owning the trilinear sample at world z `pz` (its base plane, clamped as the
+// sampler clamps it).
+__device__ __forceinline__ int sample_owner(const VolGeom& g, float pz) {
+    const float iz = (pz - g.start[2]) / g.voxel[2];
+    const int zc = min(max(f2i_rd(iz), 0), g.dimz - 1);
+    return (zc / g.chunk) % g.nshards;
+}
+
 // Project one voxel (reference tsdf.cu:30-44).  Returns camera-space z in *qz and the
 // pixel in *px/*py.
 __device__ __forceinline__ void project_voxel(const float* __restrict__ E, const float* __restrict__ K,
@@ -627,7 +641,10 @@ __device__ __forceinline__ Tri tri_setup(const VolGeom& g, float px, float py, f
     const int xn = min(max(x + 1, 0), g.dimx - 1), yn = min(max(y + 1, 0), g.dimy - 1),
               zn = min(max(z + 1, 0), g.dimz - 1);
     const uint64_t plane = (uint64_t)g.dimy * (uint64_t)g.zs;
-    t.i000 = (uint64_t)xc * plane + (uint64_t)yc * g.zs + (uint64_t)zc;
+    // global plane -> local plane of this shard (the caller only samples planes it owns;
+    // zn = zc + 1 is then the chunk's next plane or its halo plane)
+    const int zl = g.nshards == 1 ? zc : global_to_local_z(g, zc);
+    t.i000 = (uint64_t)xc * plane + (uint64_t)yc * g.zs + (uint64_t)zl;
     t.dx = (uint64_t)(xn - xc) * plane;
     t.dy = (uint64_t)(yn - yc) * (uint64_t)g.zs;
     t.dz = (uint32_t)(zn - zc);
@@ -653,8 +670,10 @@ __device__ __forceinline__ float sample_sdf(const VolGeom& g, const float* sdf, 
 
 // The shared ray march of back_proj_kernel (tsdf.cu:90-124) and show_tsdf_kernel
 // (viewer.cu:223-257).  Returns true on a hit and the refined t.
-__device__ bool march_ray(const VolGeom& g, const float* __restrict__ sdf, float ox, float oy, float oz,
-                          float dx, float dy, float dz, float* t_hit) {
+// Slab test of the march (tsdf.cu:90-100): returns false when the ray misses the volume,
+// else the first sample position and the (exclusive) end of the march.
+__device__ __forceinline__ bool ray_bounds(const VolGeom& g, float ox, float oy, float oz, float dx, float dy,
+                                           float dz, float* t0, float* t1) {
     const float idx_ = 1.0f / dx, idy = 1.0f / dy, idz = 1.0f / dz;
     const float tbx = idx_ * (g.start[0] - ox), tby = idy * (g.start[1] - oy), tbz = idz * (g.start[2] - oz);
     const float ttx = idx_ * (g.end[0] - ox), tty = idy * (g.end[1] - oy), ttz = idz * (g.end[2] - oz);
@@ -663,8 +682,15 @@ __device__ bool march_ray(const VolGeom& g, const float* __restrict__ sdf, float
     float tfar = fminf(fminf(fmaxf(ttx, tbx), fmaxf(tty, tby)), fmaxf(ttz, tbz));
     tfar = fminf(tfar, 100.0f);
     if (tnear > tfar) return false;
-    float t = tnear + 1e-6f;
-    tfar -= 1e-6f;
+    *t0 = tnear + 1e-6f;
+    *t1 = tfar - 1e-6f;
+    return true;
+}
+
+__device__ bool march_ray(const VolGeom& g, const float* __restrict__ sdf, float ox, float oy, float oz,
+                          float dx, float dy, float dz, float* t_hit) {
+    float t, tfar;
+    if (!ray_bounds(g, ox, oy, oz, dx, dy, dz, &t, &tfar)) return false;
     float f_tt = 0.0f;
     const float vx = g.voxel[0];
     float step = vx;
@@ -759,20 +785,56 @@ __device__ __forceinline__ long long to_fix(float L) {
     return (long long)rint((double)L * kFixScale);
 }
 
-__global__ __launch_bounds__(256) void k_assoc_march(AssocArgs a) {
-    __shared__ long long s_t1[kMaxObjects][kMaxObjects];
-    __shared__ long long s_t3[kMaxObjects][kMaxObjects];
-    __shared__ long long s_t2[kMaxObjects];
-    __shared__ unsigned s_c1[kMaxObjects];
-    __shared__ unsigned s_c2[kMaxObjects];
-    __shared__ unsigned s_c3[kMaxObjects][kMaxObjects];
-    const int tid = threadIdx.x;
-    for (int k = tid; k < kMaxObjects * kMaxObjects; k += 256) {
-        (&s_t1[0][0])[k] = 0;
-        (&s_t3[0][0])[k] = 0;
-        (&s_c3[0][0])[k] = 0;
+// Workgroup-local (LDS) copy of the accumulated sums of AssocTables.
+struct AssocLds {
+    long long t1[kMaxObjects][kMaxObjects];
+    long long t3[kMaxObjects][kMaxObjects];
+    long long t2[kMaxObjects];
+    unsigned c1[kMaxObjects];
+    unsigned c2[kMaxObjects];
+    unsigned c3[kMaxObjects][kMaxObjects];
+};
+
+__device__ __forceinline__ void assoc_lds_clear(AssocLds& s) {
+    for (int k = threadIdx.x; k < kMaxObjects * kMaxObjects; k += blockDim.x) {
+        (&s.t1[0][0])[k] = 0;
+        (&s.t3[0][0])[k] = 0;
+        (&s.c3[0][0])[k] = 0;
     }
-    if (tid < kMaxObjects) { s_t2[tid] = 0; s_c1[tid] = 0; s_c2[tid] = 0; }
+    if (threadIdx.x < kMaxObjects) { s.t2[threadIdx.x] = 0; s.c1[threadIdx.x] = 0; s.c2[threadIdx.x] = 0; }
+}
+
+// One pixel's terms of filter_overlaps (tsdf.cu:312-334): p = trilinear histogram at the
+// hit (zeros without a hit), m = the pixel's current label.
+__device__ __forceinline__ void assoc_accumulate(AssocLds& s, const float* p, unsigned m, float n_obs, float eps,
+                                                 float box_thresh) {
+    if (m > 0 && m < (unsigned)kMaxObjects) {
+        atomicAdd(&s.c1[m], 1u);
+#pragma unroll
+        for (int j = 1; j < kMaxObjects; ++j) {
+            const float L = logf(fmaxf(p[j] / n_obs, eps));
+            atomicAdd(reinterpret_cast<unsigned long long*>(&s.t1[m][j]), (unsigned long long)to_fix(L));
+        }
+    }
+#pragma unroll
+    for (int n = 1; n < kMaxObjects; ++n) {
+        if (p[n] > box_thresh) {
+            const float L = logf(fmaxf(1.0f - p[n] / n_obs, eps));
+            const unsigned long long f = (unsigned long long)to_fix(L);
+            atomicAdd(reinterpret_cast<unsigned long long*>(&s.t2[n]), f);
+            atomicAdd(&s.c2[n], 1u);
+            if (m > 0 && m < (unsigned)kMaxObjects) {
+                atomicAdd(reinterpret_cast<unsigned long long*>(&s.t3[m][n]), f);
+                atomicAdd(&s.c3[m][n], 1u);
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_assoc_march(AssocArgs a) {
+    __shared__ AssocLds s;
+    const int tid = threadIdx.x;
+    assoc_lds_clear(s);
     __syncthreads();
 
     const int x = blockIdx.x * 16 + (tid & 15);
@@ -796,43 +858,22 @@ __global__ __launch_bounds__(256) void k_assoc_march(AssocArgs a) {
                 a.box_out[(size_t)px * kMaxObjects + k] = p[k] > a.box_thresh ? 1 : 0;
             }
         }
-        const unsigned m = a.mask[px];
-        if (m > 0 && m < (unsigned)kMaxObjects) {
-            atomicAdd(&s_c1[m], 1u);
-#pragma unroll
-            for (int j = 1; j < kMaxObjects; ++j) {
-                const float L = logf(fmaxf(p[j] / a.n_obs, a.eps));
-                atomicAdd(reinterpret_cast<unsigned long long*>(&s_t1[m][j]), (unsigned long long)to_fix(L));
-            }
-        }
-#pragma unroll
-        for (int n = 1; n < kMaxObjects; ++n) {
-            if (p[n] > a.box_thresh) {
-                const float L = logf(fmaxf(1.0f - p[n] / a.n_obs, a.eps));
-                const unsigned long long f = (unsigned long long)to_fix(L);
-                atomicAdd(reinterpret_cast<unsigned long long*>(&s_t2[n]), f);
-                atomicAdd(&s_c2[n], 1u);
-                if (m > 0 && m < (unsigned)kMaxObjects) {
-                    atomicAdd(reinterpret_cast<unsigned long long*>(&s_t3[m][n]), f);
-                    atomicAdd(&s_c3[m][n], 1u);
-                }
-            }
-        }
+        assoc_accumulate(s, p, a.mask[px], a.n_obs, a.eps, a.box_thresh);
     }
     __syncthreads();
     AssocTables* T = a.tables;
     for (int k = tid; k < kMaxObjects * kMaxObjects; k += 256) {
-        const long long v1 = (&s_t1[0][0])[k];
+        const long long v1 = (&s.t1[0][0])[k];
         if (v1) atomicAdd(reinterpret_cast<unsigned long long*>(&T->t1[0][0]) + k, (unsigned long long)v1);
-        const long long v3 = (&s_t3[0][0])[k];
+        const long long v3 = (&s.t3[0][0])[k];
         if (v3) atomicAdd(reinterpret_cast<unsigned long long*>(&T->t3[0][0]) + k, (unsigned long long)v3);
-        const unsigned c3 = (&s_c3[0][0])[k];
+        const unsigned c3 = (&s.c3[0][0])[k];
         if (c3) atomicAdd(&T->c3[0][0] + k, c3);
     }
     if (tid < kMaxObjects) {
-        if (s_t2[tid]) atomicAdd(reinterpret_cast<unsigned long long*>(&T->t2[tid]), (unsigned long long)s_t2[tid]);
-        if (s_c1[tid]) atomicAdd(&T->c1[tid], s_c1[tid]);
-        if (s_c2[tid]) atomicAdd(&T->c2[tid], s_c2[tid]);
+        if (s.t2[tid]) atomicAdd(reinterpret_cast<unsigned long long*>(&T->t2[tid]), (unsigned long long)s.t2[tid]);
+        if (s.c1[tid]) atomicAdd(&T->c1[tid], s.c1[tid]);
+        if (s.c2[tid]) atomicAdd(&T->c2[tid], s.c2[tid]);
     }
 }
 
@@ -930,6 +971,43 @@ hipError_t launch_relabel(uint8_t* mask, int npx, const AssocDecision* d, hipStr
 // ------------------------------------------------------------------------------------
 // render raycast (show_tsdf_kernel viewer.cu:17-86; colour mode tsdf_render.frag:125-131)
 // ------------------------------------------------------------------------------------
+// Shade one hit (viewer.cu:66-84 label mode; tsdf_render.frag:125-131 colour mode).
+__device__ __forceinline__ void shade_hit(const VolGeom& g, const VolBufs& vb, const Tri& tr, int mode, int color_i32,
+                                          const uint8_t* __restrict__ palette, uint8_t* b, uint8_t* gch, uint8_t* r) {
+    if (mode == 0) {
+        float max_cnt = 0.0f;
+        int obj = 0;
+        for (int k = 0; k < kMaxObjects; ++k) {
+            const float c = tri_eval(vb.hist + (uint64_t)k * g.nvox, tr);
+            if (c > max_cnt) { max_cnt = c; obj = k; }
+        }
+        if (obj > 0) {
+            *b = palette[obj * 3 + 2];
+            *gch = palette[obj * 3 + 1];
+            *r = palette[obj * 3 + 0];
+        }
+    } else {
+        float cc[3];
+        for (int ch = 0; ch < 3; ++ch) {
+            // colour is stored padded to 4 channels: [v*4 + ch]
+            const uint64_t i000 = tr.i000 * 4 + ch;
+            const uint64_t sx = tr.dx * 4, sy = tr.dy * 4, sz = (uint64_t)tr.dz * 4;
+            float d[8];
+            for (int k = 0; k < 8; ++k) {
+                const uint64_t off = ((k & 4) ? sx : 0) + ((k & 2) ? sy : 0) + ((k & 1) ? sz : 0);
+                d[k] = color_i32 ? (float)reinterpret_cast<const int32_t*>(vb.color)[i000 + off]
+                                 : (float)reinterpret_cast<const uint8_t*>(vb.color)[i000 + off];
+            }
+            const float low = mixf(mixf(d[0], d[4], tr.fx), mixf(d[2], d[6], tr.fx), tr.fy);
+            const float high = mixf(mixf(d[1], d[5], tr.fx), mixf(d[3], d[7], tr.fx), tr.fy);
+            cc[ch] = mixf(low, high, tr.fz);
+        }
+        *b = (uint8_t)(int)cc[0];
+        *gch = (uint8_t)(int)cc[1];
+        *r = (uint8_t)(int)cc[2];
+    }
+}
+
 __global__ __launch_bounds__(256) void k_render(RenderArgs a) {
     const int x = blockIdx.x * 16 + (threadIdx.x & 15);
     const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
@@ -942,38 +1020,7 @@ __global__ __launch_bounds__(256) void k_render(RenderArgs a) {
     if (march_ray(a.g, a.b.sdf, ox, oy, oz, dx, dy, dz, &t)) {
         th = t;
         const Tri tr = tri_setup(a.g, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
-        if (a.mode == 0) {
-            float max_cnt = 0.0f;
-            int obj = 0;
-            for (int k = 0; k < kMaxObjects; ++k) {
-                const float c = tri_eval(a.b.hist + (uint64_t)k * a.g.nvox, tr);
-                if (c > max_cnt) { max_cnt = c; obj = k; }
-            }
-            if (obj > 0) {
-                b = a.palette[obj * 3 + 2];
-                gch = a.palette[obj * 3 + 1];
-                r = a.palette[obj * 3 + 0];
-            }
-        } else {
-            float cc[3];
-            for (int ch = 0; ch < 3; ++ch) {
-                // colour is stored padded to 4 channels: [v*4 + ch]
-                const uint64_t i000 = tr.i000 * 4 + ch;
-                const uint64_t sx = tr.dx * 4, sy = tr.dy * 4, sz = (uint64_t)tr.dz * 4;
-                float d[8];
-                for (int k = 0; k < 8; ++k) {
-                    const uint64_t off = ((k & 4) ? sx : 0) + ((k & 2) ? sy : 0) + ((k & 1) ? sz : 0);
-                    d[k] = a.color_i32 ? (float)reinterpret_cast<const int32_t*>(a.b.color)[i000 + off]
-                                       : (float)reinterpret_cast<const uint8_t*>(a.b.color)[i000 + off];
-                }
-                const float low = mixf(mixf(d[0], d[4], tr.fx), mixf(d[2], d[6], tr.fx), tr.fy);
-                const float high = mixf(mixf(d[1], d[5], tr.fx), mixf(d[3], d[7], tr.fx), tr.fy);
-                cc[ch] = mixf(low, high, tr.fz);
-            }
-            b = (uint8_t)(int)cc[0];
-            gch = (uint8_t)(int)cc[1];
-            r = (uint8_t)(int)cc[2];
-        }
+        shade_hit(a.g, a.b, tr, a.mode, a.color_i32, a.palette, &b, &gch, &r);
     }
     a.out_bgr[(size_t)px * 3 + 0] = b;
     a.out_bgr[(size_t)px * 3 + 1] = gch;
@@ -983,6 +1030,292 @@ __global__ __launch_bounds__(256) void k_render(RenderArgs a) {
 
 hipError_t launch_render(const RenderArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_render, dim3((a.width + 15) / 16, (a.height + 15) / 16), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------
+// Z-sharded raycast.  The march of march_ray is sequential along the ray
+// (sticky quarter step, refinement from the previous sample), so it is split into steps
+// that every rank of the group runs on its own planes, with an all-gather of one 8-byte
+// record per pixel between steps (host side: semtsdf/shard.py):
+//   step 0  coarse march (step = voxel.x): first owned sample with f < voxel.x/2, or -1
+//           when the first sample rejects the ray;
+//   step 1  min over ranks = the global coarse event k.  f_k < 0: the owner of sample
+//           k-1 sends f_{k-1}.  Otherwise the quarter-step march continues from t_k and
+//           each rank sends its first owned sample with f < 0;
+//   step 2  min over ranks = the fine hit j; for j >= 2 the owner of sample j-1 sends it;
+//   final   t_hit = t_s + step * f / (f_prev - f) as in march_ray; the owner of the hit
+//           point shades it (render) or accumulates its association terms (assoc).
+// Sample positions are replayed with the same float additions as march_ray, a sample is
+// evaluated only by the shard owning its base plane (which also holds plane + 1), and
+// every value is computed with the same arithmetic as the single volume, so the
+// composite is bit-identical to the single-volume raycast.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ int2 gather_min(const int2* __restrict__ g, int n, int npx, int px) {
+    int2 best = make_int2(INT_MAX, 0);
+    for (int r = 0; r < n; ++r) {
+        const int2 v = g[(size_t)r * npx + px];
+        if (v.x < best.x) best = v;
+    }
+    return best;
+}
+
+__device__ __forceinline__ float replay_t(float t, int ncoarse, int nfine, float vx) {
+    for (int i = 0; i < ncoarse; ++i) t += vx;
+    const float q = vx / 4.0f;
+    for (int i = 0; i < nfine; ++i) t += q;
+    return t;
+}
+
+struct RayGeo {
+    float ox, oy, oz, dx, dy, dz, t0, t1;
+    bool in;
+};
+
+__device__ __forceinline__ RayGeo shard_ray(const ShardRayArgs& a, int x, int y) {
+    RayGeo r;
+    if (a.kind == 2) ray_assoc(a.cam, x, y, &r.ox, &r.oy, &r.oz, &r.dx, &r.dy, &r.dz);
+    else ray_render(a.cam, x, y, &r.ox, &r.oy, &r.oz, &r.dx, &r.dy, &r.dz);
+    r.in = ray_bounds(a.g, r.ox, r.oy, r.oz, r.dx, r.dy, r.dz, &r.t0, &r.t1);
+    return r;
+}
+
+__device__ __forceinline__ bool owns_at(const ShardRayArgs& a, const RayGeo& r, float t) {
+    return sample_owner(a.g, fmaf(t, r.dz, r.oz)) == a.g.shard;
+}
+
+__device__ __forceinline__ float sample_at(const ShardRayArgs& a, const RayGeo& r, float t) {
+    return sample_sdf(a.g, a.b.sdf, fmaf(t, r.dx, r.ox), fmaf(t, r.dy, r.oy), fmaf(t, r.dz, r.oz));
+}
+
+__global__ __launch_bounds__(256) void k_shard_ray_step(ShardRayArgs a) {
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15);
+    const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= a.width || y >= a.height) return;
+    const int npx = a.width * a.height;
+    const int px = y * a.width + x;
+    const RayGeo r = shard_ray(a, x, y);
+    const float vx = a.g.voxel[0];
+    int2 rec = make_int2(INT_MAX, 0);
+    if (a.step == 0) {
+        if (!r.in) {
+            rec.x = -1;
+        } else {
+            float t = r.t0;
+            bool dead = false;
+            if (owns_at(a, r, t)) {
+                const float f0 = sample_at(a, r, t);
+                if (!(f0 > 0.0f)) { rec.x = -1; dead = true; }
+            }
+            if (!dead) {
+                if (!(t < r.t1)) {
+                    rec.x = -1;
+                } else {
+                    for (int k = 0; t < r.t1; ++k, t += vx) {
+                        if (!owns_at(a, r, t)) continue;
+                        const float f = sample_at(a, r, t);
+                        if (f < vx / 2.0f) { rec = make_int2(k, __float_as_int(f)); break; }
+                    }
+                }
+            }
+        }
+    } else if (a.step == 1) {
+        const int2 c = gather_min(a.gathered, a.g.nshards, npx, px);
+        if (c.x < 0 || c.x == INT_MAX) {
+            a.st.k[px] = -1;
+        } else {
+            const int k = c.x;
+            const float fk = __int_as_float(c.y);
+            a.st.k[px] = k;
+            a.st.fk[px] = fk;
+            if (fk < 0.0f) {
+                a.st.j[px] = 0;
+                const float t = replay_t(r.t0, k - 1, 0, vx);
+                if (owns_at(a, r, t)) rec = make_int2(0, __float_as_int(sample_at(a, r, t)));
+            } else {
+                float t = replay_t(r.t0, k, 0, vx);
+                const float q = vx / 4.0f;
+                for (int j = 1;; ++j) {
+                    t += q;
+                    if (!(t < r.t1)) break;
+                    if (!owns_at(a, r, t)) continue;
+                    const float f = sample_at(a, r, t);
+                    if (f < 0.0f) { rec = make_int2(j, __float_as_int(f)); break; }
+                }
+            }
+        }
+    } else {  // step 2
+        const int k = a.st.k[px];
+        if (k >= 0) {
+            const int2 c = gather_min(a.gathered, a.g.nshards, npx, px);
+            if (a.st.fk[px] < 0.0f) {
+                a.st.fp[px] = __int_as_float(c.y);
+            } else if (c.x == INT_MAX) {
+                a.st.k[px] = -1;  // the quarter-step march ran out: miss
+            } else {
+                const int j = c.x;
+                a.st.j[px] = j;
+                a.st.fj[px] = __int_as_float(c.y);
+                if (j == 1) {
+                    a.st.fp[px] = a.st.fk[px];
+                } else {
+                    const float t = replay_t(r.t0, k, j - 1, vx);
+                    if (owns_at(a, r, t)) rec = make_int2(0, __float_as_int(sample_at(a, r, t)));
+                }
+            }
+        }
+    }
+    a.send[px] = rec;
+}
+
+// Resolve the hit after step 2's gather: returns false on a miss, else t_hit.
+__device__ __forceinline__ bool shard_resolve(const ShardRayArgs& a, const RayGeo& r, int px, int npx, float* t_hit) {
+    const int k = a.st.k[px];
+    if (k < 0) return false;
+    const float vx = a.g.voxel[0];
+    float ts, step, f, fp;
+    if (a.st.fk[px] < 0.0f) {
+        ts = replay_t(r.t0, k, 0, vx);
+        step = vx;
+        f = a.st.fk[px];
+        fp = a.st.fp[px];
+    } else {
+        const int j = a.st.j[px];
+        if (j >= 2) a.st.fp[px] = __int_as_float(gather_min(a.gathered, a.g.nshards, npx, px).y);
+        ts = replay_t(r.t0, k, j, vx);
+        step = vx / 4.0f;
+        f = a.st.fj[px];
+        fp = a.st.fp[px];
+    }
+    *t_hit = ts + step * f / (fp - f);
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_shard_render_final(ShardRayArgs a) {
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15);
+    const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= a.width || y >= a.height) return;
+    const int npx = a.width * a.height;
+    const int px = y * a.width + x;
+    const RayGeo r = shard_ray(a, x, y);
+    float t;
+    int2 rec = make_int2(INT_MAX, 0);
+    if (shard_resolve(a, r, px, npx, &t)) {
+        a.st.t[px] = t;
+        const float hx = fmaf(t, r.dx, r.ox), hy = fmaf(t, r.dy, r.oy), hz = fmaf(t, r.dz, r.oz);
+        if (sample_owner(a.g, hz) == a.g.shard) {
+            uint8_t b = 0, gch = 0, rr = 0;
+            shade_hit(a.g, a.b, tri_setup(a.g, hx, hy, hz), a.kind, a.color_i32, a.palette, &b, &gch, &rr);
+            rec = make_int2(0, (int)((unsigned)b | ((unsigned)gch << 8) | ((unsigned)rr << 16)));
+        }
+    } else {
+        a.st.t[px] = -1.0f;
+        if (a.g.shard == 0) rec = make_int2(0, 0);
+    }
+    a.send[px] = rec;
+}
+
+__global__ __launch_bounds__(256) void k_shard_render_finish(ShardRayArgs a) {
+    const int npx = a.width * a.height;
+    for (int px = blockIdx.x * blockDim.x + threadIdx.x; px < npx; px += gridDim.x * blockDim.x) {
+        const unsigned v = (unsigned)gather_min(a.gathered, a.g.nshards, npx, px).y;
+        a.out_bgr[(size_t)px * 3 + 0] = (uint8_t)(v & 0xFF);
+        a.out_bgr[(size_t)px * 3 + 1] = (uint8_t)((v >> 8) & 0xFF);
+        a.out_bgr[(size_t)px * 3 + 2] = (uint8_t)((v >> 16) & 0xFF);
+        if (a.out_t) a.out_t[px] = a.st.t[px];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_shard_assoc_partial(ShardRayArgs a) {
+    __shared__ AssocLds s;
+    assoc_lds_clear(s);
+    __syncthreads();
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15);
+    const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x < a.width && y < a.height) {
+        const int npx = a.width * a.height;
+        const int px = y * a.width + x;
+        const RayGeo r = shard_ray(a, x, y);
+        float t;
+        float p[kMaxObjects];
+#pragma unroll
+        for (int k = 0; k < kMaxObjects; ++k) p[k] = 0.0f;
+        bool mine;
+        if (shard_resolve(a, r, px, npx, &t)) {
+            const float hx = fmaf(t, r.dx, r.ox), hy = fmaf(t, r.dy, r.oy), hz = fmaf(t, r.dz, r.oz);
+            mine = sample_owner(a.g, hz) == a.g.shard;
+            if (mine) {
+                const Tri tr = tri_setup(a.g, hx, hy, hz);
+#pragma unroll
+                for (int k = 0; k < kMaxObjects; ++k) p[k] = tri_eval(a.b.hist + (uint64_t)k * a.g.nvox, tr);
+            }
+        } else {
+            mine = a.g.shard == 0;  // pixels without a hit contribute once, from shard 0
+        }
+        if (mine) assoc_accumulate(s, p, a.mask[px], a.n_obs, a.eps, a.box_thresh);
+    }
+    __syncthreads();
+    // partial layout: t1[32][32], t3[32][32], t2[32], c1[32], c2[32], c3[32][32] (int64)
+    unsigned long long* P = reinterpret_cast<unsigned long long*>(a.partial);
+    const int NN = kMaxObjects * kMaxObjects;
+    for (int k = threadIdx.x; k < NN; k += 256) {
+        const long long v1 = (&s.t1[0][0])[k];
+        if (v1) atomicAdd(P + k, (unsigned long long)v1);
+        const long long v3 = (&s.t3[0][0])[k];
+        if (v3) atomicAdd(P + NN + k, (unsigned long long)v3);
+        const unsigned c3 = (&s.c3[0][0])[k];
+        if (c3) atomicAdd(P + 2 * NN + 3 * kMaxObjects + k, (unsigned long long)c3);
+    }
+    if (threadIdx.x < kMaxObjects) {
+        const int i = threadIdx.x;
+        if (s.t2[i]) atomicAdd(P + 2 * NN + i, (unsigned long long)s.t2[i]);
+        if (s.c1[i]) atomicAdd(P + 2 * NN + kMaxObjects + i, (unsigned long long)s.c1[i]);
+        if (s.c2[i]) atomicAdd(P + 2 * NN + 2 * kMaxObjects + i, (unsigned long long)s.c2[i]);
+    }
+}
+
+__global__ void k_tables_from_partial(const long long* __restrict__ P, AssocTables* T) {
+    const int NN = kMaxObjects * kMaxObjects;
+    for (int k = threadIdx.x; k < NN; k += blockDim.x) {
+        (&T->t1[0][0])[k] = P[k];
+        (&T->t3[0][0])[k] = P[NN + k];
+        (&T->c3[0][0])[k] = (unsigned)P[2 * NN + 3 * kMaxObjects + k];
+    }
+    if (threadIdx.x < kMaxObjects) {
+        const int i = threadIdx.x;
+        T->t2[i] = P[2 * NN + i];
+        T->c1[i] = (unsigned)P[2 * NN + kMaxObjects + i];
+        T->c2[i] = (unsigned)P[2 * NN + 2 * kMaxObjects + i];
+    }
+}
+
+static dim3 tile_grid(int w, int h) { return dim3((w + 15) / 16, (h + 15) / 16); }
+
+hipError_t launch_shard_ray_step(const ShardRayArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_shard_ray_step, tile_grid(a.width, a.height), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_shard_render_final(const ShardRayArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_shard_render_final, tile_grid(a.width, a.height), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_shard_render_finish(const ShardRayArgs& a, hipStream_t s) {
+    const int npx = a.width * a.height;
+    int blocks = (npx + 255) / 256;
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(k_shard_render_finish, dim3(blocks), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_shard_assoc_partial(const ShardRayArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_shard_assoc_partial, tile_grid(a.width, a.height), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_tables_from_partial(const long long* reduced, AssocTables* t, hipStream_t s) {
+    hipLaunchKernelGGL(k_tables_from_partial, dim3(1), dim3(256), 0, s, reduced, t);
     return hipGetLastError();
 }
 

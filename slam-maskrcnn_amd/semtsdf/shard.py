@@ -92,3 +92,236 @@ class ShardLayout:
                 if not np.array_equal(a[:, :, li], locals_[o][:, :, lo]):
                     return False
         return True
+
+
+# ---------------------------------------------------------------------------------------
+# Z-sharded raycast / association protocol (include/semtsdf.h "Z-sharded raycast").
+# ---------------------------------------------------------------------------------------
+def _run_ray_protocol(members, gathered_ptr, allgather, kind, cam, c, stream):
+    """members: [(Volume, send_ptr)] of the shards driven by this process (one per rank in
+    a distributed group; all of them for an in-process group).  allgather() fills the
+    gathered buffer [nshards][record] from every shard's send buffer, in shard order."""
+    import ctypes as C
+
+    from . import _lib as L
+
+    lib = L.load()
+    camv = L.f32(cam, 16)
+    cv = L.f32(c, 3) if c is not None else None
+    nsteps = C.c_int()
+    rec = C.c_size_t()
+    for vol, _ in members:
+        L.check(lib.semtsdf_shard_ray_begin(vol.handle, int(kind), L.ptr(camv), L.ptr(cv), C.byref(rec),
+                                            C.byref(nsteps)))
+    for step in range(nsteps.value):
+        for vol, send in members:
+            L.check(lib.semtsdf_shard_ray_step(vol.handle, step, C.c_void_p(gathered_ptr) if step else None,
+                                               C.c_void_p(send), stream))
+        allgather()
+    return rec.value
+
+
+class LocalShardGroup:
+    """All shards of a Z-sharded volume driven from one process (tests, or several shards
+    per GPU): the all-gather is a device-to-device copy on one stream."""
+
+    def __init__(self, vols):
+        from . import _lib as L
+        from .volume import DeviceBuffer
+
+        self.vols = list(vols)
+        self.n = len(self.vols)
+        v0 = self.vols[0]
+        self.W, self.H = v0.W, v0.H
+        npx = self.W * self.H
+        self.rec = 8 * npx
+        self.send = [DeviceBuffer(self.rec) for _ in self.vols]
+        self.gathered = DeviceBuffer(self.n * self.rec)
+        self.partial = [DeviceBuffer(8 * L.ASSOC_PARTIAL_LEN) for _ in self.vols]
+        self.reduced = DeviceBuffer(8 * L.ASSOC_PARTIAL_LEN)
+        self.stream = v0.stream  # every call goes on shard 0's stream: one order for all
+
+    def _s(self):
+        import ctypes as C
+
+        return C.c_void_p(self.stream)
+
+    def _allgather(self):
+        import ctypes as C
+
+        from . import _lib as L
+
+        lib = L.load()
+        for r, sb in enumerate(self.send):
+            L.check(lib.semtsdf_memcpy(C.c_void_p(self.gathered.ptr + r * self.rec), C.c_void_p(sb.ptr), self.rec,
+                                       3, self._s()))
+
+    def raycast_dev(self, s2w, c, mode, out_ptr: int, t_ptr: int | None = None):
+        import ctypes as C
+
+        from . import _lib as L
+
+        members = list(zip(self.vols, [b.ptr for b in self.send]))
+        _run_ray_protocol(members, self.gathered.ptr, self._allgather, mode, s2w, c, self._s())
+        # every shard can composite the gathered records; shard 0 writes the image
+        L.check(L.load().semtsdf_shard_render_finish(self.vols[0].handle, C.c_void_p(self.gathered.ptr),
+                                                     C.c_void_p(out_ptr), C.c_void_p(t_ptr) if t_ptr else None,
+                                                     self._s()))
+
+    def raycast(self, s2w, c, mode, want_t=False):
+        import numpy as np
+
+        from .volume import DeviceBuffer
+
+        npx = self.W * self.H
+        ob = DeviceBuffer(npx * 3)
+        tb = DeviceBuffer(npx * 4) if want_t else None
+        self.raycast_dev(s2w, c, mode, ob.ptr, tb.ptr if tb else None)
+        out = np.zeros((self.H, self.W, 3), np.uint8)
+        ob.download(out, self.stream)
+        t = None
+        if tb:
+            t = np.zeros((self.H, self.W), np.float32)
+            tb.download(t, self.stream)
+        self.vols[0].sync()
+        return (out, t) if want_t else out
+
+    def associate_dev(self, mask_ptrs, E, want_stats=False):
+        """mask_ptrs: one device mask per shard (identical contents); each is relabelled."""
+        import ctypes as C
+
+        from . import _lib as L
+
+        lib = L.load()
+        members = list(zip(self.vols, [b.ptr for b in self.send]))
+        _run_ray_protocol(members, self.gathered.ptr, self._allgather, L.RAY_ASSOC, E, None, self._s())
+        for v, m, pb in zip(self.vols, mask_ptrs, self.partial):
+            L.check(lib.semtsdf_shard_assoc_partial(v.handle, C.c_void_p(self.gathered.ptr), C.c_void_p(m),
+                                                    C.c_void_p(pb.ptr), self._s()))
+        _sum_int64_dev([pb.ptr for pb in self.partial], self.reduced.ptr, L.ASSOC_PARTIAL_LEN, self.stream)
+        stats = []
+        for v, m in zip(self.vols, mask_ptrs):
+            st = L.AssocStats() if want_stats else None
+            L.check(lib.semtsdf_shard_assoc_apply(v.handle, C.c_void_p(self.reduced.ptr), C.c_void_p(m),
+                                                  C.byref(st) if st is not None else None, self._s()))
+            stats.append(st)
+        return stats
+
+    def parse_frame_dev(self, depth_ptr, rgb_ptr, mask_ptrs, E):
+        import ctypes as C
+
+        from . import _lib as L
+
+        if self.vols[0].state().n_obs > 0:
+            self.associate_dev(mask_ptrs, E)
+        for v, m in zip(self.vols, mask_ptrs):
+            v.integrate_dev(depth_ptr, rgb_ptr, m, E, self.stream)
+            L.check(L.load().semtsdf_shard_note_integrated(v.handle, C.c_void_p(m), self._s()))
+
+
+def _sum_int64_dev(ptrs, out_ptr, n, stream):
+    """out = sum of the int64 vectors at ptrs (device), via host staging (tests only: the
+    distributed path uses an all-reduce)."""
+    import ctypes as C
+
+    import numpy as np
+
+    from . import _lib as L
+
+    lib = L.load()
+    acc = np.zeros(n, np.int64)
+    tmp = np.zeros(n, np.int64)
+    for p in ptrs:
+        L.check(lib.semtsdf_memcpy(L.ptr(tmp), C.c_void_p(p), 8 * n, 2, C.c_void_p(stream)))
+        L.check(lib.semtsdf_stream_sync(C.c_void_p(stream)))
+        acc += tmp
+    L.check(lib.semtsdf_memcpy(C.c_void_p(out_ptr), L.ptr(acc), 8 * n, 1, C.c_void_p(stream)))
+
+
+class DistShardGroup:
+    """One shard per rank of a torch.distributed process group (RCCL on MI355X; gloo for
+    CPU-side rehearsal).  Buffers are torch CUDA tensors; every library call goes on the
+    current torch stream so collectives and kernels are stream-ordered."""
+
+    def __init__(self, vol, group=None):
+        import torch
+        import torch.distributed as dist
+
+        from . import _lib as L
+
+        self.vol = vol
+        self.group = group
+        self.dist = dist
+        self.n = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        if vol.params.z_nshards != self.n or vol.params.z_shard != self.rank:
+            raise ValueError("volume shard does not match the process group rank")
+        self.W, self.H = vol.W, vol.H
+        npx = self.W * self.H
+        dev = torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
+        self.send = torch.empty(2 * npx, dtype=torch.int32, device=dev)
+        self.gathered = torch.empty(self.n * 2 * npx, dtype=torch.int32, device=dev)
+        self.partial = torch.empty(L.ASSOC_PARTIAL_LEN, dtype=torch.int64, device=dev)
+        self.nccl = dist.get_backend(group) == "nccl"
+        self._parts = None if self.nccl else list(self.gathered.view(self.n, 2 * npx).unbind(0))
+
+    def _stream(self):
+        import ctypes as C
+
+        import torch
+
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _allgather(self):
+        if self.nccl:
+            self.dist.all_gather_into_tensor(self.gathered, self.send, group=self.group)
+        else:
+            self.dist.all_gather(self._parts, self.send, group=self.group)
+
+    def raycast_dev(self, s2w, c, mode, out_ptr: int, t_ptr: int | None = None):
+        import ctypes as C
+
+        from . import _lib as L
+
+        _run_ray_protocol([(self.vol, self.send.data_ptr())], self.gathered.data_ptr(), self._allgather, mode, s2w,
+                          c, self._stream())
+        L.check(L.load().semtsdf_shard_render_finish(self.vol.handle, C.c_void_p(self.gathered.data_ptr()),
+                                                     C.c_void_p(out_ptr), C.c_void_p(t_ptr) if t_ptr else None,
+                                                     self._stream()))
+
+    def raycast(self, s2w, c, mode, want_t=False):
+        import torch
+
+        out = torch.empty((self.H, self.W, 3), dtype=torch.uint8, device=self.device)
+        t = torch.empty((self.H, self.W), dtype=torch.float32, device=self.device) if want_t else None
+        self.raycast_dev(s2w, c, mode, out.data_ptr(), t.data_ptr() if t is not None else None)
+        return (out, t) if want_t else out
+
+    def associate_dev(self, mask_ptr: int, E, want_stats=False):
+        import ctypes as C
+
+        from . import _lib as L
+
+        lib = L.load()
+        _run_ray_protocol([(self.vol, self.send.data_ptr())], self.gathered.data_ptr(), self._allgather,
+                          L.RAY_ASSOC, E, None, self._stream())
+        L.check(lib.semtsdf_shard_assoc_partial(self.vol.handle, C.c_void_p(self.gathered.data_ptr()),
+                                                C.c_void_p(mask_ptr), C.c_void_p(self.partial.data_ptr()),
+                                                self._stream()))
+        self.dist.all_reduce(self.partial, op=self.dist.ReduceOp.SUM, group=self.group)
+        st = L.AssocStats() if want_stats else None
+        L.check(lib.semtsdf_shard_assoc_apply(self.vol.handle, C.c_void_p(self.partial.data_ptr()),
+                                              C.c_void_p(mask_ptr), C.byref(st) if st is not None else None,
+                                              self._stream()))
+        return st
+
+    def parse_frame_dev(self, depth_ptr: int, rgb_ptr: int, mask_ptr: int, E):
+        import ctypes as C
+
+        from . import _lib as L
+
+        if self.vol.state().n_obs > 0:
+            self.associate_dev(mask_ptr, E)
+        self.vol.integrate_dev(depth_ptr, rgb_ptr, mask_ptr, E, self._stream())
+        L.check(L.load().semtsdf_shard_note_integrated(self.vol.handle, C.c_void_p(mask_ptr), self._stream()))

@@ -304,3 +304,75 @@ def test_sharded_handles_equal_single_volume(S, oracle, stream, nshards, chunk):
     for sh in shards:
         sh.close()
     vol.close()
+
+
+def _shard_handles(S, p, nshards, chunk):
+    semtsdf, L = S
+    shards = []
+    for sidx in range(nshards):
+        q = semtsdf.default_params(64, KI, 640, 480)
+        for fld in ("dim", "vol_start", "vol_end", "voxel", "K", "Kinv"):
+            getattr(q, fld)[:] = getattr(p, fld)[:]
+        q.mu, q.flags = p.mu, p.flags
+        q.z_nshards, q.z_shard, q.z_chunk = nshards, sidx, chunk
+        shards.append(semtsdf.Volume(q, 0))
+    return shards
+
+
+@pytest.mark.parametrize("nshards,chunk", [(2, 8), (3, 5), (4, 16), (1, 64)])
+def test_sharded_pipeline_equals_single_volume(S, oracle, stream, nshards, chunk):
+    """The Z-sharded association + integrate + raycast protocol (k_shard_*, host
+    LocalShardGroup) reproduces the single-volume pipeline bit for bit: relabelled masks,
+    decisions, the gathered volume, rendered images and hit distances."""
+    from semtsdf.shard import LocalShardGroup, ShardLayout
+    from semtsdf.volume import DeviceBuffer
+
+    st, frames = stream
+    semtsdf, L = S
+    dims = (48, 40, 64)
+    p, vol, g, ost = make(S, oracle, dims, frames[0], 0x3)
+    shards = _shard_handles(S, p, nshards, chunk)
+    grp = LocalShardGroup(shards)
+    npx = 640 * 480
+    dbuf, rbuf = DeviceBuffer(npx * 2), DeviceBuffer(npx * 3)
+    mbufs = [DeviceBuffer(npx) for _ in shards]
+    for k in range(1, 6):
+        fr = frames[k]
+        E = (fr.w2c @ frames[0].c2w).astype(np.float32)
+        m_single = np.ascontiguousarray(fr.mask.copy())
+        stats = vol.parse_frame(fr.depth, fr.rgb, m_single, E)
+        dbuf.upload(fr.depth, grp.stream)
+        rbuf.upload(fr.rgb, grp.stream)
+        for mb in mbufs:
+            mb.upload(fr.mask, grp.stream)
+        if k >= 2:
+            sstats = grp.associate_dev([mb.ptr for mb in mbufs], E, want_stats=True)
+            for ss in sstats:
+                assert list(ss.assigned_prev) == list(stats.assigned_prev)
+                assert ss.num_objs == stats.num_objs and bytes(ss.lut) == bytes(stats.lut)
+        for sh, mb in zip(shards, mbufs):
+            sh.integrate_dev(dbuf.ptr, rbuf.ptr, mb.ptr, E, grp.stream)
+            L.check(L.load().semtsdf_shard_note_integrated(sh.handle, L.ptr(mb.ptr), L.ptr(grp.stream)))
+        for mb in mbufs:
+            got = np.zeros(npx, np.uint8)
+            mb.download(got, grp.stream)
+            shards[0].sync()
+            assert np.array_equal(got, m_single.reshape(-1)), f"frame {k}"
+        for sh in shards:
+            assert sh.state().num_objs == vol.state().num_objs and sh.state().n_obs == k
+    lay = ShardLayout(dims[2], nshards, chunk)
+    full = vol.download(hist=True)
+    parts = [sh.download(hist=True)["hist"].reshape(dims[0], dims[1], -1, 32) for sh in shards]
+    assert np.array_equal(lay.gather(parts, dims[0], dims[1]), full["hist"].reshape(dims + (32,)))
+    dist = float(np.mean(frames[0].depth[frames[0].depth > 0]) / 5000.0)
+    for mode in (L.RENDER_LABEL, L.RENDER_COLOR):
+        for angle in (0.0, 0.3):
+            s2w, c = semtsdf.orbit_camera(list(p.Kinv), angle, dist)
+            img, t = vol.raycast(s2w, c, mode, want_t=True)
+            simg, stt = grp.raycast(s2w, c, mode, want_t=True)
+            assert (t >= 0).mean() > 0.2
+            assert np.array_equal(stt.view(np.uint32), t.view(np.uint32)), (mode, angle)
+            assert np.array_equal(simg, img), (mode, angle)
+    for sh in shards:
+        sh.close()
+    vol.close()

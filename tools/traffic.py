@@ -1,0 +1,39 @@
+"""Per-launch HBM bytes of one kernel from rocprofv3 PMC passes (tools/pmc_integrate.sh).
+
+FETCH_SIZE and WRITE_SIZE (KiB) are collected in separate passes (they do not fit one TCC
+pass on gfx950).  Per MI355X_MICROARCH.md §HBM, FETCH_SIZE reports half the bytes of wide
+coalesced reads on gfx950, so it is doubled; WRITE_SIZE is taken as is.
+Usage: python tools/traffic.py PMC_DIR KERNEL_SUBSTRING OUT_JSON DIM [N_GPUS]
+"""
+import collections
+import csv
+import glob
+import json
+import sys
+
+
+def main():
+    d, pat, out, dim = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
+    n_gpus = int(sys.argv[5]) if len(sys.argv) > 5 else 1
+    agg = collections.defaultdict(list)
+    for f in sorted(glob.glob(f"{d}/p*/run_counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            if pat in r["Kernel_Name"]:
+                agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    if "FETCH_SIZE" not in agg or "WRITE_SIZE" not in agg:
+        raise SystemExit(f"no FETCH_SIZE/WRITE_SIZE rows for {pat!r} under {d}")
+    fetch_kib = sum(agg["FETCH_SIZE"]) / len(agg["FETCH_SIZE"])
+    write_kib = sum(agg["WRITE_SIZE"]) / len(agg["WRITE_SIZE"])
+    fetch = 2.0 * fetch_kib * 1024.0
+    write = write_kib * 1024.0
+    rec = {"kernel": pat, "dim": dim, "n_gpus": n_gpus, "dispatches": len(agg["FETCH_SIZE"]),
+           "fetch_size_kib_raw": fetch_kib, "write_size_kib_raw": write_kib,
+           "fetch_bytes": fetch, "write_bytes": write, "bytes_per_launch": fetch + write,
+           "correction": "FETCH_SIZE x2 (gfx950 wide-read tally), WRITE_SIZE x1"}
+    with open(out, "w") as f:
+        json.dump(rec, f, indent=1)
+    print(json.dumps(rec))
+
+
+if __name__ == "__main__":
+    main()
