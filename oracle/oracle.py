@@ -57,6 +57,9 @@ def lib():
         _lib.oracle_render.argtypes = [P, P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P, P, C.c_int,
                                        C.c_int]
         _lib.oracle_render.restype = None
+        _lib.oracle_shard_render_step.argtypes = [P, P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, C.c_int,
+                                                  C.c_int, C.c_int, C.c_int, P, P, P, P, P]
+        _lib.oracle_shard_render_step.restype = None
         _lib.oracle_place.argtypes = [P, C.c_int, C.c_int, P, P, C.c_double, C.c_int, P]
         _lib.oracle_place.restype = C.c_int
         _lib.oracle_orbit_camera.argtypes = [P, C.c_float, C.c_float, P, P]
@@ -155,6 +158,16 @@ def render(g: OGeom, s2w, c, W, H, mode, sdf, hist=None, color=None, color_i32=F
                         _p(np.ascontiguousarray(c, np.float32).reshape(3)), W, H, int(mode), int(color_i32), _p(sdf),
                         _p(hist), _p(color), _p(out), _p(t), 0, H)
     return out.reshape(H, W, 3), t.reshape(H, W)
+
+
+def shard_render_step(g: OGeom, s2w, c, W, H, mode, sdf, hist, color, step, shard, nshards, chunk, gathered,
+                      send, state, out=None, out_t=None, color_i32=False):
+    """One step of the Z-sharded render protocol for virtual shard `shard` (see
+    oracle_shard_render_step).  gathered/send: int32 [.., H*W*2]; state int32 [6*H*W]."""
+    lib().oracle_shard_render_step(_p(g.dims), _p(g.geo), _p(np.ascontiguousarray(s2w, np.float32).reshape(16)),
+                                   _p(np.ascontiguousarray(c, np.float32).reshape(3)), W, H, int(mode),
+                                   int(color_i32), _p(sdf), _p(hist), _p(color), int(step), int(shard),
+                                   int(nshards), int(chunk), _p(gathered), _p(send), _p(state), _p(out), _p(out_t))
 
 
 def place(depth, Kinv16, dims, mean_depth, mode):

@@ -17,6 +17,7 @@
  *   oracle_render            src/SfM_CUDA/viewer.cu:17-86, palette viewer.cu:93-126
  *   oracle_place             src/SfM_CUDA/tsdf.cu:173-199 and src/TSDF_Python/tsdf.py:32-47
  *   oracle_orbit_camera      src/SfM_CUDA/viewer.cu:140-146
+ *   oracle_shard_render_step the Z-sharded split of the march above (no reference counterpart)
  * Where the reference reads out of range (trilinear neighbours at the far faces,
  * utils.cu:103-113) the oracle clamps indices to the volume, which is the semantics the
  * build defines for that case.
@@ -407,6 +408,212 @@ void oracle_render(const int32_t* dims, const float* geo, const float* s2w, cons
                     o[ch] = (uint8_t)(int)o_tri_eval(d, &tr);
                 }
             }
+        }
+}
+
+/* ---------------------------------------------------------------- Z-sharded render
+ * Restatement of the sharded raycast protocol (k_shard_ray_step / k_shard_render_final /
+ * k_shard_render_finish in semtsdf_kernels.hip) for the tests: virtual shard `shard` of
+ * `nshards` (chunks of `chunk` planes dealt round-robin) evaluates only the samples whose
+ * base plane it owns; sampling reads the full volume, which equals the shard's local copy
+ * (halo planes are integrated identically).  Records are int32 pairs {key, value bits};
+ * the combine is the minimum key over shards.  state: 6 x npx words (k, fk, j, fj, fp, t).
+ * step 0..3 as in the kernels; step 4 = composite (gathered of step 3 -> out_bgr/out_t). */
+static int o_owner(const ogeom* g, float pz, int chunk, int nshards) {
+    const float iz = (pz - g->start[2]) / g->voxel[2];
+    const int zc = o_clamp(o_f2i_rd(iz), 0, g->dz - 1);
+    return (zc / chunk) % nshards;
+}
+
+static void o_gmin(const int32_t* gth, int n, size_t npx, size_t px, int32_t* key, int32_t* val) {
+    int32_t bk = INT_MAX, bv = 0;
+    for (int r = 0; r < n; ++r) {
+        const int32_t k = gth[((size_t)r * npx + px) * 2], v = gth[((size_t)r * npx + px) * 2 + 1];
+        if (k < bk) { bk = k; bv = v; }
+    }
+    *key = bk;
+    *val = bv;
+}
+
+static float o_bits_f(int32_t v) { float f; memcpy(&f, &v, 4); return f; }
+static int32_t o_f_bits(float f) { int32_t v; memcpy(&v, &f, 4); return v; }
+
+static float o_replay(float t, int ncoarse, int nfine, float vx) {
+    for (int i = 0; i < ncoarse; ++i) t += vx;
+    const float q = vx / 4.0f;
+    for (int i = 0; i < nfine; ++i) t += q;
+    return t;
+}
+
+void oracle_shard_render_step(const int32_t* dims, const float* geo, const float* s2w, const float* c, int width,
+                              int height, int mode, int color_i32, const float* sdf, const uint32_t* hist,
+                              const void* color, int step, int shard, int nshards, int chunk,
+                              const int32_t* gathered, int32_t* send, int32_t* state, uint8_t* out_bgr,
+                              float* out_t) {
+    const ogeom g = mk_geom(dims, geo);
+    const size_t npx = (size_t)width * height;
+    int32_t* sk = state;
+    float* sfk = (float*)(state + npx);
+    int32_t* sj = state + 2 * npx;
+    float* sfj = (float*)(state + 3 * npx);
+    float* sfp = (float*)(state + 4 * npx);
+    float* st = (float*)(state + 5 * npx);
+    const float vx = g.voxel[0];
+    for (int y = 0; y < height; ++y)
+        for (int x = 0; x < width; ++x) {
+            const size_t px = (size_t)y * width + x;
+            if (step == 4) {
+                int32_t k, v;
+                o_gmin(gathered, nshards, npx, px, &k, &v);
+                out_bgr[px * 3 + 0] = (uint8_t)(v & 0xFF);
+                out_bgr[px * 3 + 1] = (uint8_t)((v >> 8) & 0xFF);
+                out_bgr[px * 3 + 2] = (uint8_t)((v >> 16) & 0xFF);
+                if (out_t) out_t[px] = st[px];
+                continue;
+            }
+            const float fx = (float)x, fy = (float)y;
+            const float tx = o_dot3(s2w[0], s2w[1], s2w[2], fx, fy, 1.0f) + s2w[3];
+            const float ty = o_dot3(s2w[4], s2w[5], s2w[6], fx, fy, 1.0f) + s2w[7];
+            const float tz = o_dot3(s2w[8], s2w[9], s2w[10], fx, fy, 1.0f) + s2w[11];
+            const float rx = tx - c[0], ry = ty - c[1], rz = tz - c[2];
+            const float inv = 1.0f / sqrtf(o_dot3(rx, ry, rz, rx, ry, rz));
+            const float dx = rx * inv, dy = ry * inv, dz = rz * inv;
+            const float ox = c[0], oy = c[1], oz = c[2];
+            /* slab test of o_march */
+            const float ivx = 1.0f / dx, ivy = 1.0f / dy, ivz = 1.0f / dz;
+            const float tbx = ivx * (g.start[0] - ox), tby = ivy * (g.start[1] - oy), tbz = ivz * (g.start[2] - oz);
+            const float ttx = ivx * (g.end[0] - ox), tty = ivy * (g.end[1] - oy), ttz = ivz * (g.end[2] - oz);
+            float tnear = fmaxf(fmaxf(fminf(ttx, tbx), fminf(tty, tby)), fminf(ttz, tbz));
+            tnear = fmaxf(tnear, 0.01f);
+            float tfar = fminf(fminf(fmaxf(ttx, tbx), fmaxf(tty, tby)), fmaxf(ttz, tbz));
+            tfar = fminf(tfar, 100.0f);
+            const int in = !(tnear > tfar);
+            const float t0 = tnear + 1e-6f, t1 = tfar - 1e-6f;
+#define OWNS(t) (o_owner(&g, fmaf((t), dz, oz), chunk, nshards) == shard)
+#define SAMPLE(t) o_sample_sdf(&g, sdf, fmaf((t), dx, ox), fmaf((t), dy, oy), fmaf((t), dz, oz))
+            int32_t rk = INT_MAX, rv = 0;
+            if (step == 0) {
+                if (!in) {
+                    rk = -1;
+                } else {
+                    float t = t0;
+                    int dead = 0;
+                    if (OWNS(t) && !(SAMPLE(t) > 0.0f)) { rk = -1; dead = 1; }
+                    if (!dead) {
+                        if (!(t < t1)) rk = -1;
+                        else
+                            for (int k = 0; t < t1; ++k, t += vx) {
+                                if (!OWNS(t)) continue;
+                                const float f = SAMPLE(t);
+                                if (f < vx / 2.0f) { rk = k; rv = o_f_bits(f); break; }
+                            }
+                    }
+                }
+            } else if (step == 1) {
+                int32_t k, v;
+                o_gmin(gathered, nshards, npx, px, &k, &v);
+                if (k < 0 || k == INT_MAX) {
+                    sk[px] = -1;
+                } else {
+                    const float fk = o_bits_f(v);
+                    sk[px] = k;
+                    sfk[px] = fk;
+                    if (fk < 0.0f) {
+                        sj[px] = 0;
+                        const float t = o_replay(t0, k - 1, 0, vx);
+                        if (OWNS(t)) { rk = 0; rv = o_f_bits(SAMPLE(t)); }
+                    } else {
+                        float t = o_replay(t0, k, 0, vx);
+                        const float q = vx / 4.0f;
+                        for (int j = 1;; ++j) {
+                            t += q;
+                            if (!(t < t1)) break;
+                            if (!OWNS(t)) continue;
+                            const float f = SAMPLE(t);
+                            if (f < 0.0f) { rk = j; rv = o_f_bits(f); break; }
+                        }
+                    }
+                }
+            } else if (step == 2) {
+                const int k = sk[px];
+                if (k >= 0) {
+                    int32_t ck, cv;
+                    o_gmin(gathered, nshards, npx, px, &ck, &cv);
+                    if (sfk[px] < 0.0f) {
+                        sfp[px] = o_bits_f(cv);
+                    } else if (ck == INT_MAX) {
+                        sk[px] = -1;
+                    } else {
+                        sj[px] = ck;
+                        sfj[px] = o_bits_f(cv);
+                        if (ck == 1) {
+                            sfp[px] = sfk[px];
+                        } else {
+                            const float t = o_replay(t0, k, ck - 1, vx);
+                            if (OWNS(t)) { rk = 0; rv = o_f_bits(SAMPLE(t)); }
+                        }
+                    }
+                }
+            } else { /* step 3: resolve the hit, shade by the owner of the hit point */
+                const int k = sk[px];
+                if (k < 0) {
+                    st[px] = -1.0f;
+                    if (shard == 0) { rk = 0; rv = 0; }
+                } else {
+                    float ts, stp, f, fp;
+                    if (sfk[px] < 0.0f) {
+                        ts = o_replay(t0, k, 0, vx);
+                        stp = vx;
+                        f = sfk[px];
+                        fp = sfp[px];
+                    } else {
+                        const int j = sj[px];
+                        if (j >= 2) {
+                            int32_t ck, cv;
+                            o_gmin(gathered, nshards, npx, px, &ck, &cv);
+                            sfp[px] = o_bits_f(cv);
+                        }
+                        ts = o_replay(t0, k, j, vx);
+                        stp = vx / 4.0f;
+                        f = sfj[px];
+                        fp = sfp[px];
+                    }
+                    const float t = ts + stp * f / (fp - f);
+                    st[px] = t;
+                    const float hx = fmaf(t, dx, ox), hy = fmaf(t, dy, oy), hz = fmaf(t, dz, oz);
+                    if (o_owner(&g, hz, chunk, nshards) == shard) {
+                        uint8_t o[3] = {0, 0, 0};
+                        if (mode == 0) {
+                            float cnt[OMAX];
+                            o_sample_hist(&g, hist, hx, hy, hz, cnt);
+                            float best = 0.0f;
+                            int obj = 0;
+                            for (int b = 0; b < OMAX; ++b)
+                                if (cnt[b] > best) { best = cnt[b]; obj = b; }
+                            if (obj > 0) {
+                                o[0] = o_palette[obj * 3 + 2];
+                                o[1] = o_palette[obj * 3 + 1];
+                                o[2] = o_palette[obj * 3 + 0];
+                            }
+                        } else {
+                            const otri tr = o_tri(&g, hx, hy, hz);
+                            for (int ch = 0; ch < 3; ++ch) {
+                                float d[8];
+                                for (int kk = 0; kk < 8; ++kk)
+                                    d[kk] = color_i32 ? (float)((const int32_t*)color)[tr.idx[kk] * 3 + ch]
+                                                      : (float)((const uint8_t*)color)[tr.idx[kk] * 3 + ch];
+                                o[ch] = (uint8_t)(int)o_tri_eval(d, &tr);
+                            }
+                        }
+                        rk = 0;
+                        rv = (int32_t)((uint32_t)o[0] | ((uint32_t)o[1] << 8) | ((uint32_t)o[2] << 16));
+                    }
+                }
+            }
+#undef OWNS
+#undef SAMPLE
+            send[px * 2] = rk;
+            send[px * 2 + 1] = rv;
         }
 }
 

@@ -352,7 +352,7 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateArgs a, UnitGrid ug)
             const int x = (int)(uxy % ug.nux);
             const int y = (int)(uxy / ug.nux) * UY + (lane >> 3);
             const int l0 = (int)(u / (ug.nux * ug.nuy)) * UZ + (lane & 7) * 4;
-            const bool row_ok = (y < g.dimy) && (l0 < g.lz);
+            const bool row_ok = (y < g.dimy) & (l0 < g.lz);
             const float px = fmaf((float)x, g.voxel[0], g.start[0]);
             const float py = fmaf((float)y, g.voxel[1], g.start[1]);
             const uint64_t v = (uint64_t)x * plane + (uint64_t)y * (uint64_t)g.zs + (uint64_t)l0;
@@ -365,10 +365,10 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateArgs a, UnitGrid ug)
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 int gz = l0 + k;
-                bool zok = row_ok && (l0 + k < g.lz);
+                bool zok = row_ok & (l0 + k < g.lz);
                 if (SHARD) {
                     gz = local_to_global_z(g, l0 + k);
-                    zok = zok && gz < g.dimz;
+                    zok = zok & (gz < g.dimz);
                 }
                 const float pz = fmaf((float)gz, g.voxel[2], g.start[2]);
                 const float qx = dot3(a.E[0], a.E[1], a.E[2], px, py, pz) + a.E[3];
@@ -384,19 +384,20 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateArgs a, UnitGrid ug)
                     sy = dot3(a.K[3], a.K[4], a.K[5], qx, qy, qz[k]);
                     sz = dot3(a.K[6], a.K[7], a.K[8], qx, qy, qz[k]);
                 }
-                // floor(sx/sz), floor(sy/sz) through the reciprocal (see floor_div); lanes
-                // whose quotient is too close to an integer are redone exactly below
+                // floor(sx/sz), floor(sy/sz) through the reciprocal.  |qu - RN(sx/sz)| <=
+                // 2^-22 |qu| (v_rcp_f32 is within 1 ulp, plus the rounding of the product), so
+                // when qu - tol and qu + tol (tol = 2^-21 |qu|) floor to the same integer, so
+                // does the IEEE quotient.  NaN/Inf and near-integer quotients fail the test and
+                // are redone exactly below; a quotient that is huge but "fast" is off-image
+                // either way.  Bitwise &, not &&: no per-voxel branches.
                 const float r = __builtin_amdgcn_rcpf(sz);
                 const float qu = sx * r, qv = sy * r;
-                const float fu = floorf(qu), fvv = floorf(qv);
-                const float tu = fabsf(qu) * 0x1p-19f, tv = fabsf(qv) * 0x1p-19f;
-                const bool fast = (qu - fu > tu) && (qu - fu < 1.0f - tu) && (qv - fvv > tv) &&
-                                  (qv - fvv < 1.0f - tv) && fabsf(sz) > 1.0e-30f && fabsf(qu) < 8.0e6f &&
-                                  fabsf(qv) < 8.0e6f;
-                const int ix = (int)fu, iy = (int)fvv;
-                const bool in = zok && ix >= 0 && ix < a.width && iy >= 0 && iy < a.height;
-                img[k] = in ? iy * a.width + ix : -1;
-                if (zok && !fast) slow |= 1u << k;
+                const float tu = fabsf(qu) * 0x1p-21f, tv = fabsf(qv) * 0x1p-21f;
+                const float fu = floorf(qu - tu), fvv = floorf(qv - tv);
+                const bool fast = (fu == floorf(qu + tu)) & (fvv == floorf(qv + tv));
+                const bool in = zok & (fu >= 0.0f) & (fu < (float)a.width) & (fvv >= 0.0f) & (fvv < (float)a.height);
+                img[k] = in ? (int)fvv * a.width + (int)fu : -1;
+                slow |= ((zok & !fast) ? 1u : 0u) << k;
                 sxv[k] = sx; syv[k] = sy; szv[k] = sz;
             }
             if (slow) {  // rare: exact IEEE quotients
@@ -418,11 +419,11 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateArgs a, UnitGrid ug)
             for (int k = 0; k < 4; ++k) {
                 const float d = img[k] >= 0 ? dm[k] : 0.0f;
                 float diff = d - qz[k];
-                const bool t = (d != 0.0f) && (diff > -g.mu);
+                const bool t = (d != 0.0f) & (diff > -g.mu);
                 diff = (diff > g.mu) ? g.mu : diff;
-                fv[k] = (a.debug == 7) ? diff * __builtin_amdgcn_rcpf(g.mu) : diff / g.mu;
+                fv[k] = diff / g.mu;
                 tmask |= (t ? 1u : 0u) << k;
-                gmask |= ((t && (!GATE || fv[k] < a.gate)) ? 1u : 0u) << k;
+                gmask |= ((t & (!GATE || fv[k] < a.gate)) ? 1u : 0u) << k;
             }
             if (COUNT) {
                 n_touch += __popc(tmask);
@@ -467,8 +468,7 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateArgs a, UnitGrid ug)
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const bool t = (tmask >> k) & 1u;
-                const float upd = (a.debug == 7) ? fmaf(so[k], (float)wo[k], fv[k]) * __builtin_amdgcn_rcpf((float)(wo[k] + 1))
-                                                 : fmaf(so[k], (float)wo[k], fv[k]) / (float)(wo[k] + 1);
+                const float upd = fmaf(so[k], (float)wo[k], fv[k]) / (float)(wo[k] + 1);
                 sn[k] = t ? upd : so[k];
                 wn[k] = wo[k] + (t ? 1 : 0);
             }

@@ -71,6 +71,19 @@ def _rank_main(rank, world, port, out_q):
             dist.gather(hist_local, hbufs, dst=0)
         else:
             dist.gather(hist_local, None, dst=0)
+        # sharded render protocol over gloo: every rank steps its shard, records are
+        # all-gathered between steps; the composite must equal the single-volume render
+        full_r = O.OState([D] * 3, np.float32(pl["mu"]), semantic=True)
+        for f in fr[1:]:
+            E = (f.w2c @ fr[0].c2w).astype(np.float32)
+            O.integrate(g, full_r, _K(), E, f.depth, f.rgb, f.gt_ids, flags=0x3)
+        img, t_img = _shard_render(O, g, full_r, pl, fr, lambda send: _gloo_allgather(dist, send, world), rank, world,
+                                   lay.chunk)
+        if rank == 0:
+            ref, t_ref = _single_render(O, g, full_r, pl, fr)
+            out_q.put(("render", bool(np.array_equal(img, ref)), bool(np.array_equal(t_img.view(np.uint32),
+                                                                                        t_ref.view(np.uint32))),
+                       float((t_ref >= 0).mean())))
         # bench protocol: max over ranks of a per-rank time
         t = torch.tensor([float(rank + 1)], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -86,6 +99,83 @@ def _rank_main(rank, world, port, out_q):
             out_q.put((ok, ok_h, lay.check_halo(locs), float(t.item())))
     finally:
         dist.destroy_process_group()
+
+
+W, H = 640, 480
+
+
+def _camera(O, pl, fr):
+    Kinv = np.linalg.inv(_K()).astype(np.float32)
+    dist = float(np.mean(fr[0].depth[fr[0].depth > 0]) / 5000.0)
+    return O.orbit_camera(Kinv.reshape(-1), 0.25, dist)
+
+
+def _single_render(O, g, st, pl, fr, mode=0):
+    s2w, c = _camera(O, pl, fr)
+    return O.render(g, s2w, c, W, H, mode, st.sdf, st.hist, st.color)
+
+
+def _gloo_allgather(dist, send, world):
+    import torch
+
+    t = torch.from_numpy(send)
+    parts = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    return np.concatenate([p.numpy() for p in parts])
+
+
+def _shard_render(O, g, st, pl, fr, allgather, shard, nshards, chunk, mode=0):
+    """Drive the 4 protocol steps for one shard; allgather(send) -> gathered records."""
+    s2w, c = _camera(O, pl, fr)
+    npx = W * H
+    state = np.zeros(6 * npx, np.int32)
+    send = np.zeros(2 * npx, np.int32)
+    gathered = np.zeros(2 * npx * nshards, np.int32)
+    for step in range(4):
+        O.shard_render_step(g, s2w, c, W, H, mode, st.sdf, st.hist, st.color, step, shard, nshards, chunk, gathered,
+                            send, state)
+        gathered = allgather(send.copy())
+    out = np.zeros(npx * 3, np.uint8)
+    t = np.zeros(npx, np.float32)
+    O.shard_render_step(g, s2w, c, W, H, mode, st.sdf, st.hist, st.color, 4, shard, nshards, chunk, gathered, send,
+                        state, out, t)
+    return out.reshape(H, W, 3), t.reshape(H, W)
+
+
+@pytest.mark.parametrize("nshards,chunk,mode", [(2, 4, 0), (3, 5, 1), (4, 2, 0), (1, 32, 1)])
+def test_sharded_render_protocol_equals_single_volume(oracle, nshards, chunk, mode):
+    """The split march (SURVEY.md §8e raycast composite) restated in the C oracle: virtual
+    shards stepping in lockstep with an in-process all-gather reproduce the single-volume
+    render bit for bit (image and hit distance)."""
+    O = oracle
+    D = 32
+    fr = _frames()
+    pl = O.place(fr[0].depth, np.linalg.inv(_K()).astype(np.float32), [D] * 3,
+                 np.mean(fr[0].depth[fr[0].depth > 0]) / 5000.0, 0)
+    g = O.OGeom([D] * 3, pl["vol_start"], pl["voxel"], pl["mu"], pl["vol_end"])
+    st = O.OState([D] * 3, np.float32(pl["mu"]), semantic=True)
+    for f in fr[1:]:
+        E = (f.w2c @ fr[0].c2w).astype(np.float32)
+        O.integrate(g, st, _K(), E, f.depth, f.rgb, f.gt_ids, flags=0x3)
+    ref, t_ref = _single_render(O, g, st, pl, fr, mode)
+    assert (t_ref >= 0).mean() > 0.2
+    npx = W * H
+    s2w, c = _camera(O, pl, fr)
+    states = [np.zeros(6 * npx, np.int32) for _ in range(nshards)]
+    sends = [np.zeros(2 * npx, np.int32) for _ in range(nshards)]
+    gathered = np.zeros(2 * npx * nshards, np.int32)
+    for step in range(4):
+        for r in range(nshards):
+            O.shard_render_step(g, s2w, c, W, H, mode, st.sdf, st.hist, st.color, step, r, nshards, chunk, gathered,
+                                sends[r], states[r])
+        gathered = np.concatenate(sends)
+    for r in range(nshards):
+        out = np.zeros(npx * 3, np.uint8)
+        t = np.zeros(npx, np.float32)
+        O.shard_render_step(g, s2w, c, W, H, mode, st.sdf, st.hist, st.color, 4, r, nshards, chunk, gathered,
+                            sends[r], states[r], out, t)
+        assert np.array_equal(out.reshape(H, W, 3), ref), r
+        assert np.array_equal(t.view(np.uint32), t_ref.reshape(-1).view(np.uint32)), r
 
 
 def _free_port():
@@ -108,6 +198,12 @@ def test_gloo_world2_sharded_integrate_equals_single_volume():
     for p in procs:
         p.join(timeout=240)
         assert p.exitcode == 0, f"rank exit code {p.exitcode}"
-    ok, ok_h, halo_ok, tmax = q.get(timeout=10)
+    res = {}
+    for _ in range(2):
+        item = q.get(timeout=10)
+        res[item[0] if isinstance(item[0], str) else "integrate"] = item
+    ok, ok_h, halo_ok, tmax = res["integrate"]
     assert ok and ok_h and halo_ok
     assert tmax == 2.0
+    _, img_ok, t_ok, hit = res["render"]
+    assert img_ok and t_ok and hit > 0.2
