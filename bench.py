@@ -169,23 +169,15 @@ def host_cores() -> int:
 
 
 def copy_bandwidth(device: int, nbytes: int = 1 << 30) -> float:
-    """Achievable HBM bandwidth (GB/s, read + write) of a device-to-device copy, for context
-    beside the 8 TB/s spec peak."""
-    import torch
+    """Achievable HBM bandwidth (GB/s, read + write) of a float4 device copy (library kernel),
+    for context beside the 8 TB/s spec peak."""
+    import ctypes as C
 
-    a = torch.empty(nbytes // 4, dtype=torch.float32, device=f"cuda:{device}").fill_(1.0)
-    b = torch.empty_like(a)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    best = 1e9
-    for _ in range(5):
-        e0.record()
-        b.copy_(a)
-        e1.record()
-        e1.synchronize()
-        best = min(best, e0.elapsed_time(e1))
-    del a, b
-    torch.cuda.empty_cache()
-    return 2.0 * nbytes / (best * 1e-3) / 1e9
+    from semtsdf import _lib as L
+
+    out = C.c_double()
+    L.check(L.load().semtsdf_copy_bandwidth(int(device), int(nbytes), 5, C.byref(out)))
+    return out.value
 
 
 def main():

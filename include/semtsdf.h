@@ -211,6 +211,10 @@ int semtsdf_shard_assoc_apply(semtsdf_vol* v, const int64_t* reduced_d, uint8_t*
  * n_obs > 0), then integrate_dev, then note_integrated (n_obs++, first-frame object count). */
 int semtsdf_shard_note_integrated(semtsdf_vol* v, const uint8_t* mask_d, void* stream);
 
+/* Achievable HBM bandwidth on `device` (GB/s, read + write bytes) of a float4 device copy
+ * of `bytes` bytes, best of `reps` runs: the practical ceiling beside the 8 TB/s spec peak. */
+int semtsdf_copy_bandwidth(int device, size_t bytes, int reps, double* gbs);
+
 /* ---- state transfer (parity, checkpoint/resume) ------------------------------------------
  * Reference layouts, local storage (for an unsharded handle: the whole volume).  Any
  * pointer may be NULL.  color is u8 [N*3] or i32 [N*3] per SEMTSDF_F_COLOR_I32; hist is

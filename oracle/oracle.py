@@ -60,6 +60,8 @@ def lib():
         _lib.oracle_shard_render_step.argtypes = [P, P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, C.c_int,
                                                   C.c_int, C.c_int, C.c_int, P, P, P, P, P]
         _lib.oracle_shard_render_step.restype = None
+        _lib.oracle_div_rcp_mismatches.argtypes = [P, C.c_int, C.c_float]
+        _lib.oracle_div_rcp_mismatches.restype = C.c_int
         _lib.oracle_place.argtypes = [P, C.c_int, C.c_int, P, P, C.c_double, C.c_int, P]
         _lib.oracle_place.restype = C.c_int
         _lib.oracle_orbit_camera.argtypes = [P, C.c_float, C.c_float, P, P]
@@ -168,6 +170,11 @@ def shard_render_step(g: OGeom, s2w, c, W, H, mode, sdf, hist, color, step, shar
                                    _p(np.ascontiguousarray(c, np.float32).reshape(3)), W, H, int(mode),
                                    int(color_i32), _p(sdf), _p(hist), _p(color), int(step), int(shard),
                                    int(nshards), int(chunk), _p(gathered), _p(send), _p(state), _p(out), _p(out_t))
+
+
+def div_rcp_mismatches(a, b: float) -> int:
+    a = np.ascontiguousarray(a, np.float32)
+    return int(lib().oracle_div_rcp_mismatches(_p(a), a.size, float(b)))
 
 
 def place(depth, Kinv16, dims, mean_depth, mode):

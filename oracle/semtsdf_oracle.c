@@ -696,3 +696,21 @@ void oracle_orbit_camera(const float* Kinv16, float angle, float dist, float* s2
     c[1] = 0.0f;
     c[2] = r - r * ca;
 }
+
+/* ---------------------------------------------------------------- division check
+ * Test support for k_integrate's div_by_rcp: number of a[i] (|a| >= 2^-60) for which
+ * RN(q0 + r y), q0 = RN(a y), r = fma(-q0, b, a), y = RN(1/b), differs from RN(a/b). */
+int oracle_div_rcp_mismatches(const float* a, int n, float b) {
+    const float y = 1.0f / b;
+    int bad = 0;
+    for (int i = 0; i < n; ++i) {
+        const float x = a[i];
+        if (!(fabsf(x) >= 0x1p-60f)) continue;
+        const float q0 = x * y;
+        const float r = fmaf(-q0, b, x);
+        const float q1 = fmaf(r, y, q0);
+        const float ref = x / b;
+        if (memcmp(&q1, &ref, 4) != 0) ++bad;
+    }
+    return bad;
+}

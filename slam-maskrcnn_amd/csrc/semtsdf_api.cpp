@@ -211,6 +211,8 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
     a.counters = v->counters_d;
     a.unit_flags = v->unit_flags_d;
     a.pinhole = (a.K[1] == 0.0f && a.K[3] == 0.0f && a.K[6] == 0.0f && a.K[7] == 0.0f && a.K[8] == 1.0f) ? 1 : 0;
+    a.rmu = 1.0f / v->g.mu;  // IEEE: the correctly rounded reciprocal
+    a.fastdiv = (v->g.mu >= 0x1p-20f && v->g.mu <= 0x1p20f && a.debug != 8) ? 1 : 0;
     if (a.debug == 2) return SEMTSDF_OK;
     EventPair epp;
     timing_begin(v, v->ev_prep, s, &epp);
@@ -911,6 +913,39 @@ int semtsdf_shard_note_integrated(semtsdf_vol* v, const uint8_t* mask_d, void* s
     }
     v->n_obs++;
     return SEMTSDF_OK;
+}
+
+int semtsdf_copy_bandwidth(int device, size_t bytes, int reps, double* gbs) {
+    if (!gbs || bytes < 16 || reps < 1) return fail(SEMTSDF_ERR_INVALID, "bad argument");
+    HIPC(hipSetDevice(device));
+    bytes &= ~(size_t)15;
+    void *a = nullptr, *b = nullptr;
+    hipStream_t s = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int rc = SEMTSDF_OK;
+    float best = 1e30f;
+    if (hipMalloc(&a, bytes) != hipSuccess || hipMalloc(&b, bytes) != hipSuccess ||
+        hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
+        hipEventCreate(&e1) != hipSuccess || hipMemsetAsync(a, 0, bytes, s) != hipSuccess) {
+        rc = fail(SEMTSDF_ERR_HIP, "copy_bandwidth setup failed");
+    } else {
+        for (int r = 0; r <= reps && rc == SEMTSDF_OK; ++r) {
+            float ms = 0.0f;
+            if (hipEventRecord(e0, s) != hipSuccess || launch_copy_f4(a, b, bytes / 16, s) != hipSuccess ||
+                hipEventRecord(e1, s) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+                hipEventElapsedTime(&ms, e0, e1) != hipSuccess)
+                rc = fail(SEMTSDF_ERR_HIP, "copy_bandwidth run failed");
+            else if (r > 0 && ms < best)  // run 0 is a warm-up
+                best = ms;
+        }
+    }
+    if (rc == SEMTSDF_OK) *gbs = 2.0 * (double)bytes / ((double)best * 1e-3) / 1e9;
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (s) (void)hipStreamDestroy(s);
+    if (a) (void)hipFree(a);
+    if (b) (void)hipFree(b);
+    return rc;
 }
 
 int semtsdf_orbit_camera(const float Kinv[16], float angle, float dist, float s2w[16], float c[3]) {

@@ -62,6 +62,8 @@ struct IntegrateArgs {
     unsigned long long* counters;  // [0] touched, [1] gated, [2] bad-label flag, [3] live bricks
     uint8_t* unit_flags;           // per cull unit: 1 = may hold a touched voxel (cull pass output)
     int pinhole;                   // K rows are (fx 0 cx; 0 fy cy; 0 0 1)
+    float rmu;                     // RN(1/mu), for the exact division by mu (k_integrate)
+    int fastdiv;                   // mu in [2^-20, 2^20]: divisions by mu/(w+1) via RN reciprocals
 };
 
 // Association accumulators (fixed point, scale 2^28, deterministic).
@@ -161,6 +163,7 @@ hipError_t launch_shard_render_final(const ShardRayArgs& a, hipStream_t s);
 hipError_t launch_shard_render_finish(const ShardRayArgs& a, hipStream_t s);
 hipError_t launch_shard_assoc_partial(const ShardRayArgs& a, hipStream_t s);
 hipError_t launch_tables_from_partial(const long long* reduced, AssocTables* t, hipStream_t s);
+hipError_t launch_copy_f4(const void* src, void* dst, size_t n16, hipStream_t s);
 hipError_t launch_fill_volume(const VolGeom& g, const VolBufs& b, uint32_t flags, hipStream_t s);
 hipError_t launch_depth_pyramid(const uint16_t* depth, const uint8_t* rgb, const uint8_t* mask, int w, int h,
                                 float scale, const DepthPyramid& p, hipStream_t s);

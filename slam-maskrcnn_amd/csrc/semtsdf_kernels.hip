@@ -100,6 +100,16 @@ __global__ __launch_bounds__(256) void k_fill_f32(float* __restrict__ p, uint64_
     }
 }
 
+__global__ __launch_bounds__(256) void k_copy_f4(const float4* __restrict__ a, float4* __restrict__ b, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        b[i] = a[i];
+}
+
+hipError_t launch_copy_f4(const void* src, void* dst, size_t n16, hipStream_t s) {
+    hipLaunchKernelGGL(k_copy_f4, dim3(8192), dim3(256), 0, s, (const float4*)src, (float4*)dst, n16);
+    return hipGetLastError();
+}
+
 hipError_t launch_fill_volume(const VolGeom& g, const VolBufs& b, uint32_t flags, hipStream_t s) {
     (void)flags;
     const uint64_t n = g.nvox;
@@ -196,6 +206,20 @@ __device__ __forceinline__ int floor_div(float a, float b) {
     if (fr > tol && fr < 1.0f - tol && fabsf(b) > 1.0e-30f && fabsf(q) < 8.0e6f) return (int)fq;
     return f2i_rd(a / b);
 }
+
+// RN(a / b) from y = RN(1/b): q0 = RN(a y) is within 1 ulp of a/b, the remainder
+// r = a - q0 b is exact (fma), and RN(q0 + r y) = RN(a/b) (Markstein's theorem).  The
+// remainder stays a normal number for |a| >= 2^-60 and b in [2^-20, 2^20] (checked
+// exhaustively on the host for the mu range, tests/test_oracle_props.py); smaller |a|
+// takes the IEEE division, zero keeps its sign.
+__device__ __forceinline__ float div_by_rcp(float a, float b, float y) {
+    const float q0 = a * y;
+    const float r = fmaf(-q0, b, a);
+    return fmaf(r, y, q0);
+}
+
+// Table of RN(1/n), n = 1..kRcpTable, for the weighted running means (w + 1 <= kRcpTable).
+constexpr int kRcpTable = 4096;
 
 // (c*w + x) / (w+1) for 0 <= c, x <= 255 via the float reciprocal plus one exact integer
 // correction (quotient <= 255, so the float estimate is within one of it); integer
@@ -333,6 +357,9 @@ uint64_t brick_count_max(const VolGeom& g) { return unit_grid(g).n; }
 template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT, bool SHARD, bool PIN>
 __global__ __launch_bounds__(256) void k_integrate(IntegrateArgs a, UnitGrid ug) {
     const VolGeom& g = a.g;
+    __shared__ float s_rcp[kRcpTable];
+    for (int i = threadIdx.x; i < kRcpTable; i += blockDim.x) s_rcp[i] = 1.0f / (float)(i + 1);
+    __syncthreads();
     const int lane = threadIdx.x & 63;
     const unsigned wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     const unsigned nwaves = gridDim.x * (blockDim.x >> 6);
@@ -421,7 +448,12 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateArgs a, UnitGrid ug)
                 float diff = d - qz[k];
                 const bool t = (d != 0.0f) & (diff > -g.mu);
                 diff = (diff > g.mu) ? g.mu : diff;
-                fv[k] = diff / g.mu;
+                if (a.fastdiv) {
+                    fv[k] = div_by_rcp(diff, g.mu, a.rmu);
+                    if (!(fabsf(diff) >= 0x1p-60f)) fv[k] = diff == 0.0f ? diff : diff / g.mu;
+                } else {
+                    fv[k] = diff / g.mu;
+                }
                 tmask |= (t ? 1u : 0u) << k;
                 gmask |= ((t & (!GATE || fv[k] < a.gate)) ? 1u : 0u) << k;
             }
@@ -468,7 +500,14 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateArgs a, UnitGrid ug)
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const bool t = (tmask >> k) & 1u;
-                const float upd = fmaf(so[k], (float)wo[k], fv[k]) / (float)(wo[k] + 1);
+                const float num = fmaf(so[k], (float)wo[k], fv[k]);
+                float upd;
+                if (a.fastdiv && (unsigned)wo[k] < (unsigned)kRcpTable) {
+                    upd = div_by_rcp(num, (float)(wo[k] + 1), s_rcp[wo[k]]);
+                    if (!(fabsf(num) >= 0x1p-60f)) upd = num == 0.0f ? num : num / (float)(wo[k] + 1);
+                } else {
+                    upd = num / (float)(wo[k] + 1);
+                }
                 sn[k] = t ? upd : so[k];
                 wn[k] = wo[k] + (t ? 1 : 0);
             }

@@ -152,6 +152,7 @@ SIGNATURES = {
     "semtsdf_shard_assoc_partial": (_I, [_P, _P, _P, _P, _P]),
     "semtsdf_shard_assoc_apply": (_I, [_P, _P, _P, C.POINTER(AssocStats), _P]),
     "semtsdf_shard_note_integrated": (_I, [_P, _P, _P]),
+    "semtsdf_copy_bandwidth": (_I, [_I, C.c_size_t, _I, C.POINTER(C.c_double)]),
     "semtsdf_download": (_I, [_P, _P, _P, _P, _P, _P, _P]),
     "semtsdf_upload": (_I, [_P, _P, _P, _P, _P, _P, _P]),
     "semtsdf_set_instrumentation": (_I, [_P, _I]),

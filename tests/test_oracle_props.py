@@ -148,3 +148,23 @@ def test_synthetic_stream_properties():
     assert f.mask.max() <= 6 and set(np.unique(f.mask)) - {0} == set(range(1, f.mask.max() + 1))
     f2 = SyntheticStream(seed=1).frame(0)
     assert np.array_equal(f.depth, f2.depth) and np.array_equal(f.mask, f2.mask)
+
+
+def test_reciprocal_division_is_correctly_rounded(oracle):
+    """k_integrate divides by mu and by w+1 through RN reciprocals (div_by_rcp, Markstein);
+    it must equal the IEEE quotient of the reference (tsdf.cu:52,56) for |a| >= 2^-60."""
+    rng = np.random.default_rng(5)
+    # diff / mu: diff in [-mu, mu], mu = 5 voxel for voxels of 0.5 mm .. 10 cm
+    for mu in np.float32([0.0025, 0.0234375, 0.03125, 0.5]).tolist() + rng.uniform(0.002, 0.5, 12).astype(
+            np.float32).tolist():
+        mu = np.float32(mu)
+        a = np.concatenate([rng.uniform(-mu, mu, 200000).astype(np.float32),
+                            np.float32(mu) * np.float32([1, -1, 0.5, -0.5, 0.999999, 1e-6, -1e-12]),
+                            (rng.standard_normal(20000) * np.float32(2.0) ** rng.integers(-60, 0, 20000)).astype(
+                                np.float32)])
+        a = np.clip(a, -mu, mu)
+        assert oracle.div_rcp_mismatches(a, float(mu)) == 0, mu
+    # (sdf * w + f) / (w + 1): |numerator| <= w + 1, w + 1 <= 4096 (the LDS table)
+    for den in list(range(1, 70)) + rng.integers(70, 4097, 60).tolist():
+        a = rng.uniform(-den, den, 20000).astype(np.float32)
+        assert oracle.div_rcp_mismatches(a, float(den)) == 0, den
