@@ -93,6 +93,7 @@ struct semtsdf_vol {
     int ray_kind = -1;
     int ray_next = 0;              // next expected step
     uint32_t n_obs = 0;
+    bool bmin_dirty = true;        // the empty-space map needs a rebuild before the next march
     // instrumentation
     int instr = 0;
     std::vector<EventPair> ev_integrate, ev_assoc, ev_render, ev_prep;
@@ -117,8 +118,8 @@ int dev_alloc(semtsdf_vol* v, void** p, size_t bytes) {
 }
 
 void free_all(semtsdf_vol* v) {
-    void* ptrs[] = {v->b.sdf, v->b.wt, v->b.color, v->b.hist, v->b.cls, v->b.cls_cnt, v->depth_d, v->rgb_d,
-                    v->mask_d, v->cls_d, v->pyr.metres, v->pyr.rgbl, v->pyr.l0, v->pyr.l1, v->pyr.l2, v->tables_d, v->decision_d,
+    void* ptrs[] = {v->b.sdf, v->b.wt, v->b.bmin, v->b.color, v->b.hist, v->b.cls, v->b.cls_cnt, v->depth_d, v->rgb_d,
+                    v->mask_d, v->cls_d, v->pyr.metres, v->pyr.rgbl, v->pyr.l0, v->pyr.l1, v->tables_d, v->decision_d,
                     v->num_objs_d, v->probs_d, v->box_d, v->palette_d, v->render_d, v->render_t_d,
                     v->counters_d, v->unit_flags_d, v->ray_state_d};
     for (void* q : ptrs)
@@ -143,6 +144,9 @@ int check_params(const semtsdf_params* p) {
     if (!(p->depth_scale > 0.0f)) return fail(SEMTSDF_ERR_INVALID, "depth_scale must be > 0");
     if ((p->flags & SEMTSDF_F_VOTE) && (p->flags & SEMTSDF_F_SEMANTIC))
         return fail(SEMTSDF_ERR_INVALID, "SEMANTIC and VOTE are exclusive");
+    for (int i = 0; i < 3; ++i)
+        if (!(p->voxel[i] >= 0x1p-20f && p->voxel[i] <= 0x1p20f))
+            return fail(SEMTSDF_ERR_INVALID, "voxel size %g outside [2^-20, 2^20]", (double)p->voxel[i]);
     if (p->z_nshards < 1 || p->z_shard < 0 || p->z_shard >= p->z_nshards)
         return fail(SEMTSDF_ERR_INVALID, "bad shard %d of %d", p->z_shard, p->z_nshards);
     if (p->z_nshards > 1 && (p->z_chunk < 1 || p->z_chunk > p->dim[2]))
@@ -211,6 +215,10 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
     a.counters = v->counters_d;
     a.unit_flags = v->unit_flags_d;
     a.pinhole = (a.K[1] == 0.0f && a.K[3] == 0.0f && a.K[6] == 0.0f && a.K[7] == 0.0f && a.K[8] == 1.0f) ? 1 : 0;
+    {
+        static const char* deal = getenv("SEMTSDF_DEAL");  // A/B of the work deal (default 0)
+        a.deal = deal ? atoi(deal) : 0;
+    }
     a.rmu = 1.0f / v->g.mu;  // IEEE: the correctly rounded reciprocal
     a.fastdiv = (v->g.mu >= 0x1p-20f && v->g.mu <= 0x1p20f && a.debug != 8) ? 1 : 0;
     if (a.debug == 2) return SEMTSDF_OK;
@@ -220,11 +228,29 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
     HIPC(launch_cull(a, s));
     timing_end(v, v->ev_prep, s, &epp);
     v->n_prep++;
-    if (a.debug == 1) return SEMTSDF_OK;
+    // instrumentation: SEMTSDF_WAVE_STATS=<file> appends per-wave start/end/units records
+    static const char* ws_path = getenv("SEMTSDF_WAVE_STATS");
+    unsigned long long* ws = nullptr;
+    if (ws_path && !(a.flags & 0x80000000u)) {
+        HIPC(hipMalloc((void**)&ws, 8192 * 4 * sizeof(unsigned long long)));
+        HIPC(hipMemsetAsync(ws, 0, 8192 * 4 * sizeof(unsigned long long), s));
+        a.wave_stats = ws;
+    }
     EventPair ep;  // events bracket the integrate kernel alone (the roofline kernel)
     timing_begin(v, v->ev_integrate, s, &ep);
     HIPC(launch_integrate(a, s));
     timing_end(v, v->ev_integrate, s, &ep);
+    v->bmin_dirty = true;
+    if (ws) {
+        std::vector<unsigned long long> h(8192 * 4);
+        HIPC(hipMemcpyAsync(h.data(), ws, h.size() * 8, hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+        HIPC(hipFree(ws));
+        if (FILE* f = fopen(ws_path, "ab")) {
+            fwrite(h.data(), 8, h.size(), f);
+            fclose(f);
+        }
+    }
     v->n_integrate++;
     return SEMTSDF_OK;
 }
@@ -248,12 +274,21 @@ MarchCamera assoc_camera(const semtsdf_vol* v, const float E[16]) {
     return c;
 }
 
+// Rebuild the empty-space map after the volume changed (integrate, upload, reset).
+int ensure_bmin(semtsdf_vol* v, hipStream_t s) {
+    if (!v->bmin_dirty) return SEMTSDF_OK;
+    HIPC(launch_brick_min(v->g, v->b, s));
+    v->bmin_dirty = false;
+    return SEMTSDF_OK;
+}
+
 int associate_impl(semtsdf_vol* v, uint8_t* mask_d, const float E[16], hipStream_t s, bool want_decision) {
     if (v->p.z_nshards != 1) return fail(SEMTSDF_ERR_UNSUPPORTED, "association on a Z-sharded handle is not supported yet");
     if (!(v->p.flags & SEMTSDF_F_SEMANTIC)) return fail(SEMTSDF_ERR_STATE, "association needs a SEMANTIC volume");
     if (v->n_obs == 0) return fail(SEMTSDF_ERR_STATE, "association needs n_obs > 0 (tsdf.cu:426)");
     EventPair ep;
     timing_begin(v, v->ev_assoc, s, &ep);
+    if (int rc = ensure_bmin(v, s)) return rc;
     HIPC(hipMemsetAsync(v->tables_d, 0, sizeof(AssocTables), s));
     HIPC(hipMemsetAsync(&v->tables_d->first_px[0], 0xFF, sizeof(unsigned) * 256, s));
     HIPC(launch_mask_stats(mask_d, (int)npx(v), v->tables_d, s));
@@ -486,6 +521,8 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     for (int i = 0; i < 3; ++i) { g.start[i] = p->vol_start[i]; g.end[i] = p->vol_end[i]; g.voxel[i] = p->voxel[i]; }
     g.mu = p->mu;
     g.nvox = (uint64_t)g.dimx * (uint64_t)g.dimy * (uint64_t)g.zs;
+    g.nbx = (g.dimx + 7) / 8; g.nby = (g.dimy + 7) / 8; g.nbz = (g.lz + 7) / 8;
+    for (int i = 0; i < 3; ++i) g.rvox[i] = 1.0f / g.voxel[i];  // IEEE: correctly rounded
     const size_t n = g.nvox;
     const size_t px = (size_t)p->width * p->height;
     auto bail = [&](int code) { free_all(v); delete v; return code; };
@@ -494,6 +531,7 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     const bool ci32 = p->flags & SEMTSDF_F_COLOR_I32;
     if ((rc = dev_alloc(v, (void**)&v->b.sdf, n * 4))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->b.wt, n * 4))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&v->b.bmin, (size_t)g.nbx * g.nby * g.nbz * 4))) return bail(rc);
     if ((rc = dev_alloc(v, &v->b.color, n * 4 * (ci32 ? 4 : 1)))) return bail(rc);
     if (p->flags & SEMTSDF_F_SEMANTIC)
         if ((rc = dev_alloc(v, (void**)&v->b.hist, n * kMaxObjects * 4))) return bail(rc);
@@ -508,17 +546,17 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     DepthPyramid& pyr = v->pyr;
     pyr.w0 = (p->width + 7) / 8; pyr.h0 = (p->height + 7) / 8;
     pyr.w1 = (p->width + 31) / 32; pyr.h1 = (p->height + 31) / 32;
-    pyr.w2 = (p->width + 127) / 128; pyr.h2 = (p->height + 127) / 128;
-    if ((rc = dev_alloc(v, (void**)&pyr.metres, px * 4))) return bail(rc);
-    if ((rc = dev_alloc(v, (void**)&pyr.rgbl, px * 4))) return bail(rc);
+    pyr.wb = (p->width + 1) / 2;
+    const size_t pxb = (size_t)pyr.wb * ((p->height + 7) / 8) * 16;  // block-linear, padded
+    if ((rc = dev_alloc(v, (void**)&pyr.metres, pxb * 4))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&pyr.rgbl, pxb * 4))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&pyr.l0, (size_t)pyr.w1 * 4 * pyr.h1 * 4 * 2))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&pyr.l1, (size_t)pyr.w1 * pyr.h1 * 2))) return bail(rc);
-    if ((rc = dev_alloc(v, (void**)&pyr.l2, (size_t)pyr.w2 * pyr.h2 * 4))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&v->unit_flags_d, unit_count(g)))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->tables_d, sizeof(AssocTables)))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->decision_d, sizeof(AssocDecision)))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->num_objs_d, 16))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->counters_d, 4 * sizeof(unsigned long long)))) return bail(rc);
-    if ((rc = dev_alloc(v, (void**)&v->unit_flags_d, brick_count_max(g)))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->palette_d, sizeof(kPalette)))) return bail(rc);
     if (hipHostMalloc((void**)&v->decision_h, sizeof(AssocDecision), 0) != hipSuccess)
         return bail(fail(SEMTSDF_ERR_HIP, "hipHostMalloc failed"));
@@ -584,6 +622,7 @@ int semtsdf_reset(semtsdf_vol* v, void* stream) {
     HIPC(hipMemsetAsync(v->num_objs_d, 0, 16, s));
     HIPC(hipMemsetAsync(v->counters_d, 0, 4 * sizeof(unsigned long long), s));
     v->n_obs = 0;
+    v->bmin_dirty = true;
     return SEMTSDF_OK;
 }
 
@@ -682,6 +721,7 @@ int semtsdf_assoc_probs(semtsdf_vol* v, const float E[16], float* probs, uint8_t
     a.tables = v->tables_d;
     a.probs_out = v->probs_d;
     a.box_out = v->box_d;
+    if (int rc = ensure_bmin(v, s)) return rc;
     HIPC(launch_assoc_march(a, s));
     HIPC(hipMemcpyAsync(probs, v->probs_d, n * 4, hipMemcpyDeviceToHost, s));
     HIPC(hipMemcpyAsync(box_mask, v->box_d, n, hipMemcpyDeviceToHost, s));
@@ -810,6 +850,8 @@ int semtsdf_shard_ray_begin(semtsdf_vol* v, int kind, const float cam[16], const
         m.use_s2w = 1;
         v->ray_cam = m;
     }
+    if (int rc = ensure_bmin(v, v->stream)) return rc;
+    HIPC(hipStreamSynchronize(v->stream));  // the protocol's steps may run on another stream
     v->ray_kind = kind;
     v->ray_next = 0;
     if (record_bytes) *record_bytes = 8 * npx(v);
@@ -986,6 +1028,7 @@ static int raycast_impl(semtsdf_vol* v, const float s2w[16], const float c[3], i
     a.out_t = out_t_d;
     EventPair ep;
     timing_begin(v, v->ev_render, s, &ep);
+    if (int rc = ensure_bmin(v, s)) return rc;
     HIPC(launch_render(a, s));
     timing_end(v, v->ev_render, s, &ep);
     v->n_render++;
@@ -1140,6 +1183,7 @@ int semtsdf_upload(semtsdf_vol* v, const float* sdf, const int32_t* wt, const vo
         }
         HIPC(hipFree(stage));
     }
+    v->bmin_dirty = true;
     HIPC(hipStreamSynchronize(s));
     return SEMTSDF_OK;
 }

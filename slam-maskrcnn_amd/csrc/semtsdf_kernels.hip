@@ -48,6 +48,27 @@ __device__ __forceinline__ float mixf(float a, float b, float t) {
     return fmaf(t, b, (1.0f - t) * a);
 }
 
+// RN(a / b) from y = RN(1/b): q0 = RN(a y) is within 1 ulp of a/b, the remainder
+// r = a - q0 b is exact (fma), and RN(q0 + r y) = RN(a/b) (Markstein's theorem).  The
+// remainder stays a normal number for |a| >= 2^-60 and b in [2^-20, 2^20] (checked
+// exhaustively on the host for the mu range, tests/test_oracle_props.py); smaller |a|
+// takes the IEEE division, zero keeps its sign.
+__device__ __forceinline__ float div_by_rcp(float a, float b, float y) {
+    const float q0 = a * y;
+    const float r = fmaf(-q0, b, a);
+    return fmaf(r, y, q0);
+}
+
+// (p - start) / voxel, correctly rounded: reciprocal form (div_by_rcp) with the IEEE
+// division for operands too small for it (voxel sizes outside [2^-20, 2^20] are rejected
+// at create time).
+__device__ __forceinline__ float vox_coord(float p, float start, float voxel, float rvox) {
+    const float a = p - start;
+    float q = div_by_rcp(a, voxel, rvox);
+    if (!(fabsf(a) >= 0x1p-60f)) q = a == 0.0f ? a / voxel : a / voxel;
+    return q;
+}
+
 __device__ __forceinline__ int local_to_global_z(const VolGeom& g, int l) {
     if (g.nshards == 1) return l;
     const int per = g.chunk + g.halo;
@@ -65,7 +86,7 @@ __device__ __forceinline__ int global_to_local_z(const VolGeom& g, int z) {
 // Shard owning the trilinear sample at world z `pz` (its base plane, clamped as the
 // sampler clamps it).
 __device__ __forceinline__ int sample_owner(const VolGeom& g, float pz) {
-    const float iz = (pz - g.start[2]) / g.voxel[2];
+    const float iz = vox_coord(pz, g.start[2], g.voxel[2], g.rvox[2]);
     const int zc = min(max(f2i_rd(iz), 0), g.dimz - 1);
     return (zc / g.chunk) % g.nshards;
 }
@@ -110,6 +131,35 @@ hipError_t launch_copy_f4(const void* src, void* dst, size_t n16, hipStream_t s)
     return hipGetLastError();
 }
 
+// Empty-space map: one wave per 8^3 brick, min of sdf over local voxels
+// [8b, 8b + 8] per axis (the brick plus the +1 border every trilinear sample based in the
+// brick reads), clamped to the stored volume.
+__global__ __launch_bounds__(256) void k_brick_min(VolGeom g, const float* __restrict__ sdf, float* __restrict__ bmin) {
+    const unsigned nb = (unsigned)g.nbx * g.nby * g.nbz;
+    const unsigned br = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (br >= nb) return;
+    const int lane = threadIdx.x & 63;
+    const int bz = br % g.nbz, by = (br / g.nbz) % g.nby, bx = br / (g.nbz * g.nby);
+    const int x0 = bx * 8, y0 = by * 8, z0 = bz * 8;
+    const int nx = min(9, g.dimx - x0), ny = min(9, g.dimy - y0), nz = min(9, g.lz - z0);
+    const uint64_t plane = (uint64_t)g.dimy * (uint64_t)g.zs;
+    float m = 3.0e38f;
+    for (int row = lane; row < nx * ny; row += 64) {
+        const int x = x0 + row / ny, y = y0 + row % ny;
+        const float* p = sdf + (uint64_t)x * plane + (uint64_t)y * g.zs + z0;
+        for (int k = 0; k < nz; ++k) m = fminf(m, p[k]);
+    }
+    for (int off = 32; off > 0; off >>= 1) m = fminf(m, __shfl_xor(m, off, 64));
+    if (lane == 0) bmin[br] = m;
+}
+
+hipError_t launch_brick_min(const VolGeom& g, const VolBufs& b, hipStream_t s) {
+    const unsigned nb = (unsigned)g.nbx * g.nby * g.nbz;
+    if (nb == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_brick_min, dim3((nb + 3) / 4), dim3(256), 0, s, g, b.sdf, b.bmin);
+    return hipGetLastError();
+}
+
 hipError_t launch_fill_volume(const VolGeom& g, const VolBufs& b, uint32_t flags, hipStream_t s) {
     (void)flags;
     const uint64_t n = g.nvox;
@@ -121,30 +171,53 @@ hipError_t launch_fill_volume(const VolGeom& g, const VolBufs& b, uint32_t flags
 }
 
 // ------------------------------------------------------------------------------------
-// depth pyramid: max raw depth over 8/32/128-pixel tiles, for brick culling.
-// One workgroup per 32x32 pixel tile; 256 lanes x 4 pixels.
+// frame prepass: depth in metres, rgb+label packed per pixel, and max raw depth over 8- and
+// 32-pixel tiles for unit culling.  One workgroup per 32x32 pixel tile; lane = (row,
+// 4 columns), loaded as one 8-B depth vector, one 4-B mask word and three 4-B rgb words
+// when the rows are 4-pixel aligned (vec), else pixel by pixel.
 // ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restrict__ depth, const uint8_t* __restrict__ rgb,
                                                        const uint8_t* __restrict__ mask, int w, int h, float scale,
-                                                       DepthPyramid p) {
+                                                       int vec, DepthPyramid p) {
     __shared__ unsigned s_m[32][8];
     const int tx = blockIdx.x, ty = blockIdx.y;
     const int t = threadIdx.x;
     const int r = t >> 3;          // row in tile
     const int c4 = (t & 7) * 4;    // first column in tile
     const int yy = ty * 32 + r;
+    const int x0 = tx * 32 + c4;
     unsigned m = 0;
-    if (yy < h) {
-        for (int k = 0; k < 4; ++k) {
-            const int xx = tx * 32 + c4 + k;
-            if (xx < w) {
-                const unsigned d = depth[(size_t)yy * w + xx];
+    if (yy < h && x0 < w) {
+        const size_t px0 = (size_t)yy * w + x0;
+        if (vec && x0 + 3 < w) {
+            const ushort4 d4 = *reinterpret_cast<const ushort4*>(depth + px0);
+            const unsigned d[4] = {d4.x, d4.y, d4.z, d4.w};
+            m = max(max(d[0], d[1]), max(d[2], d[3]));
+            const int b0 = pix_block_index(x0, yy, p.wb), b1 = pix_block_index(x0 + 2, yy, p.wb);
+            *reinterpret_cast<float2*>(p.metres + b0) = make_float2((float)d[0] / scale, (float)d[1] / scale);
+            *reinterpret_cast<float2*>(p.metres + b1) = make_float2((float)d[2] / scale, (float)d[3] / scale);
+            if (rgb) {
+                const uint32_t* c = reinterpret_cast<const uint32_t*>(rgb + px0 * 3);
+                const uint32_t c0 = c[0], c1 = c[1], c2 = c[2];  // r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3
+                const uint32_t lab = mask ? *reinterpret_cast<const uint32_t*>(mask + px0) : 0u;
+                uint4 o;
+                o.x = (c0 & 0xFFFFFFu) | ((lab & 0xFFu) << 24);
+                o.y = (c0 >> 24) | ((c1 & 0xFFFFu) << 8) | (((lab >> 8) & 0xFFu) << 24);
+                o.z = (c1 >> 16) | ((c2 & 0xFFu) << 16) | (((lab >> 16) & 0xFFu) << 24);
+                o.w = (c2 >> 8) | ((lab >> 24) << 24);
+                *reinterpret_cast<uint2*>(p.rgbl + b0) = make_uint2(o.x, o.y);
+                *reinterpret_cast<uint2*>(p.rgbl + b1) = make_uint2(o.z, o.w);
+            }
+        } else {
+            for (int k = 0; k < 4 && x0 + k < w; ++k) {
+                const size_t px = px0 + k;
+                const unsigned d = depth[px];
                 m = max(m, d);
-                const size_t px = (size_t)yy * w + xx;
-                p.metres[px] = (float)d / scale;  // depth[img] / 5000.f (tsdf.cu:49)
+                const int bi = pix_block_index(x0 + k, yy, p.wb);
+                p.metres[bi] = (float)d / scale;  // depth[img] / 5000.f (tsdf.cu:49)
                 if (rgb) {
                     const unsigned lab = mask ? (unsigned)mask[px] : 0u;
-                    p.rgbl[px] = (unsigned)rgb[px * 3] | ((unsigned)rgb[px * 3 + 1] << 8) |
+                    p.rgbl[bi] = (unsigned)rgb[px * 3] | ((unsigned)rgb[px * 3 + 1] << 8) |
                                  ((unsigned)rgb[px * 3 + 2] << 16) | (lab << 24);
                 }
             }
@@ -170,15 +243,15 @@ __global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restric
         for (int a = 0; a < 4; ++a)
             for (int bcol = 0; bcol < 4; ++bcol) mm = max(mm, s_l0[a][bcol]);
         p.l1[ty * p.w1 + tx] = (uint16_t)mm;
-        atomicMax(p.l2 + (ty / 4) * p.w2 + (tx / 4), mm);
     }
 }
 
 hipError_t launch_depth_pyramid(const uint16_t* depth, const uint8_t* rgb, const uint8_t* mask, int w, int h,
                                 float scale, const DepthPyramid& p, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(p.l2, 0, (size_t)p.w2 * p.h2 * sizeof(uint32_t), s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_depth_pyramid, dim3(p.w1, p.h1), dim3(256), 0, s, depth, rgb, mask, w, h, scale, p);
+    const bool vec = (w % 4 == 0) && ((uintptr_t)depth % 8 == 0) && (!rgb || (uintptr_t)rgb % 4 == 0) &&
+                     (!mask || (uintptr_t)mask % 4 == 0);
+    hipLaunchKernelGGL(k_depth_pyramid, dim3(p.w1, p.h1), dim3(256), 0, s, depth, rgb, mask, w, h, scale,
+                       vec ? 1 : 0, p);
     return hipGetLastError();
 }
 
@@ -207,19 +280,8 @@ __device__ __forceinline__ int floor_div(float a, float b) {
     return f2i_rd(a / b);
 }
 
-// RN(a / b) from y = RN(1/b): q0 = RN(a y) is within 1 ulp of a/b, the remainder
-// r = a - q0 b is exact (fma), and RN(q0 + r y) = RN(a/b) (Markstein's theorem).  The
-// remainder stays a normal number for |a| >= 2^-60 and b in [2^-20, 2^20] (checked
-// exhaustively on the host for the mu range, tests/test_oracle_props.py); smaller |a|
-// takes the IEEE division, zero keeps its sign.
-__device__ __forceinline__ float div_by_rcp(float a, float b, float y) {
-    const float q0 = a * y;
-    const float r = fmaf(-q0, b, a);
-    return fmaf(r, y, q0);
-}
-
 // Table of RN(1/n), n = 1..kRcpTable, for the weighted running means (w + 1 <= kRcpTable).
-constexpr int kRcpTable = 4096;
+constexpr int kRcpTable = 1024;
 
 // (c*w + x) / (w+1) for 0 <= c, x <= 255 via the float reciprocal plus one exact integer
 // correction (quotient <= 255, so the float estimate is within one of it); integer
@@ -269,7 +331,9 @@ __device__ int unit_cull(const IntegrateArgs& a, int x0, int y0, int lz0) {
         const float qz = dot3(a.E[8], a.E[9], a.E[10], px, py, pz) + a.E[11];
         float sx, sy, sz;
         screen(a, qx, qy, qz, &sx, &sy, &sz);
-        const float u = sx / sz, v = sy / sz;
+        // conservative test: the reciprocal's ~1e-4 px error is far inside the 1-px guard band
+        const float rz = __builtin_amdgcn_rcpf(sz);
+        const float u = sx * rz, v = sy * rz;
         umin = fminf(umin, u); umax = fmaxf(umax, u);
         vmin = fminf(vmin, v); vmax = fmaxf(vmax, v);
         zmin = fminf(zmin, qz); zmax = fmaxf(zmax, qz);
@@ -293,12 +357,11 @@ __device__ int unit_cull(const IntegrateArgs& a, int x0, int y0, int lz0) {
     if (((u1 >> 3) - (u0 >> 3) + 1) * ((v1 >> 3) - (v0 >> 3) + 1) <= 16) {
         for (int ty = v0 >> 3; ty <= (v1 >> 3); ++ty)
             for (int tx = u0 >> 3; tx <= (u1 >> 3); ++tx) m = max(m, (unsigned)a.pyr.l0[ty * a.pyr.w0 + tx]);
-    } else if (((u1 >> 5) - (u0 >> 5) + 1) * ((v1 >> 5) - (v0 >> 5) + 1) <= 16) {
+    } else if (((u1 >> 5) - (u0 >> 5) + 1) * ((v1 >> 5) - (v0 >> 5) + 1) <= 64) {
         for (int ty = v0 >> 5; ty <= (v1 >> 5); ++ty)
             for (int tx = u0 >> 5; tx <= (u1 >> 5); ++tx) m = max(m, (unsigned)a.pyr.l1[ty * a.pyr.w1 + tx]);
     } else {
-        for (int ty = v0 >> 7; ty <= (v1 >> 7); ++ty)
-            for (int tx = u0 >> 7; tx <= (u1 >> 7); ++tx) m = max(m, a.pyr.l2[ty * a.pyr.w2 + tx]);
+        return 0;  // footprint wider than 256x256 px (units at the near plane): keep
     }
     if (m == 0) return 1;  // every pixel of the footprint has depth 0
     const float dmax = (float)m / a.depth_scale;
@@ -321,7 +384,7 @@ __host__ __device__ inline UnitGrid unit_grid(const VolGeom& g) {
     return u;
 }
 
-// Pass 1: one lane per unit.  flags[u] = 1 when the unit may hold a touched voxel.
+// Cull pass: one lane per unit.  flags[u] = 1 when the unit may hold a touched voxel.
 __global__ __launch_bounds__(256) void k_cull_units(IntegrateArgs a, UnitGrid ug) {
     const unsigned u = blockIdx.x * blockDim.x + threadIdx.x;
     if (u >= ug.n) return;
@@ -330,25 +393,14 @@ __global__ __launch_bounds__(256) void k_cull_units(IntegrateArgs a, UnitGrid ug
     a.unit_flags[u] = (uint8_t)live;
 }
 
-__global__ __launch_bounds__(256) void k_count_live(const uint8_t* __restrict__ flags, unsigned n,
-                                                    unsigned long long* counters) {
-    unsigned c = 0;
-    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) c += flags[i];
-    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
-    if ((threadIdx.x & 63) == 0 && c) atomicAdd(counters + 3, (unsigned long long)c);
-}
-
 hipError_t launch_cull(const IntegrateArgs& a, hipStream_t s) {
     const UnitGrid ug = unit_grid(a.g);
     if (ug.n == 0) return hipSuccess;  // a shard that owns no chunk
     hipLaunchKernelGGL(k_cull_units, dim3((ug.n + 255) / 256), dim3(256), 0, s, a, ug);
-    hipError_t e = hipGetLastError();
-    if (e == hipSuccess && a.counters && (a.flags & 0x80000000u))
-        hipLaunchKernelGGL(k_count_live, dim3(64), dim3(256), 0, s, a.unit_flags, ug.n, a.counters);
-    return e == hipSuccess ? hipGetLastError() : e;
+    return hipGetLastError();
 }
 
-uint64_t brick_count_max(const VolGeom& g) { return unit_grid(g).n; }
+uint64_t unit_count(const VolGeom& g) { return unit_grid(g).n; }
 
 // Pass 2: persistent wavefronts over units.  Branch-free classification and update
 // (selects instead of divergent ifs) keep the scalar/branch overhead per item low; the only
@@ -365,16 +417,23 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateArgs a, UnitGrid ug)
     const unsigned nwaves = gridDim.x * (blockDim.x >> 6);
     const uint64_t plane = (uint64_t)g.dimy * (uint64_t)g.zs;
     unsigned n_touch = 0, n_gate = 0;
-    // The wave's units are wave, wave + nwaves, ...; their flags are fetched 64 at a time
-    // (one per lane) and the live ones are visited through the ballot mask.
-    for (unsigned first = wave; first < ug.n; first += 64u * nwaves) {
-        const unsigned mine = first + (unsigned)lane * nwaves;
+    unsigned n_live = 0, n_done = 0;
+    const uint64_t t_start = a.wave_stats ? __builtin_amdgcn_s_memrealtime() : 0;
+    // Work deal.  a.deal == 1: one wave per batch of 64 consecutive units, a grid of as
+    // many waves as batches (the dispatcher balances the uneven live counts).  a.deal == 0:
+    // persistent waves, wave w takes units w, w + nwaves, ...  Either way the cull flags
+    // are fetched 64 at a time (one per lane) and the live ones visited through the ballot.
+    const unsigned stride = a.deal ? 1u : nwaves;
+    for (unsigned first = a.deal ? wave * 64u : wave; first < ug.n; first += 64u * nwaves) {
+        const unsigned mine = first + (unsigned)lane * stride;
         const bool lv = mine < ug.n && a.unit_flags[mine];
         unsigned long long todo = __ballot(lv);
+        if (COUNT) n_live += (unsigned)__popcll(todo);
         while (todo) {
             const int kk = __ffsll((long long)todo) - 1;
             todo &= todo - 1ull;
-            const unsigned u = first + (unsigned)kk * nwaves;
+            const unsigned u = first + (unsigned)kk * stride;
+            ++n_done;
             const unsigned uxy = u % (ug.nux * ug.nuy);
             const int x = (int)(uxy % ug.nux);
             const int y = (int)(uxy / ug.nux) * UY + (lane >> 3);
@@ -385,7 +444,7 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateArgs a, UnitGrid ug)
             const uint64_t v = (uint64_t)x * plane + (uint64_t)y * (uint64_t)g.zs + (uint64_t)l0;
 
             // ---- project the lane's 4 voxels (tsdf.cu:30-44)
-            int img[4];
+            int img[4], bix[4];
             float qz[4];
             unsigned slow = 0;
             float sxv[4], syv[4], szv[4];
@@ -424,6 +483,7 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateArgs a, UnitGrid ug)
                 const bool fast = (fu == floorf(qu + tu)) & (fvv == floorf(qv + tv));
                 const bool in = zok & (fu >= 0.0f) & (fu < (float)a.width) & (fvv >= 0.0f) & (fvv < (float)a.height);
                 img[k] = in ? (int)fvv * a.width + (int)fu : -1;
+                bix[k] = in ? pix_block_index((int)fu, (int)fvv, a.pyr.wb) : 0;
                 slow |= ((zok & !fast) ? 1u : 0u) << k;
                 sxv[k] = sx; syv[k] = sy; szv[k] = sz;
             }
@@ -432,13 +492,15 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateArgs a, UnitGrid ug)
                 for (int k = 0; k < 4; ++k) {
                     if (!(slow & (1u << k))) continue;
                     const int ix = f2i_rd(sxv[k] / szv[k]), iy = f2i_rd(syv[k] / szv[k]);
-                    img[k] = (ix >= 0 && ix < a.width && iy >= 0 && iy < a.height) ? iy * a.width + ix : -1;
+                    const bool in = ix >= 0 && ix < a.width && iy >= 0 && iy < a.height;
+                    img[k] = in ? iy * a.width + ix : -1;
+                    bix[k] = in ? pix_block_index(ix, iy, a.pyr.wb) : 0;
                 }
             }
             // ---- depth gather (one dword per voxel from the metres image)
             float dm[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) dm[k] = a.pyr.metres[img[k] >= 0 ? img[k] : 0];
+            for (int k = 0; k < 4; ++k) dm[k] = a.debug == 9 ? 2.0f : a.pyr.metres[bix[k]];  // 9: no gather probe
             // ---- classify (tsdf.cu:48-52), branch-free
             float fv[4];
             unsigned tmask = 0, gmask = 0;
@@ -490,7 +552,7 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateArgs a, UnitGrid ug)
                     c8 = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint32_t*>(a.b.color) + v);
                 }
 #pragma unroll
-                for (int k = 0; k < 4; ++k) pix[k] = a.pyr.rgbl[img[k] >= 0 ? img[k] : 0];
+                for (int k = 0; k < 4; ++k) pix[k] = a.pyr.rgbl[bix[k]];
             }
             // ---- update (tsdf.cu:56, 68), branch-free selects
             const float so[4] = {s4.x, s4.y, s4.z, s4.w};
@@ -511,8 +573,12 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateArgs a, UnitGrid ug)
                 sn[k] = t ? upd : so[k];
                 wn[k] = wo[k] + (t ? 1 : 0);
             }
-            *reinterpret_cast<float4*>(a.b.sdf + v) = make_float4(sn[0], sn[1], sn[2], sn[3]);
-            *reinterpret_cast<int4*>(a.b.wt + v) = make_int4(wn[0], wn[1], wn[2], wn[3]);
+            if (a.debug == 10) {  // timing probe: loads but no sdf/weight stores
+                asm volatile("" ::"v"(sn[0] + sn[1] + sn[2] + sn[3]), "v"(wn[0] + wn[1] + wn[2] + wn[3]));
+            } else {
+                *reinterpret_cast<float4*>(a.b.sdf + v) = make_float4(sn[0], sn[1], sn[2], sn[3]);
+                *reinterpret_cast<int4*>(a.b.wt + v) = make_int4(wn[0], wn[1], wn[2], wn[3]);
+            }
             if (gmask) {  // tsdf.cu:57-62
                 if (CI32) {
                     int4* c = reinterpret_cast<int4*>(a.b.color) + v;
@@ -581,6 +647,17 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateArgs a, UnitGrid ug)
             }
         }
     }
+    if (a.wave_stats && lane == 0) {  // instrumentation: per-wave start/end (100 MHz ticks), units
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        unsigned hw_id;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_id));
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        a.wave_stats[wave * 4 + 0] = t_start;
+        a.wave_stats[wave * 4 + 1] = t_end;
+        a.wave_stats[wave * 4 + 2] = n_done;
+        a.wave_stats[wave * 4 + 3] = ((uint64_t)xcc << 32) | hw_id;
+    }
     if (COUNT) {
         unsigned long long t = n_touch, gg = n_gate;
         for (int off = 32; off > 0; off >>= 1) {
@@ -590,12 +667,20 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateArgs a, UnitGrid ug)
         if (lane == 0) {
             if (t) atomicAdd(a.counters + 0, t);
             if (gg) atomicAdd(a.counters + 1, gg);
+            if (n_live) atomicAdd(a.counters + 3, (unsigned long long)n_live);
         }
     }
 }
 
 // Persistent grid sized to exactly the resident capacity (blocks/CU from the occupancy
 // query x CUs): an oversubscribed persistent grid leaves a tail of late blocks.
+static unsigned resident_grid_cus() {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 256;
+    return (unsigned)cus;
+}
+
 template <typename K>
 static unsigned resident_grid(K kernel) {
     int dev = 0, cus = 0, per = 0;
@@ -608,9 +693,12 @@ static unsigned resident_grid(K kernel) {
 template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT, bool SHARD, bool PIN>
 static hipError_t launch_integrate_k(const IntegrateArgs& a, hipStream_t s) {
     if (unit_grid(a.g).n == 0) return hipSuccess;
+    // ROCm 7.2's occupancy query over-reports by one block per CU for SGPR-heavy 256-thread
+    // kernels (MI355X_MICROARCH.md): the persistent grid uses one block per CU less.
     static const unsigned grid0 = resident_grid(k_integrate<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>);
-    unsigned grid = grid0;
-    if (a.debug >= 100) grid = grid0 * (unsigned)(a.debug - 100) / 8u;  // timing probe: fraction of residency
+    const unsigned ncu = resident_grid_cus();
+    unsigned grid = a.deal ? (unsigned)((unit_grid(a.g).n + 255) / 256) : (grid0 > 2 * ncu ? grid0 - ncu : grid0);
+    if (!a.deal && a.debug >= 100) grid = grid0 * (unsigned)(a.debug - 100) / 8u;  // probe: fraction of residency
     hipLaunchKernelGGL((k_integrate<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>), dim3(grid), dim3(256), 0, s, a,
                        unit_grid(a.g));
     return hipGetLastError();
@@ -667,27 +755,52 @@ struct Tri {
     float fx, fy, fz;
 };
 
-__device__ __forceinline__ Tri tri_setup(const VolGeom& g, float px, float py, float pz) {
-    const float ix = (px - g.start[0]) / g.voxel[0];
-    const float iy = (py - g.start[1]) / g.voxel[1];
-    const float iz = (pz - g.start[2]) / g.voxel[2];
+// Base voxel (clamped) of the trilinear sample at p, its local plane and the fractions.
+struct TriCoord {
+    int xc, yc, zc, zl;   // clamped base voxel; zl = local plane of zc
+    int dxv, dyv, dzv;    // 1, or 0 where the +1 neighbour is clamped
+    float fx, fy, fz;
+};
+
+__device__ __forceinline__ TriCoord tri_coord(const VolGeom& g, float px, float py, float pz) {
+    const float ix = vox_coord(px, g.start[0], g.voxel[0], g.rvox[0]);
+    const float iy = vox_coord(py, g.start[1], g.voxel[1], g.rvox[1]);
+    const float iz = vox_coord(pz, g.start[2], g.voxel[2], g.rvox[2]);
     const int x = f2i_rd(ix), y = f2i_rd(iy), z = f2i_rd(iz);
-    Tri t;
-    t.fx = ix - (float)x;
-    t.fy = iy - (float)y;
-    t.fz = iz - (float)z;
-    const int xc = min(max(x, 0), g.dimx - 1), yc = min(max(y, 0), g.dimy - 1), zc = min(max(z, 0), g.dimz - 1);
-    const int xn = min(max(x + 1, 0), g.dimx - 1), yn = min(max(y + 1, 0), g.dimy - 1),
-              zn = min(max(z + 1, 0), g.dimz - 1);
-    const uint64_t plane = (uint64_t)g.dimy * (uint64_t)g.zs;
+    TriCoord c;
+    c.fx = ix - (float)x;
+    c.fy = iy - (float)y;
+    c.fz = iz - (float)z;
+    c.xc = min(max(x, 0), g.dimx - 1);
+    c.yc = min(max(y, 0), g.dimy - 1);
+    c.zc = min(max(z, 0), g.dimz - 1);
+    c.dxv = min(max(x + 1, 0), g.dimx - 1) - c.xc;
+    c.dyv = min(max(y + 1, 0), g.dimy - 1) - c.yc;
+    c.dzv = min(max(z + 1, 0), g.dimz - 1) - c.zc;
     // global plane -> local plane of this shard (the caller only samples planes it owns;
-    // zn = zc + 1 is then the chunk's next plane or its halo plane)
-    const int zl = g.nshards == 1 ? zc : global_to_local_z(g, zc);
-    t.i000 = (uint64_t)xc * plane + (uint64_t)yc * g.zs + (uint64_t)zl;
-    t.dx = (uint64_t)(xn - xc) * plane;
-    t.dy = (uint64_t)(yn - yc) * (uint64_t)g.zs;
-    t.dz = (uint32_t)(zn - zc);
+    // zc + 1 is then the chunk's next plane or its halo plane)
+    c.zl = g.nshards == 1 ? c.zc : global_to_local_z(g, c.zc);
+    return c;
+}
+
+__device__ __forceinline__ Tri tri_from(const VolGeom& g, const TriCoord& c) {
+    Tri t;
+    const uint64_t plane = (uint64_t)g.dimy * (uint64_t)g.zs;
+    t.i000 = (uint64_t)c.xc * plane + (uint64_t)c.yc * g.zs + (uint64_t)c.zl;
+    t.dx = (uint64_t)c.dxv * plane;
+    t.dy = (uint64_t)c.dyv * (uint64_t)g.zs;
+    t.dz = (uint32_t)c.dzv;
+    t.fx = c.fx; t.fy = c.fy; t.fz = c.fz;
     return t;
+}
+
+__device__ __forceinline__ Tri tri_setup(const VolGeom& g, float px, float py, float pz) {
+    return tri_from(g, tri_coord(g, px, py, pz));
+}
+
+// Empty-space map: brick of 8^3 local voxels holding the sample's 8 corners.
+__device__ __forceinline__ int brick_of(const VolGeom& g, const TriCoord& c) {
+    return ((c.xc >> 3) * g.nby + (c.yc >> 3)) * g.nbz + (c.zl >> 3);
 }
 
 template <typename T>
@@ -726,22 +839,108 @@ __device__ __forceinline__ bool ray_bounds(const VolGeom& g, float ox, float oy,
     return true;
 }
 
-__device__ bool march_ray(const VolGeom& g, const float* __restrict__ sdf, float ox, float oy, float oz,
-                          float dx, float dy, float dz, float* t_hit) {
+// Skip threshold: a trilinear sample whose 8 corners are all >= m is >= m (1 - 2^-21) in
+// f32 (three levels of mix), so corners >= thr = (voxel/2)(1 + 2^-16) guarantee a sample
+// >= voxel/2: no event of the march (no hit, no step switch).  Skipped samples are not
+// evaluated; t still advances by the same additions, so the result is unchanged.
+__device__ __forceinline__ float skip_threshold(const VolGeom& g) { return g.voxel[0] / 2.0f * (1.0f + 0x1p-16f); }
+
+// Sample evaluator with the brick map: returns false (and no value) when the sample's
+// brick is known to hold only values >= thr.  Caches the last brick looked up.
+struct SkipCursor {
+    int brick = -1;
+    bool skip = false;
+    float lo[3], hi[3];  // approximate voxel-coordinate box surely inside the skippable brick
+};
+
+// Approximate voxel coordinates of a ray point (|error| ~1e-4 voxel; only used to prove
+// that a sample lies well inside a brick already known to be skippable).
+struct RayVox {
+    float k[3], c[3];
+};
+
+__device__ __forceinline__ RayVox ray_vox(const VolGeom& g, float ox, float oy, float oz, float dx, float dy,
+                                          float dz) {
+    RayVox r;
+    r.k[0] = dx * g.rvox[0]; r.k[1] = dy * g.rvox[1]; r.k[2] = dz * g.rvox[2];
+    r.c[0] = (ox - g.start[0]) * g.rvox[0];
+    r.c[1] = (oy - g.start[1]) * g.rvox[1];
+    r.c[2] = (oz - g.start[2]) * g.rvox[2];
+    return r;
+}
+
+__device__ __forceinline__ bool sample_or_skip(const VolGeom& g, const VolBufs& b, float thr, SkipCursor& cur,
+                                               float px, float py, float pz, float* f, const RayVox* rv = nullptr,
+                                               float t = 0.0f) {
+    if (rv && cur.skip) {  // fast path: still well inside the current skippable brick
+        const float ax = fmaf(t, rv->k[0], rv->c[0]), ay = fmaf(t, rv->k[1], rv->c[1]),
+                    az = fmaf(t, rv->k[2], rv->c[2]);
+        if ((ax > cur.lo[0]) & (ax < cur.hi[0]) & (ay > cur.lo[1]) & (ay < cur.hi[1]) & (az > cur.lo[2]) &
+            (az < cur.hi[2]))
+            return false;
+    }
+    const TriCoord c = tri_coord(g, px, py, pz);
+    if (b.bmin) {
+        const int br = brick_of(g, c);
+        if (br != cur.brick) {
+            cur.brick = br;
+            cur.skip = b.bmin[br] >= thr;
+            if (cur.skip && rv) {
+                // brick bounds in voxel coordinates, shrunk by a margin far above the
+                // approximation error; the outer faces of the volume extend to infinity
+                // (samples there clamp into the edge brick)
+                const int bx = c.xc >> 3, by = c.yc >> 3, bz = c.zl >> 3;
+                const float m = 0.01f;
+                cur.lo[0] = bx == 0 ? -1e30f : 8.0f * bx + m;
+                cur.hi[0] = bx == g.nbx - 1 ? 1e30f : 8.0f * bx + 8.0f - m;
+                cur.lo[1] = by == 0 ? -1e30f : 8.0f * by + m;
+                cur.hi[1] = by == g.nby - 1 ? 1e30f : 8.0f * by + 8.0f - m;
+                cur.lo[2] = bz == 0 ? -1e30f : 8.0f * bz + m;
+                cur.hi[2] = bz == g.nbz - 1 ? 1e30f : 8.0f * bz + 8.0f - m;
+            }
+        }
+        if (cur.skip) return false;
+    }
+    *f = tri_eval(b.sdf, tri_from(g, c));
+    return true;
+}
+
+// The shared ray march of back_proj_kernel (tsdf.cu:90-124) and show_tsdf_kernel
+// (viewer.cu:223-257).  Returns true on a hit and the refined t.
+__device__ bool march_ray(const VolGeom& g, const VolBufs& b, float ox, float oy, float oz, float dx, float dy,
+                          float dz, float* t_hit) {
     float t, tfar;
     if (!ray_bounds(g, ox, oy, oz, dx, dy, dz, &t, &tfar)) return false;
-    float f_tt = 0.0f;
     const float vx = g.voxel[0];
+    const float thr = skip_threshold(g);
+    SkipCursor cur;
+    const RayVox rv = ray_vox(g, ox, oy, oz, dx, dy, dz);
+    const RayVox* rvp = g.nshards == 1 ? &rv : nullptr;  // local z == global z only unsharded
+    float f_t = 1.0f, f_tt = 0.0f;
+    bool prev_skipped = false;  // f_t not evaluated: re-evaluate it at t_prev if needed
+    float t_prev = t;
+    if (sample_or_skip(g, b, thr, cur, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz), &f_t, rvp, t)) {
+        if (!(f_t > 0.0f)) return false;
+    } else {
+        prev_skipped = true;
+    }
     float step = vx;
-    float f_t = sample_sdf(g, sdf, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
-    if (!(f_t > 0.0f)) return false;
     for (; t < tfar; t += step) {
-        f_tt = sample_sdf(g, sdf, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
+        float f;
+        if (!sample_or_skip(g, b, thr, cur, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz), &f, rvp, t)) {
+            prev_skipped = true;  // f >= voxel/2: neither a hit nor a step switch
+            t_prev = t;
+            f_tt = 1.0f;
+            continue;
+        }
+        f_tt = f;
         if (f_tt < 0.0f) break;
         if (f_tt < vx / 2.0f) step = vx / 4.0f;
         f_t = f_tt;
+        prev_skipped = false;
     }
     if (!(f_tt < 0.0f)) return false;
+    if (prev_skipped) f_t = sample_sdf(g, b.sdf, fmaf(t_prev, dx, ox), fmaf(t_prev, dy, oy), fmaf(t_prev, dz, oz));
     t += step * f_tt / (f_t - f_tt);
     *t_hit = t;
     return true;
@@ -884,7 +1083,7 @@ __global__ __launch_bounds__(256) void k_assoc_march(AssocArgs a) {
         float p[kMaxObjects];
 #pragma unroll
         for (int k = 0; k < kMaxObjects; ++k) p[k] = 0.0f;
-        if (march_ray(a.g, a.b.sdf, ox, oy, oz, dx, dy, dz, &t)) {
+        if (march_ray(a.g, a.b, ox, oy, oz, dx, dy, dz, &t)) {
             const Tri tr = tri_setup(a.g, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
 #pragma unroll
             for (int k = 0; k < kMaxObjects; ++k) p[k] = tri_eval(a.b.hist + (uint64_t)k * a.g.nvox, tr);
@@ -1056,7 +1255,7 @@ __global__ __launch_bounds__(256) void k_render(RenderArgs a) {
     ray_render(a.cam, x, y, &ox, &oy, &oz, &dx, &dy, &dz);
     uint8_t b = 0, gch = 0, r = 0;
     float th = -1.0f;
-    if (march_ray(a.g, a.b.sdf, ox, oy, oz, dx, dy, dz, &t)) {
+    if (march_ray(a.g, a.b, ox, oy, oz, dx, dy, dz, &t)) {
         th = t;
         const Tri tr = tri_setup(a.g, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
         shade_hit(a.g, a.b, tr, a.mode, a.color_i32, a.palette, &b, &gch, &r);
@@ -1127,6 +1326,12 @@ __device__ __forceinline__ float sample_at(const ShardRayArgs& a, const RayGeo& 
     return sample_sdf(a.g, a.b.sdf, fmaf(t, r.dx, r.ox), fmaf(t, r.dy, r.oy), fmaf(t, r.dz, r.oz));
 }
 
+// false when the brick map proves the sample >= voxel/2 (see march_ray)
+__device__ __forceinline__ bool sample_at_skip(const ShardRayArgs& a, const RayGeo& r, float t, float thr,
+                                               SkipCursor& cur, float* f) {
+    return sample_or_skip(a.g, a.b, thr, cur, fmaf(t, r.dx, r.ox), fmaf(t, r.dy, r.oy), fmaf(t, r.dz, r.oz), f);
+}
+
 __global__ __launch_bounds__(256) void k_shard_ray_step(ShardRayArgs a) {
     const int x = blockIdx.x * 16 + (threadIdx.x & 15);
     const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
@@ -1142,8 +1347,10 @@ __global__ __launch_bounds__(256) void k_shard_ray_step(ShardRayArgs a) {
         } else {
             float t = r.t0;
             bool dead = false;
-            if (owns_at(a, r, t)) {
-                const float f0 = sample_at(a, r, t);
+            const float thr = skip_threshold(a.g);
+            SkipCursor cur;
+            float f0;
+            if (owns_at(a, r, t) && sample_at_skip(a, r, t, thr, cur, &f0)) {
                 if (!(f0 > 0.0f)) { rec.x = -1; dead = true; }
             }
             if (!dead) {
@@ -1152,7 +1359,8 @@ __global__ __launch_bounds__(256) void k_shard_ray_step(ShardRayArgs a) {
                 } else {
                     for (int k = 0; t < r.t1; ++k, t += vx) {
                         if (!owns_at(a, r, t)) continue;
-                        const float f = sample_at(a, r, t);
+                        float f;
+                        if (!sample_at_skip(a, r, t, thr, cur, &f)) continue;
                         if (f < vx / 2.0f) { rec = make_int2(k, __float_as_int(f)); break; }
                     }
                 }
@@ -1174,11 +1382,14 @@ __global__ __launch_bounds__(256) void k_shard_ray_step(ShardRayArgs a) {
             } else {
                 float t = replay_t(r.t0, k, 0, vx);
                 const float q = vx / 4.0f;
+                const float thr = skip_threshold(a.g);
+                SkipCursor cur;
                 for (int j = 1;; ++j) {
                     t += q;
                     if (!(t < r.t1)) break;
                     if (!owns_at(a, r, t)) continue;
-                    const float f = sample_at(a, r, t);
+                    float f;
+                    if (!sample_at_skip(a, r, t, thr, cur, &f)) continue;
                     if (f < 0.0f) { rec = make_int2(j, __float_as_int(f)); break; }
                 }
             }
