@@ -93,7 +93,8 @@ struct semtsdf_vol {
     int ray_kind = -1;
     int ray_next = 0;              // next expected step
     uint32_t n_obs = 0;
-    bool bmin_dirty = true;        // the empty-space map needs a rebuild before the next march
+    bool bmin_dirty = false;       // integrated since the last map update: update marked bricks
+    bool bmin_stale = true;        // reset/upload: rebuild the whole map
     // instrumentation
     int instr = 0;
     std::vector<EventPair> ev_integrate, ev_assoc, ev_render, ev_prep;
@@ -118,7 +119,7 @@ int dev_alloc(semtsdf_vol* v, void** p, size_t bytes) {
 }
 
 void free_all(semtsdf_vol* v) {
-    void* ptrs[] = {v->b.sdf, v->b.wt, v->b.bmin, v->b.color, v->b.hist, v->b.cls, v->b.cls_cnt, v->depth_d, v->rgb_d,
+    void* ptrs[] = {v->b.sdf, v->b.wt, v->b.bmin, v->b.bplain, v->b.bdirty, v->b.color, v->b.hist, v->b.cls, v->b.cls_cnt, v->depth_d, v->rgb_d,
                     v->mask_d, v->cls_d, v->pyr.metres, v->pyr.rgbl, v->pyr.l0, v->pyr.l1, v->tables_d, v->decision_d,
                     v->num_objs_d, v->probs_d, v->box_d, v->palette_d, v->render_d, v->render_t_d,
                     v->counters_d, v->unit_flags_d, v->ray_state_d};
@@ -276,9 +277,11 @@ MarchCamera assoc_camera(const semtsdf_vol* v, const float E[16]) {
 
 // Rebuild the empty-space map after the volume changed (integrate, upload, reset).
 int ensure_bmin(semtsdf_vol* v, hipStream_t s) {
-    if (!v->bmin_dirty) return SEMTSDF_OK;
-    HIPC(launch_brick_min(v->g, v->b, s));
+    if (!v->bmin_dirty && !v->bmin_stale) return SEMTSDF_OK;
+    // stale (reset/upload): every brick; dirty (integrate): the bricks the cull marked
+    HIPC(launch_brick_min(v->g, v->b, v->bmin_stale, s));
     v->bmin_dirty = false;
+    v->bmin_stale = false;
     return SEMTSDF_OK;
 }
 
@@ -531,7 +534,11 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     const bool ci32 = p->flags & SEMTSDF_F_COLOR_I32;
     if ((rc = dev_alloc(v, (void**)&v->b.sdf, n * 4))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->b.wt, n * 4))) return bail(rc);
-    if ((rc = dev_alloc(v, (void**)&v->b.bmin, (size_t)g.nbx * g.nby * g.nbz * 4))) return bail(rc);
+    const size_t nbricks = (size_t)g.nbx * g.nby * g.nbz;
+    if ((rc = dev_alloc(v, (void**)&v->b.bmin, nbricks * 4))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&v->b.bplain, nbricks * 4))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&v->b.bdirty, nbricks))) return bail(rc);
+    if (nbricks && hipMemset(v->b.bdirty, 0, nbricks) != hipSuccess) return bail(fail(SEMTSDF_ERR_HIP, "memset failed"));
     if ((rc = dev_alloc(v, &v->b.color, n * 4 * (ci32 ? 4 : 1)))) return bail(rc);
     if (p->flags & SEMTSDF_F_SEMANTIC)
         if ((rc = dev_alloc(v, (void**)&v->b.hist, n * kMaxObjects * 4))) return bail(rc);
@@ -622,7 +629,7 @@ int semtsdf_reset(semtsdf_vol* v, void* stream) {
     HIPC(hipMemsetAsync(v->num_objs_d, 0, 16, s));
     HIPC(hipMemsetAsync(v->counters_d, 0, 4 * sizeof(unsigned long long), s));
     v->n_obs = 0;
-    v->bmin_dirty = true;
+    v->bmin_stale = true;
     return SEMTSDF_OK;
 }
 
@@ -1027,10 +1034,25 @@ static int raycast_impl(semtsdf_vol* v, const float s2w[16], const float c[3], i
     a.out_bgr = out_bgr_d;
     a.out_t = out_t_d;
     EventPair ep;
-    timing_begin(v, v->ev_render, s, &ep);
     if (int rc = ensure_bmin(v, s)) return rc;
+    // instrumentation: SEMTSDF_RAY_STATS=<file> appends per-pixel march counters and
+    // per-wave timestamps of every render
+    static const char* rs_path = getenv("SEMTSDF_RAY_STATS");
+    const size_t rs_words = npx(v) * 4 + ((npx(v) + 63) / 64 + 64) * 4;
+    if (rs_path) HIPC(hipMalloc((void**)&a.ray_stats, rs_words * 4));
+    timing_begin(v, v->ev_render, s, &ep);
     HIPC(launch_render(a, s));
     timing_end(v, v->ev_render, s, &ep);
+    if (rs_path) {
+        std::vector<unsigned> h(rs_words);
+        HIPC(hipMemcpyAsync(h.data(), a.ray_stats, rs_words * 4, hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+        HIPC(hipFree(a.ray_stats));
+        if (FILE* f = fopen(rs_path, "ab")) {
+            fwrite(h.data(), 4, h.size(), f);
+            fclose(f);
+        }
+    }
     v->n_render++;
     return SEMTSDF_OK;
 }
@@ -1183,7 +1205,7 @@ int semtsdf_upload(semtsdf_vol* v, const float* sdf, const int32_t* wt, const vo
         }
         HIPC(hipFree(stage));
     }
-    v->bmin_dirty = true;
+    v->bmin_stale = true;
     HIPC(hipStreamSynchronize(s));
     return SEMTSDF_OK;
 }

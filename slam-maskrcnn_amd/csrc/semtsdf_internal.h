@@ -33,6 +33,8 @@ struct VolBufs {
     int32_t* cls;      // vote mode
     int32_t* cls_cnt;  // vote mode
     float* bmin;       // per 8^3 brick: min sdf over its voxels and the +1 border (ray skipping)
+    float* bplain;     // per 8^3 brick: min sdf over its own voxels
+    uint8_t* bdirty;   // per 8^3 brick: overlaps a unit integrated since the last map update
 };
 
 // Per-frame depth pyramid used by the brick culler: max raw depth over tiles of
@@ -136,6 +138,8 @@ struct RenderArgs {
     const uint8_t* palette;  // [32*3] RGB, written BGR
     uint8_t* out_bgr;
     float* out_t;
+    unsigned* ray_stats;     // instrumentation (SEMTSDF_RAY_STATS): per pixel iterations, lookups,
+                             // evaluations, skipped samples; per wave start/end ticks after them
 };
 
 // Z-sharded raycast protocol (k_shard_* in semtsdf_kernels.hip): per-pixel march state.
@@ -176,7 +180,7 @@ hipError_t launch_shard_render_finish(const ShardRayArgs& a, hipStream_t s);
 hipError_t launch_shard_assoc_partial(const ShardRayArgs& a, hipStream_t s);
 hipError_t launch_tables_from_partial(const long long* reduced, AssocTables* t, hipStream_t s);
 hipError_t launch_copy_f4(const void* src, void* dst, size_t n16, hipStream_t s);
-hipError_t launch_brick_min(const VolGeom& g, const VolBufs& b, hipStream_t s);
+hipError_t launch_brick_min(const VolGeom& g, const VolBufs& b, bool all, hipStream_t s);
 hipError_t launch_fill_volume(const VolGeom& g, const VolBufs& b, uint32_t flags, hipStream_t s);
 hipError_t launch_depth_pyramid(const uint16_t* depth, const uint8_t* rgb, const uint8_t* mask, int w, int h,
                                 float scale, const DepthPyramid& p, hipStream_t s);

@@ -131,32 +131,58 @@ hipError_t launch_copy_f4(const void* src, void* dst, size_t n16, hipStream_t s)
     return hipGetLastError();
 }
 
-// Empty-space map: one wave per 8^3 brick, min of sdf over local voxels
-// [8b, 8b + 8] per axis (the brick plus the +1 border every trilinear sample based in the
-// brick reads), clamped to the stored volume.
-__global__ __launch_bounds__(256) void k_brick_min(VolGeom g, const float* __restrict__ sdf, float* __restrict__ bmin) {
+// Empty-space map, in two passes.  k_brick_plain: one wave per 8^3 brick (lane = one of
+// its 64 (x, y) rows, two float4 loads) writes the min of sdf over the brick's own voxels;
+// with all == 0 only bricks the cull pass marked dirty (they overlap a live unit, the only
+// voxels an integrate can change) are recomputed.  k_brick_dilate: bmin[b] = min of the
+// plain map over b + {0,1}^3, which covers [8b, 8b + 8] per axis: every voxel a trilinear
+// sample based in brick b reads.
+__global__ __launch_bounds__(256) void k_brick_plain(VolGeom g, const float* __restrict__ sdf, float* __restrict__ plain,
+                                                     uint8_t* __restrict__ dirty, int all) {
     const unsigned nb = (unsigned)g.nbx * g.nby * g.nbz;
     const unsigned br = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (br >= nb) return;
+    if (!all && !dirty[br]) return;
     const int lane = threadIdx.x & 63;
     const int bz = br % g.nbz, by = (br / g.nbz) % g.nby, bx = br / (g.nbz * g.nby);
-    const int x0 = bx * 8, y0 = by * 8, z0 = bz * 8;
-    const int nx = min(9, g.dimx - x0), ny = min(9, g.dimy - y0), nz = min(9, g.lz - z0);
-    const uint64_t plane = (uint64_t)g.dimy * (uint64_t)g.zs;
+    const int x = bx * 8 + (lane >> 3), y = by * 8 + (lane & 7), z0 = bz * 8;
     float m = 3.0e38f;
-    for (int row = lane; row < nx * ny; row += 64) {
-        const int x = x0 + row / ny, y = y0 + row % ny;
-        const float* p = sdf + (uint64_t)x * plane + (uint64_t)y * g.zs + z0;
-        for (int k = 0; k < nz; ++k) m = fminf(m, p[k]);
+    if (x < g.dimx && y < g.dimy) {
+        const float* p = sdf + (uint64_t)x * ((uint64_t)g.dimy * g.zs) + (uint64_t)y * g.zs + z0;
+        if (z0 + 8 <= g.lz) {
+            const float4 a = *reinterpret_cast<const float4*>(p), c = *reinterpret_cast<const float4*>(p + 4);
+            m = fminf(fminf(fminf(a.x, a.y), fminf(a.z, a.w)), fminf(fminf(c.x, c.y), fminf(c.z, c.w)));
+        } else {
+            for (int k = 0; k < g.lz - z0; ++k) m = fminf(m, p[k]);
+        }
     }
     for (int off = 32; off > 0; off >>= 1) m = fminf(m, __shfl_xor(m, off, 64));
-    if (lane == 0) bmin[br] = m;
+    if (lane == 0) {
+        plain[br] = m;
+        dirty[br] = 0;
+    }
 }
 
-hipError_t launch_brick_min(const VolGeom& g, const VolBufs& b, hipStream_t s) {
+__global__ __launch_bounds__(256) void k_brick_dilate(VolGeom g, const float* __restrict__ plain, float* __restrict__ bmin) {
+    const unsigned nb = (unsigned)g.nbx * g.nby * g.nbz;
+    const unsigned br = blockIdx.x * blockDim.x + threadIdx.x;
+    if (br >= nb) return;
+    const int bz = br % g.nbz, by = (br / g.nbz) % g.nby, bx = br / (g.nbz * g.nby);
+    float m = 3.0e38f;
+    for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 2; ++j)
+            for (int k = 0; k < 2; ++k) {
+                const int xx = bx + i, yy = by + j, zz = bz + k;
+                if (xx < g.nbx && yy < g.nby && zz < g.nbz) m = fminf(m, plain[((unsigned)xx * g.nby + yy) * g.nbz + zz]);
+            }
+    bmin[br] = m;
+}
+
+hipError_t launch_brick_min(const VolGeom& g, const VolBufs& b, bool all, hipStream_t s) {
     const unsigned nb = (unsigned)g.nbx * g.nby * g.nbz;
     if (nb == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_brick_min, dim3((nb + 3) / 4), dim3(256), 0, s, g, b.sdf, b.bmin);
+    hipLaunchKernelGGL(k_brick_plain, dim3((nb + 3) / 4), dim3(256), 0, s, g, b.sdf, b.bplain, b.bdirty, all ? 1 : 0);
+    hipLaunchKernelGGL(k_brick_dilate, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.bplain, b.bmin);
     return hipGetLastError();
 }
 
@@ -391,6 +417,13 @@ __global__ __launch_bounds__(256) void k_cull_units(IntegrateArgs a, UnitGrid ug
     const int ux = (int)(u % ug.nux), uy = (int)((u / ug.nux) % ug.nuy), uz = (int)(u / (ug.nux * ug.nuy));
     const int live = a.cull ? !unit_cull(a, ux * UX, uy * UY, uz * UZ) : 1;
     a.unit_flags[u] = (uint8_t)live;
+    if (live && a.b.bdirty) {  // the bricks this unit overlaps may change (empty-space map)
+        static_assert(UX == 1 && UY == 8 && UZ == 32, "brick marking assumes 1x8x32 units");
+        const VolGeom& g = a.g;
+        const unsigned base = ((unsigned)(ux >> 3) * g.nby + uy) * g.nbz;
+        for (int j = 0; j < 4; ++j)
+            if (uz * 4 + j < g.nbz) a.b.bdirty[base + uz * 4 + j] = 1;
+    }
 }
 
 hipError_t launch_cull(const IntegrateArgs& a, hipStream_t s) {
@@ -820,8 +853,6 @@ __device__ __forceinline__ float sample_sdf(const VolGeom& g, const float* sdf, 
     return tri_eval(sdf, tri_setup(g, px, py, pz));
 }
 
-// The shared ray march of back_proj_kernel (tsdf.cu:90-124) and show_tsdf_kernel
-// (viewer.cu:223-257).  Returns true on a hit and the refined t.
 // Slab test of the march (tsdf.cu:90-100): returns false when the ray misses the volume,
 // else the first sample position and the (exclusive) end of the march.
 __device__ __forceinline__ bool ray_bounds(const VolGeom& g, float ox, float oy, float oz, float dx, float dy,
@@ -869,26 +900,27 @@ __device__ __forceinline__ RayVox ray_vox(const VolGeom& g, float ox, float oy, 
     return r;
 }
 
+__device__ __forceinline__ bool in_skip_box(const SkipCursor& cur, const RayVox& rv, float t) {
+    const float ax = fmaf(t, rv.k[0], rv.c[0]), ay = fmaf(t, rv.k[1], rv.c[1]), az = fmaf(t, rv.k[2], rv.c[2]);
+    return (ax > cur.lo[0]) & (ax < cur.hi[0]) & (ay > cur.lo[1]) & (ay < cur.hi[1]) & (az > cur.lo[2]) &
+           (az < cur.hi[2]);
+}
+
+// Evaluates the sample at p unless the brick map proves it >= voxel/2 (returns false).
+// Caches the last brick looked up and, with `box`, the conservative voxel-coordinate box
+// of a skippable brick for in_skip_box.
 __device__ __forceinline__ bool sample_or_skip(const VolGeom& g, const VolBufs& b, float thr, SkipCursor& cur,
-                                               float px, float py, float pz, float* f, const RayVox* rv = nullptr,
-                                               float t = 0.0f) {
-    if (rv && cur.skip) {  // fast path: still well inside the current skippable brick
-        const float ax = fmaf(t, rv->k[0], rv->c[0]), ay = fmaf(t, rv->k[1], rv->c[1]),
-                    az = fmaf(t, rv->k[2], rv->c[2]);
-        if ((ax > cur.lo[0]) & (ax < cur.hi[0]) & (ay > cur.lo[1]) & (ay < cur.hi[1]) & (az > cur.lo[2]) &
-            (az < cur.hi[2]))
-            return false;
-    }
+                                               float px, float py, float pz, float* f, bool box = false) {
     const TriCoord c = tri_coord(g, px, py, pz);
     if (b.bmin) {
         const int br = brick_of(g, c);
         if (br != cur.brick) {
             cur.brick = br;
             cur.skip = b.bmin[br] >= thr;
-            if (cur.skip && rv) {
+            if (cur.skip && box) {
                 // brick bounds in voxel coordinates, shrunk by a margin far above the
-                // approximation error; the outer faces of the volume extend to infinity
-                // (samples there clamp into the edge brick)
+                // approximation error of RayVox; the outer faces of the volume extend to
+                // infinity (samples there clamp into the edge brick)
                 const int bx = c.xc >> 3, by = c.yc >> 3, bz = c.zl >> 3;
                 const float m = 0.01f;
                 cur.lo[0] = bx == 0 ? -1e30f : 8.0f * bx + m;
@@ -907,30 +939,60 @@ __device__ __forceinline__ bool sample_or_skip(const VolGeom& g, const VolBufs& 
 
 // The shared ray march of back_proj_kernel (tsdf.cu:90-124) and show_tsdf_kernel
 // (viewer.cu:223-257).  Returns true on a hit and the refined t.
+struct MarchStats {
+    unsigned iters = 0, lookups = 0, evals = 0, skipped = 0;
+};
+
 __device__ bool march_ray(const VolGeom& g, const VolBufs& b, float ox, float oy, float oz, float dx, float dy,
-                          float dz, float* t_hit) {
+                          float dz, float* t_hit, MarchStats* st = nullptr) {
     float t, tfar;
     if (!ray_bounds(g, ox, oy, oz, dx, dy, dz, &t, &tfar)) return false;
     const float vx = g.voxel[0];
     const float thr = skip_threshold(g);
     SkipCursor cur;
     const RayVox rv = ray_vox(g, ox, oy, oz, dx, dy, dz);
-    const RayVox* rvp = g.nshards == 1 ? &rv : nullptr;  // local z == global z only unsharded
+    const bool box = g.nshards == 1 && b.bmin;  // local z == global z only unsharded
     float f_t = 1.0f, f_tt = 0.0f;
     bool prev_skipped = false;  // f_t not evaluated: re-evaluate it at t_prev if needed
     float t_prev = t;
-    if (sample_or_skip(g, b, thr, cur, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz), &f_t, rvp, t)) {
-        if (!(f_t > 0.0f)) return false;
-    } else {
-        prev_skipped = true;
+    {
+        float f;
+        if (sample_or_skip(g, b, thr, cur, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz), &f, box)) {
+            if (!(f > 0.0f)) return false;
+            f_t = f;
+        } else {
+            prev_skipped = true;
+        }
     }
     float step = vx;
-    for (; t < tfar; t += step) {
+    // One memory access (a brick lookup or a sample) per iteration; in between, each lane
+    // runs through the samples of its current skippable brick with arithmetic only, so the
+    // lanes of a wave do not wait for each other's memory round trips sample by sample.
+    while (t < tfar) {
+        if (st) st->iters++;
+        if (box && cur.skip && in_skip_box(cur, rv, t)) {
+            do {
+                t_prev = t;
+                t += step;
+                if (st) st->skipped++;
+            } while (t < tfar && in_skip_box(cur, rv, t));
+            prev_skipped = true;  // those samples are >= voxel/2: no hit, no step switch
+            f_tt = 1.0f;
+            if (!(t < tfar)) break;
+        }
         float f;
-        if (!sample_or_skip(g, b, thr, cur, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz), &f, rvp, t)) {
-            prev_skipped = true;  // f >= voxel/2: neither a hit nor a step switch
+        const int brick_before = cur.brick;
+        const bool evaluated =
+            sample_or_skip(g, b, thr, cur, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz), &f, box);
+        if (st) {
+            st->lookups += cur.brick != brick_before;
+            st->evals += evaluated;
+        }
+        if (!evaluated) {
+            prev_skipped = true;
             t_prev = t;
             f_tt = 1.0f;
+            t += step;
             continue;
         }
         f_tt = f;
@@ -938,6 +1000,7 @@ __device__ bool march_ray(const VolGeom& g, const VolBufs& b, float ox, float oy
         if (f_tt < vx / 2.0f) step = vx / 4.0f;
         f_t = f_tt;
         prev_skipped = false;
+        t += step;
     }
     if (!(f_tt < 0.0f)) return false;
     if (prev_skipped) f_t = sample_sdf(g, b.sdf, fmaf(t_prev, dx, ox), fmaf(t_prev, dy, oy), fmaf(t_prev, dz, oz));
@@ -1120,13 +1183,25 @@ hipError_t launch_assoc_march(const AssocArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-// Decision (tsdf.cu:337-389), one wave: per-(i,j) probabilities in parallel, the greedy
-// one-to-one assignment and the new-id order sequentially in lane 0.
-__global__ __launch_bounds__(64) void k_assoc_decide(const AssocTables* __restrict__ T, AssocDecision* D,
-                                                     int* num_objs_dev, float eps) {
+// Decision (tsdf.cu:337-389), one workgroup of 256 lanes, every step parallel:
+// probabilities exp(A/C) per (i, j); per current label i its best previous id j (first
+// maximum, as the reference's strict '>'); per previous id j the winning label i (scanning
+// i in order with a strict '<', i.e. the reference's greedy overwrite); unmatched labels get
+// new ids in the order of their first pixel (tsdf.cu:378-387) by ranking first_px.
+__global__ __launch_bounds__(256) void k_assoc_decide(const AssocTables* __restrict__ T, AssocDecision* D,
+                                                      int* num_objs_dev, float eps) {
     __shared__ double s_prob[kMaxObjects][kMaxObjects];
+    __shared__ int s_bestj[kMaxObjects];
+    __shared__ double s_bestp[kMaxObjects];
+    __shared__ int s_map_i[kMaxObjects];
+    __shared__ double s_map_p[kMaxObjects];
+    __shared__ int s_rev[256];
+    __shared__ unsigned s_first[256];
+    __shared__ int s_newcount;
+    const int tid = threadIdx.x;
     const int max_now = (int)T->max_label + 1;
-    for (int k = threadIdx.x; k < kMaxObjects * kMaxObjects; k += 64) {
+    const double thr = (double)(3.0f * eps);
+    for (int k = tid; k < kMaxObjects * kMaxObjects; k += 256) {
         const int i = k / kMaxObjects, j = k % kMaxObjects;
         double prob = 0.0;
         if (i >= 1 && j >= 1 && i < max_now && i < kMaxObjects) {
@@ -1136,59 +1211,66 @@ __global__ __launch_bounds__(64) void k_assoc_decide(const AssocTables* __restri
         }
         s_prob[i][j] = prob;
     }
+    s_rev[tid] = -1;
+    s_first[tid] = T->first_px[tid];
+    if (tid == 0) s_newcount = 0;
     __syncthreads();
-    if (threadIdx.x != 0) return;
-    const float thr = 3.0f * eps;
-    int map_i[kMaxObjects];
-    double map_p[kMaxObjects];
-    for (int j = 0; j < kMaxObjects; ++j) { map_i[j] = -1; map_p[j] = 0.0; }
-    D->max_obj_now = max_now;
-    for (int i = 0; i < kMaxObjects; ++i) { D->assigned_prev[i] = -1; D->assigned_prob[i] = 0.0f; }
-    for (int i = 1; i < max_now && i < kMaxObjects; ++i) {
+    if (tid < kMaxObjects) {
         int max_j = -1;
         double max_p = 0.0;
-        for (int j = 1; j < kMaxObjects; ++j) {
-            if (s_prob[i][j] > max_p) { max_j = j; max_p = s_prob[i][j]; }
-        }
-        if (max_p > (double)thr) {
-            if (map_i[max_j] < 0 || map_p[max_j] < max_p) { map_i[max_j] = i; map_p[max_j] = max_p; }
-        }
+        if (tid >= 1 && tid < max_now)
+            for (int j = 1; j < kMaxObjects; ++j)
+                if (s_prob[tid][j] > max_p) { max_j = j; max_p = s_prob[tid][j]; }
+        s_bestj[tid] = max_j;
+        s_bestp[tid] = max_p;
     }
-    int rev[256];
-    for (int v = 0; v < 256; ++v) rev[v] = -1;
-    for (int j = 0; j < kMaxObjects; ++j) {
-        if (map_i[j] >= 0) {
-            rev[map_i[j]] = j;
-            D->assigned_prev[map_i[j]] = j;
-            D->assigned_prob[map_i[j]] = (float)map_p[j];
-        }
+    __syncthreads();
+    if (tid < kMaxObjects) {
+        int mi = -1;
+        double mp = 0.0;
+        for (int i = 1; i < max_now && i < kMaxObjects; ++i)
+            if (s_bestj[i] == tid && s_bestp[i] > thr && (mi < 0 || mp < s_bestp[i])) { mi = i; mp = s_bestp[i]; }
+        s_map_i[tid] = mi;
+        s_map_p[tid] = mp;
+        D->assigned_prev[tid] = -1;
+        D->assigned_prob[tid] = 0.0f;
     }
-    int num = *num_objs_dev;
-    D->num_objs_before = num;
-    // unmatched labels get new ids in order of their first pixel (tsdf.cu:378-387)
-    bool done[256];
-    for (int v = 0; v < 256; ++v) { done[v] = false; D->lut[v] = (unsigned char)v; }
-    for (int v = 1; v < 256; ++v) if (rev[v] >= 0) { D->lut[v] = (unsigned char)rev[v]; done[v] = true; }
-    for (;;) {
-        unsigned best = 0xFFFFFFFFu;
-        int bv = -1;
-        for (int v = 1; v < 256; ++v) {
-            if (!done[v] && T->first_px[v] < best) { best = T->first_px[v]; bv = v; }
-        }
-        if (bv < 0) break;
-        done[bv] = true;
-        D->lut[bv] = (unsigned char)num;
-        ++num;
+    __syncthreads();
+    if (tid < kMaxObjects && s_map_i[tid] >= 0) {
+        s_rev[s_map_i[tid]] = tid;
+        D->assigned_prev[s_map_i[tid]] = tid;
+        D->assigned_prob[s_map_i[tid]] = (float)s_map_p[tid];
     }
-    D->num_objs_after = num;
-    D->bad_label = (num > kMaxObjects || max_now > kMaxObjects) ? 1 : 0;
-    *num_objs_dev = num;
+    __syncthreads();
+    const int num = *num_objs_dev;
+    // lanes 1..255: a present, unmatched label gets num + (rank of its first pixel)
+    const bool fresh = tid >= 1 && s_rev[tid] < 0 && s_first[tid] != 0xFFFFFFFFu;
+    int lut = tid;
+    if (tid >= 1 && s_rev[tid] >= 0) {
+        lut = s_rev[tid];
+    } else if (fresh) {
+        int rank = 0;
+        for (int u = 1; u < 256; ++u)
+            rank += (s_rev[u] < 0 && s_first[u] != 0xFFFFFFFFu && s_first[u] < s_first[tid]) ? 1 : 0;
+        lut = num + rank;
+        atomicAdd(&s_newcount, 1);
+    }
+    D->lut[tid] = (unsigned char)lut;
+    __syncthreads();
+    if (tid == 0) {
+        const int after = num + s_newcount;
+        D->max_obj_now = max_now;
+        D->num_objs_before = num;
+        D->num_objs_after = after;
+        D->bad_label = (after > kMaxObjects || max_now > kMaxObjects) ? 1 : 0;
+        *num_objs_dev = after;
+    }
 }
 
 hipError_t launch_assoc_decide(const AssocTables* t, AssocDecision* d, int num_objs, float eps,
                                int* num_objs_dev, hipStream_t s) {
     (void)num_objs;
-    hipLaunchKernelGGL(k_assoc_decide, dim3(1), dim3(64), 0, s, t, d, num_objs_dev, eps);
+    hipLaunchKernelGGL(k_assoc_decide, dim3(1), dim3(256), 0, s, t, d, num_objs_dev, eps);
     return hipGetLastError();
 }
 
@@ -1255,7 +1337,9 @@ __global__ __launch_bounds__(256) void k_render(RenderArgs a) {
     ray_render(a.cam, x, y, &ox, &oy, &oz, &dx, &dy, &dz);
     uint8_t b = 0, gch = 0, r = 0;
     float th = -1.0f;
-    if (march_ray(a.g, a.b, ox, oy, oz, dx, dy, dz, &t)) {
+    MarchStats ms;
+    const uint64_t t_start = a.ray_stats ? __builtin_amdgcn_s_memrealtime() : 0;
+    if (march_ray(a.g, a.b, ox, oy, oz, dx, dy, dz, &t, a.ray_stats ? &ms : nullptr)) {
         th = t;
         const Tri tr = tri_setup(a.g, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
         shade_hit(a.g, a.b, tr, a.mode, a.color_i32, a.palette, &b, &gch, &r);
@@ -1264,6 +1348,18 @@ __global__ __launch_bounds__(256) void k_render(RenderArgs a) {
     a.out_bgr[(size_t)px * 3 + 1] = gch;
     a.out_bgr[(size_t)px * 3 + 2] = r;
     if (a.out_t) a.out_t[px] = th;
+    if (a.ray_stats) {  // instrumentation
+        unsigned* q = a.ray_stats + (size_t)px * 4;
+        q[0] = ms.iters; q[1] = ms.lookups; q[2] = ms.evals; q[3] = ms.skipped;
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        const size_t npx = (size_t)a.width * a.height;
+        const unsigned wave = (blockIdx.y * gridDim.x + blockIdx.x) * 4 + (threadIdx.x >> 6);
+        if ((threadIdx.x & 63) == 0) {
+            unsigned long long* w = reinterpret_cast<unsigned long long*>(a.ray_stats + npx * 4) + wave * 2;
+            w[0] = t_start;
+            w[1] = t_end;
+        }
+    }
 }
 
 hipError_t launch_render(const RenderArgs& a, hipStream_t s) {
