@@ -80,6 +80,19 @@ void oracle_integrate(const int32_t* dims, const float* geo, const float* K9, co
     if (!zmap) lz = g.dz;
     const int sem = flags & 1, gate = flags & 2, ci32 = flags & 4, vote = flags & 8;
     uint64_t n_touch = 0, n_gate = 0, n_bad = 0;
+    /* Screen map of the build's f32 contract: proj = E[0:3] . (p, 1) and
+       screen = K . proj (tsdf.cu:31-39) are folded into s = M p + m, M = RN(K E3) and
+       m = RN(K t), each entry a left-to-right sum of three double products rounded once;
+       every affine row is evaluated as aff(r, c, p) = fma(r2, pz, fma(r1, py, fma(r0, px, c))). */
+    float M[9], m[3];
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j)
+            M[i * 3 + j] = (float)((double)K9[i * 3 + 0] * (double)E16[0 * 4 + j] +
+                                   (double)K9[i * 3 + 1] * (double)E16[1 * 4 + j] +
+                                   (double)K9[i * 3 + 2] * (double)E16[2 * 4 + j]);
+        m[i] = (float)((double)K9[i * 3 + 0] * (double)E16[3] + (double)K9[i * 3 + 1] * (double)E16[7] +
+                       (double)K9[i * 3 + 2] * (double)E16[11]);
+    }
     for (int x = x_begin; x < x_end; ++x) {
         const float px = fmaf((float)x, g.voxel[0], g.start[0]);
         for (int y = 0; y < g.dy; ++y) {
@@ -88,14 +101,12 @@ void oracle_integrate(const int32_t* dims, const float* geo, const float* K9, co
                 const int gz = zmap ? zmap[z] : z;
                 if (gz >= g.dz) continue;
                 const float pz = fmaf((float)gz, g.voxel[2], g.start[2]);
-                /* proj = extrinsic2init[0:3] . (p, 1)   (tsdf.cu:31-34) */
-                const float qx = o_dot3(E16[0], E16[1], E16[2], px, py, pz) + E16[3];
-                const float qy = o_dot3(E16[4], E16[5], E16[6], px, py, pz) + E16[7];
-                const float qz = o_dot3(E16[8], E16[9], E16[10], px, py, pz) + E16[11];
-                /* screen = K[0:3,0:3] . proj, perspective divide, floor (tsdf.cu:35-44) */
-                const float sx = o_dot3(K9[0], K9[1], K9[2], qx, qy, qz);
-                const float sy = o_dot3(K9[3], K9[4], K9[5], qx, qy, qz);
-                const float sz = o_dot3(K9[6], K9[7], K9[8], qx, qy, qz);
+                /* camera depth proj.z (tsdf.cu:31-34) and screen position (tsdf.cu:35-39) */
+                const float qz = fmaf(E16[10], pz, fmaf(E16[9], py, fmaf(E16[8], px, E16[11])));
+                const float sx = fmaf(M[2], pz, fmaf(M[1], py, fmaf(M[0], px, m[0])));
+                const float sy = fmaf(M[5], pz, fmaf(M[4], py, fmaf(M[3], px, m[1])));
+                const float sz = fmaf(M[8], pz, fmaf(M[7], py, fmaf(M[6], px, m[2])));
+                /* perspective divide and floor (tsdf.cu:40-44) */
                 const int ix = o_f2i_rd(sx / sz);
                 const int iy = o_f2i_rd(sy / sz);
                 if (ix < 0 || ix >= width || iy < 0 || iy >= height) continue;

@@ -86,6 +86,9 @@ struct semtsdf_vol {
     float* render_t_d = nullptr;
     unsigned long long* counters_d = nullptr;
     uint8_t* unit_flags_d = nullptr;
+    unsigned* unit_list_d = nullptr;  // live units of the frame (cull pass)
+    unsigned* list_count_d = nullptr; // [kListSegs]
+    float* rcp_table_d = nullptr;    // RN(1/n), n = 1..kRcpTable
     AssocDecision* decision_h = nullptr;  // pinned
     // Z-sharded raycast protocol (allocated on first use)
     void* ray_state_d = nullptr;   // ShardRayState arrays, 6 x npx x 4 B
@@ -120,9 +123,9 @@ int dev_alloc(semtsdf_vol* v, void** p, size_t bytes) {
 
 void free_all(semtsdf_vol* v) {
     void* ptrs[] = {v->b.sdf, v->b.wt, v->b.bmin, v->b.bplain, v->b.bdirty, v->b.color, v->b.hist, v->b.cls, v->b.cls_cnt, v->depth_d, v->rgb_d,
-                    v->mask_d, v->cls_d, v->pyr.metres, v->pyr.rgbl, v->pyr.l0, v->pyr.l1, v->tables_d, v->decision_d,
+                    v->mask_d, v->cls_d, v->pyr.px, v->pyr.l0, v->pyr.l1, v->tables_d, v->decision_d,
                     v->num_objs_d, v->probs_d, v->box_d, v->palette_d, v->render_d, v->render_t_d,
-                    v->counters_d, v->unit_flags_d, v->ray_state_d};
+                    v->counters_d, v->unit_flags_d, v->ray_state_d, v->unit_list_d, v->list_count_d, v->rcp_table_d};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (v->decision_h) (void)hipHostFree(v->decision_h);
@@ -184,6 +187,27 @@ void timing_end(semtsdf_vol* v, std::vector<EventPair>& vec, hipStream_t s, Even
     vec.push_back(*ep);
 }
 
+// Screen map of the integrate contract: s = M p + m with M = RN(K E3),
+// m = RN(K t), each entry a left-to-right sum of three double products rounded once to
+// f32 (oracle_integrate restates it); ftol is the exactness window of the reciprocal pixel
+// floor in k_integrate.
+void screen_map(IntegrateArgs& a) {
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) {
+            const double acc = (double)a.K[i * 3 + 0] * (double)a.E[0 * 4 + j] +
+                               (double)a.K[i * 3 + 1] * (double)a.E[1 * 4 + j] +
+                               (double)a.K[i * 3 + 2] * (double)a.E[2 * 4 + j];
+            a.M[i * 3 + j] = (float)acc;
+        }
+        const double acc = (double)a.K[i * 3 + 0] * (double)a.E[3] + (double)a.K[i * 3 + 1] * (double)a.E[7] +
+                           (double)a.K[i * 3 + 2] * (double)a.E[11];
+        a.m[i] = (float)acc;
+    }
+    int b = 1;
+    while (b < (a.width > a.height ? a.width : a.height) + 2) b <<= 1;
+    a.ftol = 0.5f - ldexpf((float)b, -21);
+}
+
 int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d, const uint8_t* mask_d,
                    const int32_t* cls_d, const float E[16], hipStream_t s) {
     if (!E) return fail(SEMTSDF_ERR_INVALID, "E is NULL");
@@ -215,43 +239,26 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
     a.pyr = v->pyr;
     a.counters = v->counters_d;
     a.unit_flags = v->unit_flags_d;
+    a.unit_list = v->unit_list_d;
+    a.list_count = v->list_count_d;
+    a.rcp_table = v->rcp_table_d;
+    screen_map(a);
     a.pinhole = (a.K[1] == 0.0f && a.K[3] == 0.0f && a.K[6] == 0.0f && a.K[7] == 0.0f && a.K[8] == 1.0f) ? 1 : 0;
-    {
-        static const char* deal = getenv("SEMTSDF_DEAL");  // A/B of the work deal (default 0)
-        a.deal = deal ? atoi(deal) : 0;
-    }
     a.rmu = 1.0f / v->g.mu;  // IEEE: the correctly rounded reciprocal
     a.fastdiv = (v->g.mu >= 0x1p-20f && v->g.mu <= 0x1p20f && a.debug != 8) ? 1 : 0;
     if (a.debug == 2) return SEMTSDF_OK;
     EventPair epp;
     timing_begin(v, v->ev_prep, s, &epp);
-    HIPC(launch_depth_pyramid(depth_d, rgb_d, mask_d, v->p.width, v->p.height, v->p.depth_scale, v->pyr, s));
+    HIPC(launch_depth_pyramid(depth_d, rgb_d, mask_d, v->p.width, v->p.height, v->p.depth_scale, v->pyr,
+                              v->list_count_d, s));
     HIPC(launch_cull(a, s));
     timing_end(v, v->ev_prep, s, &epp);
     v->n_prep++;
-    // instrumentation: SEMTSDF_WAVE_STATS=<file> appends per-wave start/end/units records
-    static const char* ws_path = getenv("SEMTSDF_WAVE_STATS");
-    unsigned long long* ws = nullptr;
-    if (ws_path && !(a.flags & 0x80000000u)) {
-        HIPC(hipMalloc((void**)&ws, 8192 * 4 * sizeof(unsigned long long)));
-        HIPC(hipMemsetAsync(ws, 0, 8192 * 4 * sizeof(unsigned long long), s));
-        a.wave_stats = ws;
-    }
     EventPair ep;  // events bracket the integrate kernel alone (the roofline kernel)
     timing_begin(v, v->ev_integrate, s, &ep);
     HIPC(launch_integrate(a, s));
     timing_end(v, v->ev_integrate, s, &ep);
     v->bmin_dirty = true;
-    if (ws) {
-        std::vector<unsigned long long> h(8192 * 4);
-        HIPC(hipMemcpyAsync(h.data(), ws, h.size() * 8, hipMemcpyDeviceToHost, s));
-        HIPC(hipStreamSynchronize(s));
-        HIPC(hipFree(ws));
-        if (FILE* f = fopen(ws_path, "ab")) {
-            fwrite(h.data(), 8, h.size(), f);
-            fclose(f);
-        }
-    }
     v->n_integrate++;
     return SEMTSDF_OK;
 }
@@ -553,13 +560,19 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     DepthPyramid& pyr = v->pyr;
     pyr.w0 = (p->width + 7) / 8; pyr.h0 = (p->height + 7) / 8;
     pyr.w1 = (p->width + 31) / 32; pyr.h1 = (p->height + 31) / 32;
-    pyr.wb = (p->width + 1) / 2;
-    const size_t pxb = (size_t)pyr.wb * ((p->height + 7) / 8) * 16;  // block-linear, padded
-    if ((rc = dev_alloc(v, (void**)&pyr.metres, pxb * 4))) return bail(rc);
-    if ((rc = dev_alloc(v, (void**)&pyr.rgbl, pxb * 4))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&pyr.px, px * 8))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&pyr.l0, (size_t)pyr.w1 * 4 * pyr.h1 * 4 * 2))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&pyr.l1, (size_t)pyr.w1 * pyr.h1 * 2))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->unit_flags_d, unit_count(g)))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&v->unit_list_d, unit_list_capacity(g) * sizeof(unsigned)))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&v->list_count_d, kListSegs * sizeof(unsigned)))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&v->rcp_table_d, kRcpTable * sizeof(float)))) return bail(rc);
+    {
+        float t[kRcpTable];
+        for (int i = 0; i < kRcpTable; ++i) t[i] = 1.0f / (float)(i + 1);  // IEEE: correctly rounded
+        if (hipMemcpy(v->rcp_table_d, t, sizeof(t), hipMemcpyHostToDevice) != hipSuccess)
+            return bail(fail(SEMTSDF_ERR_HIP, "rcp table upload failed"));
+    }
     if ((rc = dev_alloc(v, (void**)&v->tables_d, sizeof(AssocTables)))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->decision_d, sizeof(AssocDecision)))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->num_objs_d, 16))) return bail(rc);

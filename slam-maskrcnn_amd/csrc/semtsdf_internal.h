@@ -8,6 +8,8 @@
 namespace semtsdf {
 
 constexpr int kMaxObjects = 32;
+constexpr int kRcpTable = 1024;  // RN(1/n) table of the running means (w + 1 <= kRcpTable)
+constexpr int kListSegs = 8;     // segments (and counters) of the live-unit list
 
 // Geometry of the locally stored part of the volume.
 struct VolGeom {
@@ -37,19 +39,11 @@ struct VolBufs {
     uint8_t* bdirty;   // per 8^3 brick: overlaps a unit integrated since the last map update
 };
 
-// Per-frame depth pyramid used by the brick culler: max raw depth over tiles of
-// 8, 32 and 128 pixels.
-// The per-pixel images are block-linear: 2 (wide) x 8 (tall) pixel blocks of 16 values (one
-// 64-B line), blocks row-major.  The pixels a unit of 8 voxel rows projects to are tall
-// and narrow, so a wave's gather touches ~45 % fewer lines than with row-major images.
-__host__ __device__ inline int pix_block_index(int u, int v, int wb) {
-    return (((v >> 3) * wb + (u >> 1)) << 4) | ((v & 7) << 1) | (u & 1);
-}
-
+// Per-frame images of the integrate: depth in metres and rgb+label per pixel (row-major,
+// W x H), and the max raw depth over 8- and 32-pixel tiles used by the unit culler.
 struct DepthPyramid {
-    float* metres;  // block-linear [H][W] depth / depth_scale (IEEE division, tsdf.cu:49)
-    uint32_t* rgbl; // block-linear r | g << 8 | b << 16 | label << 24 (one gather per gated voxel)
-    int wb;         // blocks per block row = ceil(W / 2)
+    uint2* px;      // [H][W] pixel records {bits of depth / depth_scale (IEEE, tsdf.cu:49),
+                    //                       r | g << 8 | b << 16 | label << 24}: one 8-B gather per voxel
     uint16_t* l0;  // [ceil(H/8)][ceil(W/8)]
     uint16_t* l1;  // [ceil(H/32)][ceil(W/32)]
     int w0, h0, w1, h1;
@@ -60,6 +54,10 @@ struct IntegrateArgs {
     VolBufs b;
     float E[12];     // rows 0..2 of extrinsic2init
     float K[9];      // rows 0..2, cols 0..2 of the intrinsic
+    float M[9];      // RN(K E[0:3,0:3]) (products summed in double): screen map s = M p + m
+    float m[3];      // RN(K E[0:3,3])
+    float ftol;      // 0.5 - B 2^-21, B = 2^ceil(log2(max(W, H) + 2)): exactness window of the pixel floor
+    const float* rcp_table;        // [kRcpTable] RN(1/n), n = 1.. (volume constant)
     int width, height;
     float depth_scale;
     float gate;
@@ -76,8 +74,8 @@ struct IntegrateArgs {
     int pinhole;                   // K rows are (fx 0 cx; 0 fy cy; 0 0 1)
     float rmu;                     // RN(1/mu), for the exact division by mu (k_integrate)
     int fastdiv;                   // mu in [2^-20, 2^20]: divisions by mu/(w+1) via RN reciprocals
-    int deal;                      // work deal of k_integrate: 1 batch per wave, 0 persistent
-    unsigned long long* wave_stats;  // instrumentation (SEMTSDF_WAVE_STATS): per wave t0, t1, units, hw id
+    unsigned* unit_list;           // live units, kListSegs segments (k_cull_units)
+    unsigned* list_count;          // [kListSegs] entries per segment (zeroed by the frame prepass)
 };
 
 // Association accumulators (fixed point, scale 2^28, deterministic).
@@ -183,11 +181,12 @@ hipError_t launch_copy_f4(const void* src, void* dst, size_t n16, hipStream_t s)
 hipError_t launch_brick_min(const VolGeom& g, const VolBufs& b, bool all, hipStream_t s);
 hipError_t launch_fill_volume(const VolGeom& g, const VolBufs& b, uint32_t flags, hipStream_t s);
 hipError_t launch_depth_pyramid(const uint16_t* depth, const uint8_t* rgb, const uint8_t* mask, int w, int h,
-                                float scale, const DepthPyramid& p, hipStream_t s);
+                                float scale, const DepthPyramid& p, unsigned* list_count, hipStream_t s);
 hipError_t launch_color_chunk(const void* src, void* dst, bool to_ref, bool i32, const VolGeom& g, uint64_t v0,
                               uint64_t nv, hipStream_t s);
 hipError_t launch_integrate(const IntegrateArgs& a, hipStream_t s); // persistent cull + integrate
 uint64_t unit_count(const VolGeom& g);
+uint64_t unit_list_capacity(const VolGeom& g);
 hipError_t launch_cull(const IntegrateArgs& a, hipStream_t s);       // per-unit cull flags
 hipError_t launch_mask_stats(const uint8_t* mask, int npx, AssocTables* t, hipStream_t s);
 hipError_t launch_assoc_march(const AssocArgs& a, hipStream_t s);

@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <limits.h>
+#include <stdlib.h>
 #include "semtsdf_internal.h"
 
 namespace semtsdf {
@@ -204,10 +205,11 @@ hipError_t launch_fill_volume(const VolGeom& g, const VolBufs& b, uint32_t flags
 // ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restrict__ depth, const uint8_t* __restrict__ rgb,
                                                        const uint8_t* __restrict__ mask, int w, int h, float scale,
-                                                       int vec, DepthPyramid p) {
+                                                       int vec, DepthPyramid p, unsigned* list_count) {
     __shared__ unsigned s_m[32][8];
     const int tx = blockIdx.x, ty = blockIdx.y;
     const int t = threadIdx.x;
+    if (list_count && tx == 0 && ty == 0 && t < kListSegs) list_count[t] = 0u;  // this frame's live-unit list
     const int r = t >> 3;          // row in tile
     const int c4 = (t & 7) * 4;    // first column in tile
     const int yy = ty * 32 + r;
@@ -219,33 +221,32 @@ __global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restric
             const ushort4 d4 = *reinterpret_cast<const ushort4*>(depth + px0);
             const unsigned d[4] = {d4.x, d4.y, d4.z, d4.w};
             m = max(max(d[0], d[1]), max(d[2], d[3]));
-            const int b0 = pix_block_index(x0, yy, p.wb), b1 = pix_block_index(x0 + 2, yy, p.wb);
-            *reinterpret_cast<float2*>(p.metres + b0) = make_float2((float)d[0] / scale, (float)d[1] / scale);
-            *reinterpret_cast<float2*>(p.metres + b1) = make_float2((float)d[2] / scale, (float)d[3] / scale);
+            uint4 o = make_uint4(0, 0, 0, 0);
             if (rgb) {
                 const uint32_t* c = reinterpret_cast<const uint32_t*>(rgb + px0 * 3);
                 const uint32_t c0 = c[0], c1 = c[1], c2 = c[2];  // r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3
                 const uint32_t lab = mask ? *reinterpret_cast<const uint32_t*>(mask + px0) : 0u;
-                uint4 o;
                 o.x = (c0 & 0xFFFFFFu) | ((lab & 0xFFu) << 24);
                 o.y = (c0 >> 24) | ((c1 & 0xFFFFu) << 8) | (((lab >> 8) & 0xFFu) << 24);
                 o.z = (c1 >> 16) | ((c2 & 0xFFu) << 16) | (((lab >> 16) & 0xFFu) << 24);
                 o.w = (c2 >> 8) | ((lab >> 24) << 24);
-                *reinterpret_cast<uint2*>(p.rgbl + b0) = make_uint2(o.x, o.y);
-                *reinterpret_cast<uint2*>(p.rgbl + b1) = make_uint2(o.z, o.w);
             }
+            // depth[img] / 5000.f (tsdf.cu:49), once per pixel
+            uint4* dst = reinterpret_cast<uint4*>(p.px + px0);
+            dst[0] = make_uint4(__float_as_uint((float)d[0] / scale), o.x, __float_as_uint((float)d[1] / scale), o.y);
+            dst[1] = make_uint4(__float_as_uint((float)d[2] / scale), o.z, __float_as_uint((float)d[3] / scale), o.w);
         } else {
             for (int k = 0; k < 4 && x0 + k < w; ++k) {
                 const size_t px = px0 + k;
                 const unsigned d = depth[px];
                 m = max(m, d);
-                const int bi = pix_block_index(x0 + k, yy, p.wb);
-                p.metres[bi] = (float)d / scale;  // depth[img] / 5000.f (tsdf.cu:49)
+                unsigned c = 0;
                 if (rgb) {
                     const unsigned lab = mask ? (unsigned)mask[px] : 0u;
-                    p.rgbl[bi] = (unsigned)rgb[px * 3] | ((unsigned)rgb[px * 3 + 1] << 8) |
-                                 ((unsigned)rgb[px * 3 + 2] << 16) | (lab << 24);
+                    c = (unsigned)rgb[px * 3] | ((unsigned)rgb[px * 3 + 1] << 8) | ((unsigned)rgb[px * 3 + 2] << 16) |
+                        (lab << 24);
                 }
+                p.px[px] = make_uint2(__float_as_uint((float)d / scale), c);
             }
         }
     }
@@ -273,11 +274,11 @@ __global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restric
 }
 
 hipError_t launch_depth_pyramid(const uint16_t* depth, const uint8_t* rgb, const uint8_t* mask, int w, int h,
-                                float scale, const DepthPyramid& p, hipStream_t s) {
-    const bool vec = (w % 4 == 0) && ((uintptr_t)depth % 8 == 0) && (!rgb || (uintptr_t)rgb % 4 == 0) &&
+                                float scale, const DepthPyramid& p, unsigned* list_count, hipStream_t s) {
+    const bool vec = (w % 4 == 0) && ((uintptr_t)depth % 8 == 0) && ((uintptr_t)p.px % 16 == 0) && (!rgb || (uintptr_t)rgb % 4 == 0) &&
                      (!mask || (uintptr_t)mask % 4 == 0);
     hipLaunchKernelGGL(k_depth_pyramid, dim3(p.w1, p.h1), dim3(256), 0, s, depth, rgb, mask, w, h, scale,
-                       vec ? 1 : 0, p);
+                       vec ? 1 : 0, p, list_count);
     return hipGetLastError();
 }
 
@@ -306,8 +307,6 @@ __device__ __forceinline__ int floor_div(float a, float b) {
     return f2i_rd(a / b);
 }
 
-// Table of RN(1/n), n = 1..kRcpTable, for the weighted running means (w + 1 <= kRcpTable).
-constexpr int kRcpTable = 1024;
 
 // (c*w + x) / (w+1) for 0 <= c, x <= 255 via the float reciprocal plus one exact integer
 // correction (quotient <= 255, so the float estimate is within one of it); integer
@@ -410,286 +409,489 @@ __host__ __device__ inline UnitGrid unit_grid(const VolGeom& g) {
     return u;
 }
 
-// Cull pass: one lane per unit.  flags[u] = 1 when the unit may hold a touched voxel.
-__global__ __launch_bounds__(256) void k_cull_units(IntegrateArgs a, UnitGrid ug) {
+// Live-unit list: kListSegs segments, segment c filled by the cull workgroups b with
+// b % kListSegs == c (one counter per segment keeps the same-address atomics per counter
+// to ~1/8 of the workgroups).  Capacity of a segment: all units of its workgroups.
+__host__ __device__ inline unsigned list_seg_cap(const UnitGrid& ug) {
+    const unsigned groups = (ug.n + 255u) / 256u;
+    return (groups + kListSegs - 1u) / kListSegs * 256u;
+}
+
+// Cull pass: one lane per unit (x fastest).  flags[u] = 1 when the unit may hold a touched
+// voxel; the live units of a workgroup are appended to its segment of the live-unit list
+// (their order is irrelevant: units are independent).
+__global__ __launch_bounds__(256) void k_cull_units(IntegrateArgs a, UnitGrid ug, unsigned seg_cap) {
+    __shared__ unsigned s_cnt[4];
+    __shared__ unsigned s_base;
     const unsigned u = blockIdx.x * blockDim.x + threadIdx.x;
-    if (u >= ug.n) return;
-    const int ux = (int)(u % ug.nux), uy = (int)((u / ug.nux) % ug.nuy), uz = (int)(u / (ug.nux * ug.nuy));
-    const int live = a.cull ? !unit_cull(a, ux * UX, uy * UY, uz * UZ) : 1;
-    a.unit_flags[u] = (uint8_t)live;
-    if (live && a.b.bdirty) {  // the bricks this unit overlaps may change (empty-space map)
-        static_assert(UX == 1 && UY == 8 && UZ == 32, "brick marking assumes 1x8x32 units");
-        const VolGeom& g = a.g;
-        const unsigned base = ((unsigned)(ux >> 3) * g.nby + uy) * g.nbz;
-        for (int j = 0; j < 4; ++j)
-            if (uz * 4 + j < g.nbz) a.b.bdirty[base + uz * 4 + j] = 1;
+    int live = 0;
+    if (u < ug.n) {
+        const int ux = (int)(u % ug.nux), uy = (int)((u / ug.nux) % ug.nuy), uz = (int)(u / (ug.nux * ug.nuy));
+        live = a.cull ? !unit_cull(a, ux * UX, uy * UY, uz * UZ) : 1;
+        a.unit_flags[u] = (uint8_t)live;
+        if (live && a.b.bdirty) {  // the bricks this unit overlaps may change (empty-space map)
+            static_assert(UX == 1 && UY == 8 && UZ == 32, "brick marking assumes 1x8x32 units");
+            const VolGeom& g = a.g;
+            const unsigned base = ((unsigned)(ux >> 3) * (unsigned)g.nby + (unsigned)uy) * (unsigned)g.nbz;
+            for (int j = 0; j < 4; ++j)
+                if (uz * 4 + j < g.nbz) a.b.bdirty[base + (unsigned)uz * 4u + (unsigned)j] = 1;
+        }
+    }
+    const int lane = (int)(threadIdx.x & 63u), wv = (int)(threadIdx.x >> 6);
+    const unsigned long long bal = __ballot(live);
+    if (lane == 0) s_cnt[wv] = (unsigned)__popcll(bal);
+    __syncthreads();
+    const unsigned seg = blockIdx.x % (unsigned)kListSegs;
+    if (threadIdx.x == 0) {
+        const unsigned tot = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+        s_base = tot ? atomicAdd(a.list_count + seg, tot) : 0u;
+    }
+    __syncthreads();
+    if (live) {
+        unsigned off = s_base + (unsigned)__popcll(bal & ((1ull << lane) - 1ull));
+        for (int w = 0; w < wv; ++w) off += s_cnt[w];
+        a.unit_list[seg * seg_cap + off] = u;
     }
 }
 
 hipError_t launch_cull(const IntegrateArgs& a, hipStream_t s) {
     const UnitGrid ug = unit_grid(a.g);
     if (ug.n == 0) return hipSuccess;  // a shard that owns no chunk
-    hipLaunchKernelGGL(k_cull_units, dim3((ug.n + 255) / 256), dim3(256), 0, s, a, ug);
+    hipLaunchKernelGGL(k_cull_units, dim3((ug.n + 255) / 256), dim3(256), 0, s, a, ug, list_seg_cap(ug));
     return hipGetLastError();
 }
 
 uint64_t unit_count(const VolGeom& g) { return unit_grid(g).n; }
+uint64_t unit_list_capacity(const VolGeom& g) { return (uint64_t)list_seg_cap(unit_grid(g)) * kListSegs; }
 
-// Pass 2: persistent wavefronts over units.  Branch-free classification and update
-// (selects instead of divergent ifs) keep the scalar/branch overhead per item low; the only
-// divergent branches left guard the rare exact-division fallback, the gated colour /
-// histogram path and the stores.
-template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT, bool SHARD, bool PIN>
-__global__ __launch_bounds__(256) void k_integrate(IntegrateArgs a, UnitGrid ug) {
+// Exact floor of the colour running mean (c*w + x) / (w + 1) for 0 <= c, x <= 255 and
+// w + 1 <= kRcpTable, from r = RN(1/(w+1)): floor(RN(num*r + 2^-12)) equals the integer
+// quotient (the product is within 2.3e-5 of num/(w+1), whose fraction is 0 or in
+// [1/(w+1), 1 - 1/(w+1)]; checked exhaustively, tests/test_oracle_props.py).
+__device__ __forceinline__ unsigned avg_u8(unsigned c, unsigned x, unsigned w, float r) {
+    const unsigned num = c * w + x;
+    return (unsigned)fmaf((float)num, r, 0x1p-12f);
+}
+
+// ---- the integrate of one unit in stages ---------------------------------------------------
+// A unit (UX x UY x UZ voxels) is handled by one wavefront: lane = (zq, y) = (lane & 7,
+// lane >> 3) owns planes 4zq..4zq+3 of row y, so every state access is one 16-byte vector
+// per lane.  Stages:
+//   project  — screen position, exact pixel, gather of the pixel records (depth, rgb, label)
+//   classify — tsdf.cu:46-52 tests
+//   load     — state of the touched lanes (sdf, weight; colour and histogram words of the
+//              gated voxels)
+//   compute  — tsdf.cu:56-68 running means
+//   store
+// The wave software-pipelines its units in the order
+//   project(k+1)  compute(k)  classify(k+1)  store(k)  load(k+1)
+// so the state loads of unit k are in flight under the projection of k+1 and the pixel
+// gathers of k+1 under the compute of k.  s_waitcnt vmcnt counts memory operations in
+// issue order, and the compiler can only count the ones it knows were issued: every load
+// is therefore unconditional (lanes with nothing to load read one dummy line), stores come
+// after the waits of the iteration, and every wait names the oldest group in flight.  The
+// histogram increment is a plain load/store of the 4 words of a lane (one lane owns a
+// voxel within a frame); a lane whose gated voxels carry different labels (object borders)
+// takes no-return atomics.
+struct UnitPos {
+    int x, uy, uz;  // wave-uniform
+};
+
+__device__ __forceinline__ UnitPos unit_pos(const UnitGrid& ug, unsigned u) {
+    const unsigned uxy = u % (ug.nux * ug.nuy);
+    UnitPos p;
+    p.x = (int)(uxy % ug.nux);
+    p.uy = (int)(uxy / ug.nux);
+    p.uz = (int)(u / (ug.nux * ug.nuy));
+    return p;
+}
+
+__device__ __forceinline__ uint64_t unit_base(const VolGeom& g, const UnitPos& up) {
+    return (uint64_t)up.x * ((uint64_t)g.dimy * (uint64_t)g.zs) + (uint64_t)(up.uy * UY) * (uint64_t)g.zs +
+           (uint64_t)(up.uz * UZ);
+}
+
+struct Proj {
+    float qz[4];
+    uint2 rec[4];  // gathered pixel record {metres bits, rgbl}, valid where img >= 0
+    int img[4];    // pixel index, -1 off-image (or an invalid plane)
+};
+
+struct Cls {
+    float fv[4];
+    unsigned tmask, gmask;
+    uint32_t pix[4];   // rgbl of the voxels' pixels
+    unsigned hmode;    // 1: the gated voxels share label hlab < 32 (one 16-B histogram RMW); 2: atomics
+    unsigned hlab;
+    int img[4];        // vote mode
+};
+
+// What stage_store needs of a classification: masks, histogram mode/label and the 4 labels.
+struct StoreMeta {
+    unsigned meta;  // tmask | gmask << 4 | hmode << 8 | hlab << 16
+    unsigned labs;  // label of voxel k in bits 8k..8k+7
+};
+
+__device__ __forceinline__ StoreMeta store_meta(const Cls& C) {
+    StoreMeta m;
+    m.meta = C.tmask | (C.gmask << 4) | (C.hmode << 8) | (C.hlab << 16);
+    m.labs = (C.pix[0] >> 24) | ((C.pix[1] >> 24) << 8) | ((C.pix[2] >> 24) << 16) | ((C.pix[3] >> 24) << 24);
+    return m;
+}
+
+struct Ld {
+    float4 s4;
+    int4 w4;
+    uint4 c8;
+    int4 c32[4];
+    uint4 h4;
+    int4 vc4, vn4;
+    int vin[4];
+};
+
+struct Out {
+    float4 s4;
+    int4 w4;
+    uint4 c8;
+    int4 c32[4];
+    uint4 h4;
+    int4 vc4, vn4;
+};
+
+// Screen position s = M p + m (DESIGN.md §4 contract; per-row bases then one fma per
+// coordinate per voxel), the exact pixel through the reciprocal, and the record gather.
+template <bool SHARD, bool PIN>
+__device__ __forceinline__ void stage_project(const IntegrateArgs& a, const UnitPos& up, int lane, Proj& P) {
     const VolGeom& g = a.g;
-    __shared__ float s_rcp[kRcpTable];
-    for (int i = threadIdx.x; i < kRcpTable; i += blockDim.x) s_rcp[i] = 1.0f / (float)(i + 1);
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const unsigned wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
-    const unsigned nwaves = gridDim.x * (blockDim.x >> 6);
-    const uint64_t plane = (uint64_t)g.dimy * (uint64_t)g.zs;
-    unsigned n_touch = 0, n_gate = 0;
-    unsigned n_live = 0, n_done = 0;
-    const uint64_t t_start = a.wave_stats ? __builtin_amdgcn_s_memrealtime() : 0;
-    // Work deal.  a.deal == 1: one wave per batch of 64 consecutive units, a grid of as
-    // many waves as batches (the dispatcher balances the uneven live counts).  a.deal == 0:
-    // persistent waves, wave w takes units w, w + nwaves, ...  Either way the cull flags
-    // are fetched 64 at a time (one per lane) and the live ones visited through the ballot.
-    const unsigned stride = a.deal ? 1u : nwaves;
-    for (unsigned first = a.deal ? wave * 64u : wave; first < ug.n; first += 64u * nwaves) {
-        const unsigned mine = first + (unsigned)lane * stride;
-        const bool lv = mine < ug.n && a.unit_flags[mine];
-        unsigned long long todo = __ballot(lv);
-        if (COUNT) n_live += (unsigned)__popcll(todo);
-        while (todo) {
-            const int kk = __ffsll((long long)todo) - 1;
-            todo &= todo - 1ull;
-            const unsigned u = first + (unsigned)kk * stride;
-            ++n_done;
-            const unsigned uxy = u % (ug.nux * ug.nuy);
-            const int x = (int)(uxy % ug.nux);
-            const int y = (int)(uxy / ug.nux) * UY + (lane >> 3);
-            const int l0 = (int)(u / (ug.nux * ug.nuy)) * UZ + (lane & 7) * 4;
-            const bool row_ok = (y < g.dimy) & (l0 < g.lz);
-            const float px = fmaf((float)x, g.voxel[0], g.start[0]);
-            const float py = fmaf((float)y, g.voxel[1], g.start[1]);
-            const uint64_t v = (uint64_t)x * plane + (uint64_t)y * (uint64_t)g.zs + (uint64_t)l0;
+    const int y = up.uy * UY + (lane >> 3);
+    const int l0 = up.uz * UZ + (lane & 7) * 4;
+    const bool row_ok = (y < g.dimy) & (l0 < g.lz);
+    const float px = fmaf((float)up.x, g.voxel[0], g.start[0]);
+    const float py = fmaf((float)y, g.voxel[1], g.start[1]);
+    const float bsx = fmaf(a.M[1], py, fmaf(a.M[0], px, a.m[0]));
+    const float bsy = fmaf(a.M[4], py, fmaf(a.M[3], px, a.m[1]));
+    const float bsz = fmaf(a.M[7], py, fmaf(a.M[6], px, a.m[2]));
+    const float bqz = PIN ? bsz : fmaf(a.E[9], py, fmaf(a.E[8], px, a.E[11]));
+    unsigned slow = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        int gz = l0 + k;
+        bool zok = row_ok & (l0 + k < g.lz);
+        if (SHARD) {
+            gz = local_to_global_z(g, l0 + k);
+            zok = zok & (gz < g.dimz);
+        }
+        const float pz = fmaf((float)gz, g.voxel[2], g.start[2]);
+        const float sx = fmaf(a.M[2], pz, bsx);
+        const float sy = fmaf(a.M[5], pz, bsy);
+        const float sz = fmaf(a.M[8], pz, bsz);
+        P.qz[k] = PIN ? sz : fmaf(a.E[10], pz, bqz);
+        // floor(sx/sz), floor(sy/sz) through the reciprocal: |qu - RN(sx/sz)| <= 2^-22 |qu|,
+        // so for |qu| < B (host: B = 2^ceil(log2(max(W, H) + 2))) a fraction farther than
+        // B 2^-21 from 0 and 1 floors like the IEEE quotient; |qu| >= B is off-image either
+        // way; NaN/Inf and near-integers fail the window and are redone exactly below.
+        const float r = __builtin_amdgcn_rcpf(sz);
+        const float qu = sx * r, qv = sy * r;
+        const float eu = __builtin_amdgcn_fractf(qu) - 0.5f, ev = __builtin_amdgcn_fractf(qv) - 0.5f;
+        const bool fast = (fabsf(eu) < a.ftol) & (fabsf(ev) < a.ftol);
+        const int iu = (int)floorf(qu), iv = (int)floorf(qv);
+        slow |= ((zok & !fast) ? 1u : 0u) << k;
+        const bool in = zok & fast & ((unsigned)iu < (unsigned)a.width) & ((unsigned)iv < (unsigned)a.height);
+        P.img[k] = in ? (int)__umul24((unsigned)iv, (unsigned)a.width) + iu : -1;
+    }
+    if (slow) {  // rare: exact IEEE quotients (the screen position is recomputed)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (!(slow & (1u << k))) continue;
+            const int gz = SHARD ? local_to_global_z(g, l0 + k) : l0 + k;
+            const float pz = fmaf((float)gz, g.voxel[2], g.start[2]);
+            const float sx = fmaf(a.M[2], pz, bsx), sy = fmaf(a.M[5], pz, bsy), sz = fmaf(a.M[8], pz, bsz);
+            const int ix = f2i_rd(sx / sz), iy = f2i_rd(sy / sz);
+            const bool in = ix >= 0 && ix < a.width && iy >= 0 && iy < a.height;
+            P.img[k] = in ? iy * a.width + ix : -1;
+        }
+    }
+    // unconditional gathers (off-image lanes read pixel 0 and ignore it)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) P.rec[k] = a.pyr.px[max(P.img[k], 0)];
+}
 
-            // ---- project the lane's 4 voxels (tsdf.cu:30-44)
-            int img[4], bix[4];
-            float qz[4];
-            unsigned slow = 0;
-            float sxv[4], syv[4], szv[4];
+template <bool SEM, bool GATE, bool VOTE, bool COUNT>
+__device__ __forceinline__ void stage_classify(const IntegrateArgs& a, const Proj& P, Cls& C, bool count,
+                                               unsigned& n_touch, unsigned& n_gate) {
+    const VolGeom& g = a.g;
+    unsigned tmask = 0, dslow = 0;
+    float dm[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float d = P.img[k] >= 0 ? __uint_as_float(P.rec[k].x) : 0.0f;
+        dm[k] = d;
+        const float diff = d - P.qz[k];
+        const bool t = (d != 0.0f) & (diff > -g.mu);
+        const float dc = fminf(diff, g.mu);
+        C.fv[k] = div_by_rcp(dc, g.mu, a.rmu);
+        dslow |= ((t & !(fabsf(dc) >= 0x1p-60f)) ? 1u : 0u) << k;
+        tmask |= (t ? 1u : 0u) << k;
+        C.pix[k] = P.rec[k].y;
+        if (VOTE) C.img[k] = P.img[k];
+    }
+    if (dslow || !a.fastdiv) {  // rare: tiny differences, or mu outside the reciprocal range
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float dc = fminf(dm[k] - P.qz[k], g.mu);
+            if (!a.fastdiv || (dslow & (1u << k))) C.fv[k] = dc == 0.0f ? dc : dc / g.mu;
+        }
+    }
+    unsigned gmask = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        gmask |= (((((tmask >> k) & 1u) != 0u) & (!GATE || C.fv[k] < a.gate)) ? 1u : 0u) << k;
+    if (COUNT && count) {
+        n_touch += __popc(tmask);
+        n_gate += __popc(gmask);
+    }
+    if (a.debug == 3) tmask = gmask = 0;  // timing probe: classification only, no state traffic
+    if (a.debug == 4) gmask = 0;          // timing probe: no colour/histogram traffic
+    C.tmask = tmask;
+    C.gmask = gmask;
+    // histogram mode of the lane: the label of its first gated voxel, shared by all of them?
+    unsigned lab = 0xFFu, same = 1u;
+#pragma unroll
+    for (int k = 3; k >= 0; --k) lab = ((gmask >> k) & 1u) ? (C.pix[k] >> 24) : lab;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) same &= (((gmask >> k) & 1u) == 0u) | ((C.pix[k] >> 24) == lab);
+    C.hlab = lab;
+    C.hmode = (!SEM || !gmask || a.debug == 6) ? 0u : ((same && lab < (unsigned)kMaxObjects) ? 1u : 2u);
+}
+
+// Unconditional loads: a lane with nothing to load reads the dummy line (one 16-B vector
+// shared by all such lanes), so the issue count is the same on every path.
+template <bool SEM, bool CI32, bool VOTE>
+__device__ __forceinline__ void stage_load(const IntegrateArgs& a, const UnitPos& up, unsigned loff, const Cls& C,
+                                           Ld& L) {
+    const VolGeom& g = a.g;
+    const uint64_t v = unit_base(g, up) + loff;
+    const uint4* dummy = reinterpret_cast<const uint4*>(a.rcp_table);
+    const bool t = C.tmask != 0u, gt = C.gmask != 0u;
+    L.s4 = t ? *reinterpret_cast<const float4*>(a.b.sdf + v) : *reinterpret_cast<const float4*>(dummy);
+    L.w4 = t ? *reinterpret_cast<const int4*>(a.b.wt + v) : *reinterpret_cast<const int4*>(dummy);
+    if (CI32) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            L.c32[k] = *reinterpret_cast<const int4*>(gt ? reinterpret_cast<const uint4*>(a.b.color) + v + k : dummy);
+    } else {
+        L.c8 = *(gt ? reinterpret_cast<const uint4*>(reinterpret_cast<const uint32_t*>(a.b.color) + v) : dummy);
+    }
+    if (SEM)
+        L.h4 = *(C.hmode == 1u ? reinterpret_cast<const uint4*>(a.b.hist + (uint64_t)C.hlab * g.nvox + v) : dummy);
+    if (VOTE) {
+        L.vc4 = *(t ? reinterpret_cast<const int4*>(a.b.cls + v) : reinterpret_cast<const int4*>(dummy));
+        L.vn4 = *(t ? reinterpret_cast<const int4*>(a.b.cls_cnt + v) : reinterpret_cast<const int4*>(dummy));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) L.vin[k] = a.cls[max(C.img[k], 0)];
+    }
+}
+
+template <bool SEM, bool GATE, bool CI32, bool VOTE>
+__device__ __forceinline__ void stage_compute(const IntegrateArgs& a, const float* __restrict__ s_rcp, const Cls& C,
+                                              const Ld& L, Out& O) {
+    const unsigned tmask = C.tmask, gmask = C.gmask;
+    // ---- running mean (tsdf.cu:56, 68) through RN(1/(w+1)) from the LDS table
+    const float so[4] = {L.s4.x, L.s4.y, L.s4.z, L.s4.w};
+    const int wo[4] = {L.w4.x, L.w4.y, L.w4.z, L.w4.w};
+    float sn[4];
+    int wn[4];
+    unsigned uslow = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const bool t = (tmask >> k) & 1u;
+        const float num = fmaf(so[k], (float)wo[k], C.fv[k]);
+        const float rw = s_rcp[min((unsigned)wo[k], (unsigned)kRcpTable - 1u)];
+        const float upd = div_by_rcp(num, (float)wo[k] + 1.0f, rw);
+        uslow |= ((t & !(((unsigned)wo[k] < (unsigned)kRcpTable) & (fabsf(num) >= 0x1p-60f))) ? 1u : 0u) << k;
+        sn[k] = t ? upd : so[k];
+        wn[k] = wo[k] + (t ? 1 : 0);
+    }
+    if (uslow || !a.fastdiv) {  // rare: weights past the table, tiny numerators
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (!((tmask >> k) & 1u) || (a.fastdiv && !(uslow & (1u << k)))) continue;
+            sn[k] = fmaf(so[k], (float)wo[k], C.fv[k]) / (float)(wo[k] + 1);
+        }
+    }
+    O.s4 = make_float4(sn[0], sn[1], sn[2], sn[3]);
+    O.w4 = make_int4(wn[0], wn[1], wn[2], wn[3]);
+    if (gmask) {  // tsdf.cu:57-62
+        if (CI32) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                int gz = l0 + k;
-                bool zok = row_ok & (l0 + k < g.lz);
-                if (SHARD) {
-                    gz = local_to_global_z(g, l0 + k);
-                    zok = zok & (gz < g.dimz);
-                }
-                const float pz = fmaf((float)gz, g.voxel[2], g.start[2]);
-                const float qx = dot3(a.E[0], a.E[1], a.E[2], px, py, pz) + a.E[3];
-                const float qy = dot3(a.E[4], a.E[5], a.E[6], px, py, pz) + a.E[7];
-                qz[k] = dot3(a.E[8], a.E[9], a.E[10], px, py, pz) + a.E[11];
-                float sx, sy, sz;
-                if (PIN) {
-                    sx = fmaf(a.K[2], qz[k], a.K[0] * qx);
-                    sy = fmaf(a.K[5], qz[k], a.K[4] * qy);
-                    sz = qz[k];
-                } else {
-                    sx = dot3(a.K[0], a.K[1], a.K[2], qx, qy, qz[k]);
-                    sy = dot3(a.K[3], a.K[4], a.K[5], qx, qy, qz[k]);
-                    sz = dot3(a.K[6], a.K[7], a.K[8], qx, qy, qz[k]);
-                }
-                // floor(sx/sz), floor(sy/sz) through the reciprocal.  |qu - RN(sx/sz)| <=
-                // 2^-22 |qu| (v_rcp_f32 is within 1 ulp, plus the rounding of the product), so
-                // when qu - tol and qu + tol (tol = 2^-21 |qu|) floor to the same integer, so
-                // does the IEEE quotient.  NaN/Inf and near-integer quotients fail the test and
-                // are redone exactly below; a quotient that is huge but "fast" is off-image
-                // either way.  Bitwise &, not &&: no per-voxel branches.
-                const float r = __builtin_amdgcn_rcpf(sz);
-                const float qu = sx * r, qv = sy * r;
-                const float tu = fabsf(qu) * 0x1p-21f, tv = fabsf(qv) * 0x1p-21f;
-                const float fu = floorf(qu - tu), fvv = floorf(qv - tv);
-                const bool fast = (fu == floorf(qu + tu)) & (fvv == floorf(qv + tv));
-                const bool in = zok & (fu >= 0.0f) & (fu < (float)a.width) & (fvv >= 0.0f) & (fvv < (float)a.height);
-                img[k] = in ? (int)fvv * a.width + (int)fu : -1;
-                bix[k] = in ? pix_block_index((int)fu, (int)fvv, a.pyr.wb) : 0;
-                slow |= ((zok & !fast) ? 1u : 0u) << k;
-                sxv[k] = sx; syv[k] = sy; szv[k] = sz;
+                const bool gk = (gmask >> k) & 1u;
+                const int wi = wo[k];
+                const int r0 = C.pix[k] & 0xFF, r1 = (C.pix[k] >> 8) & 0xFF, r2 = (C.pix[k] >> 16) & 0xFF;
+                int4 n = L.c32[k];
+                n.x = avg_div(n.x * wi + r0, wi + 1);
+                n.y = avg_div(n.y * wi + r1, wi + 1);
+                n.z = avg_div(n.z * wi + r2, wi + 1);
+                O.c32[k] = gk ? n : L.c32[k];
             }
-            if (slow) {  // rare: exact IEEE quotients
+        } else {
+            const unsigned co[4] = {L.c8.x, L.c8.y, L.c8.z, L.c8.w};
+            unsigned cw[4];
+            unsigned cslow = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const bool gk = (gmask >> k) & 1u;
+                const unsigned wi = (unsigned)wo[k], o = co[k], px = C.pix[k];
+                const float rw = s_rcp[min(wi, (unsigned)kRcpTable - 1u)];
+                const unsigned n0 = avg_u8(o & 0xFFu, px & 0xFFu, wi, rw);
+                const unsigned n1 = avg_u8((o >> 8) & 0xFFu, (px >> 8) & 0xFFu, wi, rw);
+                const unsigned n2 = avg_u8((o >> 16) & 0xFFu, (px >> 16) & 0xFFu, wi, rw);
+                cw[k] = gk ? (n0 | (n1 << 8) | (n2 << 16)) : o;
+                cslow |= ((gk & (wi >= (unsigned)kRcpTable)) ? 1u : 0u) << k;
+            }
+            if (cslow) {  // rare: weights past the reciprocal table, exact integer quotient
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    if (!(slow & (1u << k))) continue;
-                    const int ix = f2i_rd(sxv[k] / szv[k]), iy = f2i_rd(syv[k] / szv[k]);
-                    const bool in = ix >= 0 && ix < a.width && iy >= 0 && iy < a.height;
-                    img[k] = in ? iy * a.width + ix : -1;
-                    bix[k] = in ? pix_block_index(ix, iy, a.pyr.wb) : 0;
+                    if (!(cslow & (1u << k))) continue;
+                    const unsigned wi = (unsigned)wo[k], o = co[k], px = C.pix[k];
+                    const unsigned n0 = ((o & 0xFFu) * wi + (px & 0xFFu)) / (wi + 1u);
+                    const unsigned n1 = (((o >> 8) & 0xFFu) * wi + ((px >> 8) & 0xFFu)) / (wi + 1u);
+                    const unsigned n2 = (((o >> 16) & 0xFFu) * wi + ((px >> 16) & 0xFFu)) / (wi + 1u);
+                    cw[k] = (n0 & 0xFFu) | ((n1 & 0xFFu) << 8) | ((n2 & 0xFFu) << 16);
                 }
             }
-            // ---- depth gather (one dword per voxel from the metres image)
-            float dm[4];
+            O.c8 = make_uint4(cw[0], cw[1], cw[2], cw[3]);
+        }
+        if (SEM) {  // tsdf.cu:61: +1 in the bin of the pixel's label
+            O.h4 = make_uint4(L.h4.x + (gmask & 1u), L.h4.y + ((gmask >> 1) & 1u), L.h4.z + ((gmask >> 2) & 1u),
+                              L.h4.w + ((gmask >> 3) & 1u));
+        }
+    }
+    if (VOTE) {  // TSDF_Python/tsdf.cu:48-57
+        int vc[4] = {L.vc4.x, L.vc4.y, L.vc4.z, L.vc4.w}, vn[4] = {L.vn4.x, L.vn4.y, L.vn4.z, L.vn4.w};
 #pragma unroll
-            for (int k = 0; k < 4; ++k) dm[k] = a.debug == 9 ? 2.0f : a.pyr.metres[bix[k]];  // 9: no gather probe
-            // ---- classify (tsdf.cu:48-52), branch-free
-            float fv[4];
-            unsigned tmask = 0, gmask = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float d = img[k] >= 0 ? dm[k] : 0.0f;
-                float diff = d - qz[k];
-                const bool t = (d != 0.0f) & (diff > -g.mu);
-                diff = (diff > g.mu) ? g.mu : diff;
-                if (a.fastdiv) {
-                    fv[k] = div_by_rcp(diff, g.mu, a.rmu);
-                    if (!(fabsf(diff) >= 0x1p-60f)) fv[k] = diff == 0.0f ? diff : diff / g.mu;
-                } else {
-                    fv[k] = diff / g.mu;
-                }
-                tmask |= (t ? 1u : 0u) << k;
-                gmask |= ((t & (!GATE || fv[k] < a.gate)) ? 1u : 0u) << k;
-            }
-            if (COUNT) {
-                n_touch += __popc(tmask);
-                n_gate += __popc(gmask);
-            }
-            if (a.debug == 3) {  // timing probe: classification only, no state traffic
-                asm volatile("" ::"v"(fv[0] + fv[1] + fv[2] + fv[3]), "v"(tmask), "v"(gmask));
-                continue;
-            }
-            if (a.debug == 4) gmask = 0;  // timing probe: no colour/histogram traffic
-            if (!tmask) continue;
-            // ---- state loads: one 16-B vector per array for the 4 voxels
-            const float4 s4 = *reinterpret_cast<const float4*>(a.b.sdf + v);
-            const int4 w4 = *reinterpret_cast<const int4*>(a.b.wt + v);
-            int4 vc4, vn4;
-            int vin[4];
-            if (VOTE) {
-                vc4 = *reinterpret_cast<const int4*>(a.b.cls + v);
-                vn4 = *reinterpret_cast<const int4*>(a.b.cls_cnt + v);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) vin[k] = a.cls[img[k] >= 0 ? img[k] : 0];
-            }
-            uint4 c8 = make_uint4(0, 0, 0, 0);
-            int4 c32[4];
-            unsigned pix[4] = {0, 0, 0, 0};
-            if (gmask) {
-                if (CI32) {
-                    const int4* c = reinterpret_cast<const int4*>(a.b.color) + v;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) c32[k] = c[k];
-                } else {
-                    c8 = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint32_t*>(a.b.color) + v);
-                }
-#pragma unroll
-                for (int k = 0; k < 4; ++k) pix[k] = a.pyr.rgbl[bix[k]];
-            }
-            // ---- update (tsdf.cu:56, 68), branch-free selects
-            const float so[4] = {s4.x, s4.y, s4.z, s4.w};
-            const int wo[4] = {w4.x, w4.y, w4.z, w4.w};
-            float sn[4];
-            int wn[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const bool t = (tmask >> k) & 1u;
-                const float num = fmaf(so[k], (float)wo[k], fv[k]);
-                float upd;
-                if (a.fastdiv && (unsigned)wo[k] < (unsigned)kRcpTable) {
-                    upd = div_by_rcp(num, (float)(wo[k] + 1), s_rcp[wo[k]]);
-                    if (!(fabsf(num) >= 0x1p-60f)) upd = num == 0.0f ? num : num / (float)(wo[k] + 1);
-                } else {
-                    upd = num / (float)(wo[k] + 1);
-                }
-                sn[k] = t ? upd : so[k];
-                wn[k] = wo[k] + (t ? 1 : 0);
-            }
-            if (a.debug == 10) {  // timing probe: loads but no sdf/weight stores
-                asm volatile("" ::"v"(sn[0] + sn[1] + sn[2] + sn[3]), "v"(wn[0] + wn[1] + wn[2] + wn[3]));
+        for (int k = 0; k < 4; ++k) {
+            if (!((tmask >> k) & 1u)) continue;
+            if (vn[k] == 0) {
+                vc[k] = L.vin[k];
+                vn[k] = 1;
+            } else if (vc[k] == L.vin[k]) {
+                vn[k] += 1;
             } else {
-                *reinterpret_cast<float4*>(a.b.sdf + v) = make_float4(sn[0], sn[1], sn[2], sn[3]);
-                *reinterpret_cast<int4*>(a.b.wt + v) = make_int4(wn[0], wn[1], wn[2], wn[3]);
+                vn[k] -= 1;
             }
-            if (gmask) {  // tsdf.cu:57-62
-                if (CI32) {
-                    int4* c = reinterpret_cast<int4*>(a.b.color) + v;
+        }
+        O.vc4 = make_int4(vc[0], vc[1], vc[2], vc[3]);
+        O.vn4 = make_int4(vn[0], vn[1], vn[2], vn[3]);
+    }
+}
+
+template <bool SEM, bool CI32, bool VOTE>
+__device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPos& up, unsigned loff,
+                                            const StoreMeta& M, const Out& O) {
+    const VolGeom& g = a.g;
+    const unsigned tmask = M.meta & 15u, gmask = (M.meta >> 4) & 15u, hmode = (M.meta >> 8) & 3u,
+                   hlab = M.meta >> 16;
+    if (!tmask) return;
+    const uint64_t v = unit_base(g, up) + loff;
+    if (a.debug != 10) {  // 10: timing probe, loads but no sdf/weight stores
+        *reinterpret_cast<float4*>(a.b.sdf + v) = O.s4;
+        *reinterpret_cast<int4*>(a.b.wt + v) = O.w4;
+    }
+    if (gmask) {
+        if (CI32) {
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const bool gk = (gmask >> k) & 1u;
-                        const int wi = wo[k];
-                        const int r0 = pix[k] & 0xFF, r1 = (pix[k] >> 8) & 0xFF, r2 = (pix[k] >> 16) & 0xFF;
-                        int4 n = c32[k];
-                        n.x = avg_div(n.x * wi + r0, wi + 1);
-                        n.y = avg_div(n.y * wi + r1, wi + 1);
-                        n.z = avg_div(n.z * wi + r2, wi + 1);
-                        c32[k] = gk ? n : c32[k];
-                    }
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) c[k] = c32[k];
-                } else {
-                    unsigned cw[4] = {c8.x, c8.y, c8.z, c8.w};
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const bool gk = (gmask >> k) & 1u;
-                        const int wi = wo[k];
-                        const unsigned o = cw[k];
-                        const unsigned n0 = (unsigned)avg_div((int)(o & 0xFF) * wi + (int)(pix[k] & 0xFF), wi + 1);
-                        const unsigned n1 =
-                            (unsigned)avg_div((int)((o >> 8) & 0xFF) * wi + (int)((pix[k] >> 8) & 0xFF), wi + 1);
-                        const unsigned n2 =
-                            (unsigned)avg_div((int)((o >> 16) & 0xFF) * wi + (int)((pix[k] >> 16) & 0xFF), wi + 1);
-                        const unsigned nw = (n0 & 0xFF) | ((n1 & 0xFF) << 8) | ((n2 & 0xFF) << 16);
-                        cw[k] = gk ? nw : o;
-                    }
-                    *reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(a.b.color) + v) =
-                        make_uint4(cw[0], cw[1], cw[2], cw[3]);
-                }
-                if (SEM) {
-                    // tsdf.cu:61.  One lane owns the voxel, so a no-return atomic add is the
-                    // plain increment without a dependent load round trip.
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const unsigned lab = pix[k] >> 24;
-                        if (((gmask >> k) & 1u) && lab < (unsigned)kMaxObjects && a.debug != 6)
-                            atomicAdd(a.b.hist + (uint64_t)lab * g.nvox + v + k, 1u);
-                    }
-                    unsigned bad = 0;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) bad |= ((gmask >> k) & 1u) && (pix[k] >> 24) >= (unsigned)kMaxObjects;
-                    if (bad) atomicOr(reinterpret_cast<unsigned*>(a.counters + 2), 1u);
-                }
-            }
-            if (VOTE) {  // TSDF_Python/tsdf.cu:48-57
-                int vc[4] = {vc4.x, vc4.y, vc4.z, vc4.w}, vn[4] = {vn4.x, vn4.y, vn4.z, vn4.w};
+            for (int k = 0; k < 4; ++k) reinterpret_cast<int4*>(a.b.color)[v + k] = O.c32[k];
+        } else {
+            *reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(a.b.color) + v) = O.c8;
+        }
+        if (SEM) {
+            if (hmode == 1u) *reinterpret_cast<uint4*>(a.b.hist + (uint64_t)hlab * g.nvox + v) = O.h4;
+            if (hmode == 2u) {  // rare: labels differ inside the lane, or a label >= 32
+                unsigned bad = 0;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    if (!((tmask >> k) & 1u)) continue;
-                    if (vn[k] == 0) {
-                        vc[k] = vin[k];
-                        vn[k] = 1;
-                    } else if (vc[k] == vin[k]) {
-                        vn[k] += 1;
-                    } else {
-                        vn[k] -= 1;
-                    }
+                    const unsigned lab = (M.labs >> (8 * k)) & 0xFFu;
+                    const bool gk = (gmask >> k) & 1u;
+                    if (gk && lab < (unsigned)kMaxObjects) atomicAdd(a.b.hist + (uint64_t)lab * g.nvox + v + k, 1u);
+                    bad |= (gk && lab >= (unsigned)kMaxObjects) ? 1u : 0u;
                 }
-                *reinterpret_cast<int4*>(a.b.cls + v) = make_int4(vc[0], vc[1], vc[2], vc[3]);
-                *reinterpret_cast<int4*>(a.b.cls_cnt + v) = make_int4(vn[0], vn[1], vn[2], vn[3]);
+                if (bad) atomicOr(reinterpret_cast<unsigned*>(a.counters + 2), 1u);
             }
         }
     }
-    if (a.wave_stats && lane == 0) {  // instrumentation: per-wave start/end (100 MHz ticks), units
-        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
-        unsigned hw_id;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_id));
-        unsigned xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        a.wave_stats[wave * 4 + 0] = t_start;
-        a.wave_stats[wave * 4 + 1] = t_end;
-        a.wave_stats[wave * 4 + 2] = n_done;
-        a.wave_stats[wave * 4 + 3] = ((uint64_t)xcc << 32) | hw_id;
+    if (VOTE) {
+        *reinterpret_cast<int4*>(a.b.cls + v) = O.vc4;
+        *reinterpret_cast<int4*>(a.b.cls_cnt + v) = O.vn4;
+    }
+}
+
+// Persistent wavefronts over the live-unit list: wave w takes entries w, w + nwaves, ...
+// (every wave gets the same number of units +-1), read with scalar loads one unit ahead.
+#ifndef SEMTSDF_INTEGRATE_WPE
+#define SEMTSDF_INTEGRATE_WPE 5  // waves per SIMD the register allocation of k_integrate targets
+#endif
+template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT, bool SHARD, bool PIN>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_INTEGRATE_WPE))) void k_integrate(
+    IntegrateArgs a, UnitGrid ug,
+                                                                                          unsigned seg_cap) {
+    __shared__ float s_rcp[kRcpTable];
+    for (int i = (int)threadIdx.x; i < kRcpTable; i += (int)blockDim.x) s_rcp[i] = a.rcp_table[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const unsigned loff = (unsigned)(lane >> 3) * (unsigned)a.g.zs + (unsigned)(lane & 7) * 4u;
+    const unsigned wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+    const unsigned nwaves = gridDim.x * (blockDim.x >> 6);
+    unsigned cnt[kListSegs];
+    unsigned total = 0;
+    const __attribute__((address_space(4))) unsigned* lc = (const __attribute__((address_space(4))) unsigned*)a.list_count;
+#pragma unroll
+    for (int c = 0; c < kListSegs; ++c) {
+        cnt[c] = lc[c];
+        total += cnt[c];
+    }
+    unsigned n_touch = 0, n_gate = 0;
+    auto entry = [&](unsigned i) -> unsigned {  // i < total
+        unsigned off = i, seg = 0;
+#pragma unroll
+        for (int c = 0; c < kListSegs; ++c)
+            if (seg == (unsigned)c && off >= cnt[c]) {
+                off -= cnt[c];
+                seg = (unsigned)c + 1u;
+            }
+        // constant address space: the list is read-only here, so this is a scalar load
+        // (s_load, lgkmcnt) and never waits behind the wave's vector memory operations
+        const __attribute__((address_space(4))) unsigned* list =
+            (const __attribute__((address_space(4))) unsigned*)a.unit_list;
+        return list[seg * seg_cap + off];
+    };
+    unsigned i = wave;
+    if (i < total) {
+        UnitPos cur = unit_pos(ug, entry(i));
+        unsigned un = (i + nwaves < total) ? entry(i + nwaves) : 0u;
+        Proj P;
+        Cls C;
+        Ld L;
+        Out O;
+        stage_project<SHARD, PIN>(a, cur, lane, P);
+        stage_classify<SEM, GATE, VOTE, COUNT>(a, P, C, true, n_touch, n_gate);
+        stage_load<SEM, CI32, VOTE>(a, cur, loff, C, L);
+        while (true) {
+            const bool has = i + nwaves < total;
+            // the last iteration projects a copy of the current unit, so the memory
+            // operations issued per iteration do not depend on the branch
+            const UnitPos nxt = has ? unit_pos(ug, un) : cur;
+            un = (i + 2u * nwaves < total) ? entry(i + 2u * nwaves) : 0u;
+            stage_project<SHARD, PIN>(a, nxt, lane, P);
+            if (C.tmask) stage_compute<SEM, GATE, CI32, VOTE>(a, s_rcp, C, L, O);  // wave-level skip
+            const StoreMeta Mc = store_meta(C);
+            stage_classify<SEM, GATE, VOTE, COUNT>(a, P, C, has, n_touch, n_gate);
+            stage_store<SEM, CI32, VOTE>(a, cur, loff, Mc, O);
+            if (!has) break;
+            stage_load<SEM, CI32, VOTE>(a, nxt, loff, C, L);
+            cur = nxt;
+            i += nwaves;
+        }
     }
     if (COUNT) {
         unsigned long long t = n_touch, gg = n_gate;
@@ -700,8 +902,8 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateArgs a, UnitGrid ug)
         if (lane == 0) {
             if (t) atomicAdd(a.counters + 0, t);
             if (gg) atomicAdd(a.counters + 1, gg);
-            if (n_live) atomicAdd(a.counters + 3, (unsigned long long)n_live);
         }
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.counters + 3, (unsigned long long)total);
     }
 }
 
@@ -725,15 +927,19 @@ static unsigned resident_grid(K kernel) {
 
 template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT, bool SHARD, bool PIN>
 static hipError_t launch_integrate_k(const IntegrateArgs& a, hipStream_t s) {
-    if (unit_grid(a.g).n == 0) return hipSuccess;
-    // ROCm 7.2's occupancy query over-reports by one block per CU for SGPR-heavy 256-thread
-    // kernels (MI355X_MICROARCH.md): the persistent grid uses one block per CU less.
+    const UnitGrid ug = unit_grid(a.g);
+    if (ug.n == 0) return hipSuccess;
+    // persistent grid of the resident capacity; the waves share the list evenly, so a grid
+    // past residency (the occupancy query can over-report, MI355X_MICROARCH.md) only adds
+    // late waves with the same share
     static const unsigned grid0 = resident_grid(k_integrate<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>);
     const unsigned ncu = resident_grid_cus();
-    unsigned grid = a.deal ? (unsigned)((unit_grid(a.g).n + 255) / 256) : (grid0 > 2 * ncu ? grid0 - ncu : grid0);
-    if (!a.deal && a.debug >= 100) grid = grid0 * (unsigned)(a.debug - 100) / 8u;  // probe: fraction of residency
-    hipLaunchKernelGGL((k_integrate<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>), dim3(grid), dim3(256), 0, s, a,
-                       unit_grid(a.g));
+    unsigned grid = grid0;
+    if (a.debug >= 100) grid = grid0 * (unsigned)(a.debug - 100) / 8u;  // probe: fraction of residency
+    static const char* gpc = getenv("SEMTSDF_GRID_PER_CU");              // probe: blocks per CU
+    if (gpc && atoi(gpc) > 0) grid = ncu * (unsigned)atoi(gpc);
+    hipLaunchKernelGGL((k_integrate<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>), dim3(grid), dim3(256), 0, s, a, ug,
+                       list_seg_cap(ug));
     return hipGetLastError();
 }
 
