@@ -87,7 +87,7 @@ struct semtsdf_vol {
     unsigned long long* counters_d = nullptr;
     uint8_t* unit_flags_d = nullptr;
     unsigned* unit_list_d = nullptr;  // live units of the frame (cull pass)
-    unsigned* list_count_d = nullptr; // [kListSegs]
+    unsigned* list_count_d = nullptr; // [kListSegs * kListCountStride]
     float* rcp_table_d = nullptr;    // RN(1/n), n = 1..kRcpTable
     AssocDecision* decision_h = nullptr;  // pinned
     // Z-sharded raycast protocol (allocated on first use)
@@ -565,7 +565,7 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     if ((rc = dev_alloc(v, (void**)&pyr.l1, (size_t)pyr.w1 * pyr.h1 * 2))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->unit_flags_d, unit_count(g)))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->unit_list_d, unit_list_capacity(g) * sizeof(unsigned)))) return bail(rc);
-    if ((rc = dev_alloc(v, (void**)&v->list_count_d, kListSegs * sizeof(unsigned)))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&v->list_count_d, kListSegs * kListCountStride * sizeof(unsigned)))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->rcp_table_d, kRcpTable * sizeof(float)))) return bail(rc);
     {
         float t[kRcpTable];

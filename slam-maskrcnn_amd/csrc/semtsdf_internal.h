@@ -9,7 +9,8 @@ namespace semtsdf {
 
 constexpr int kMaxObjects = 32;
 constexpr int kRcpTable = 1024;  // RN(1/n) table of the running means (w + 1 <= kRcpTable)
-constexpr int kListSegs = 8;     // segments (and counters) of the live-unit list
+constexpr int kListSegs = 64;    // segments (and counters) of the live-unit list
+constexpr int kListCountStride = 64;  // counters 256 B apart (separate memory channels)
 
 // Geometry of the locally stored part of the volume.
 struct VolGeom {
@@ -75,7 +76,7 @@ struct IntegrateArgs {
     float rmu;                     // RN(1/mu), for the exact division by mu (k_integrate)
     int fastdiv;                   // mu in [2^-20, 2^20]: divisions by mu/(w+1) via RN reciprocals
     unsigned* unit_list;           // live units, kListSegs segments (k_cull_units)
-    unsigned* list_count;          // [kListSegs] entries per segment (zeroed by the frame prepass)
+    unsigned* list_count;          // [kListSegs * kListCountStride] entries per segment (zeroed by the frame prepass)
 };
 
 // Association accumulators (fixed point, scale 2^28, deterministic).

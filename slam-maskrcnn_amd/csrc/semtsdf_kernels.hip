@@ -209,7 +209,7 @@ __global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restric
     __shared__ unsigned s_m[32][8];
     const int tx = blockIdx.x, ty = blockIdx.y;
     const int t = threadIdx.x;
-    if (list_count && tx == 0 && ty == 0 && t < kListSegs) list_count[t] = 0u;  // this frame's live-unit list
+    if (list_count && tx == 0 && ty == 0 && t < kListSegs) list_count[t * kListCountStride] = 0u;  // this frame's list
     const int r = t >> 3;          // row in tile
     const int c4 = (t & 7) * 4;    // first column in tile
     const int yy = ty * 32 + r;
@@ -410,8 +410,9 @@ __host__ __device__ inline UnitGrid unit_grid(const VolGeom& g) {
 }
 
 // Live-unit list: kListSegs segments, segment c filled by the cull workgroups b with
-// b % kListSegs == c (one counter per segment keeps the same-address atomics per counter
-// to ~1/8 of the workgroups).  Capacity of a segment: all units of its workgroups.
+// b % kListSegs == c (one counter per segment, 256 B apart, keeps the same-address atomics
+// per counter to 1/64 of the workgroups).  Capacity of a segment: all units of its
+// workgroups.
 __host__ __device__ inline unsigned list_seg_cap(const UnitGrid& ug) {
     const unsigned groups = (ug.n + 255u) / 256u;
     return (groups + kListSegs - 1u) / kListSegs * 256u;
@@ -444,7 +445,7 @@ __global__ __launch_bounds__(256) void k_cull_units(IntegrateArgs a, UnitGrid ug
     const unsigned seg = blockIdx.x % (unsigned)kListSegs;
     if (threadIdx.x == 0) {
         const unsigned tot = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
-        s_base = tot ? atomicAdd(a.list_count + seg, tot) : 0u;
+        s_base = tot ? atomicAdd(a.list_count + seg * kListCountStride, tot) : 0u;
     }
     __syncthreads();
     if (live) {
@@ -842,23 +843,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_INT
     const unsigned loff = (unsigned)(lane >> 3) * (unsigned)a.g.zs + (unsigned)(lane & 7) * 4u;
     const unsigned wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     const unsigned nwaves = gridDim.x * (blockDim.x >> 6);
-    unsigned cnt[kListSegs];
-    unsigned total = 0;
-    const __attribute__((address_space(4))) unsigned* lc = (const __attribute__((address_space(4))) unsigned*)a.list_count;
+    // segment counts, one per lane; inclusive prefix over the lanes (kListSegs == 64)
+    static_assert(kListSegs == 64, "one list segment per lane");
+    const unsigned cnt_l = a.list_count[lane * kListCountStride];
+    unsigned incl = cnt_l;
 #pragma unroll
-    for (int c = 0; c < kListSegs; ++c) {
-        cnt[c] = lc[c];
-        total += cnt[c];
+    for (int off = 1; off < 64; off <<= 1) {
+        const unsigned o = (unsigned)__shfl_up((int)incl, off, 64);
+        if (lane >= off) incl += o;
     }
+    const unsigned total = __builtin_amdgcn_readfirstlane((unsigned)__shfl((int)incl, 63, 64));
     unsigned n_touch = 0, n_gate = 0;
-    auto entry = [&](unsigned i) -> unsigned {  // i < total
-        unsigned off = i, seg = 0;
-#pragma unroll
-        for (int c = 0; c < kListSegs; ++c)
-            if (seg == (unsigned)c && off >= cnt[c]) {
-                off -= cnt[c];
-                seg = (unsigned)c + 1u;
-            }
+    auto entry = [&](unsigned i) -> unsigned {  // i < total: segment = number of segments ending at or before i
+        const unsigned seg = (unsigned)__popcll(__ballot(incl <= i));
+        const unsigned before = seg ? __builtin_amdgcn_readfirstlane((unsigned)__shfl((int)incl, (int)seg - 1, 64)) : 0u;
+        const unsigned off = i - before;
         // constant address space: the list is read-only here, so this is a scalar load
         // (s_load, lgkmcnt) and never waits behind the wave's vector memory operations
         const __attribute__((address_space(4))) unsigned* list =
