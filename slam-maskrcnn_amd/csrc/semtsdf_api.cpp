@@ -142,6 +142,8 @@ int check_params(const semtsdf_params* p) {
         if (!(p->voxel[i] > 0.0f) || !std::isfinite(p->voxel[i]))
             return fail(SEMTSDF_ERR_INVALID, "voxel[%d]=%g must be > 0 (place the volume first)", i, p->voxel[i]);
     }
+    if ((int64_t)p->dim[1] * (p->dim[2] + 4) >= (int64_t)1 << 30)  // 32-bit lane offsets of k_integrate
+        return fail(SEMTSDF_ERR_INVALID, "dim[1] * dim[2] = %lld too large (< 2^30)", (long long)p->dim[1] * p->dim[2]);
     if (!(p->mu > 0.0f)) return fail(SEMTSDF_ERR_INVALID, "mu=%g must be > 0", p->mu);
     if (p->width <= 0 || p->height <= 0 || (int64_t)p->width * p->height > (1 << 28))
         return fail(SEMTSDF_ERR_INVALID, "bad frame size %dx%d", p->width, p->height);
@@ -560,7 +562,8 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     DepthPyramid& pyr = v->pyr;
     pyr.w0 = (p->width + 7) / 8; pyr.h0 = (p->height + 7) / 8;
     pyr.w1 = (p->width + 31) / 32; pyr.h1 = (p->height + 31) / 32;
-    if ((rc = dev_alloc(v, (void**)&pyr.px, px * 8))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&pyr.px, (px + 1) * 8))) return bail(rc);
+    if (hipMemset(pyr.px, 0, (px + 1) * 8) != hipSuccess) return bail(fail(SEMTSDF_ERR_HIP, "memset failed"));
     if ((rc = dev_alloc(v, (void**)&pyr.l0, (size_t)pyr.w1 * 4 * pyr.h1 * 4 * 2))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&pyr.l1, (size_t)pyr.w1 * pyr.h1 * 2))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->unit_flags_d, unit_count(g)))) return bail(rc);

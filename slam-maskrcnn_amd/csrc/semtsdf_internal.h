@@ -44,7 +44,8 @@ struct VolBufs {
 // W x H), and the max raw depth over 8- and 32-pixel tiles used by the unit culler.
 struct DepthPyramid {
     uint2* px;      // [H][W] pixel records {bits of depth / depth_scale (IEEE, tsdf.cu:49),
-                    //                       r | g << 8 | b << 16 | label << 24}: one 8-B gather per voxel
+                    //                       r | g << 8 | b << 16 | label << 24}: one 8-B gather per voxel;
+                    // record W*H is zero (the target of off-image voxels)
     uint16_t* l0;  // [ceil(H/8)][ceil(W/8)]
     uint16_t* l1;  // [ceil(H/32)][ceil(W/32)]
     int w0, h0, w1, h1;

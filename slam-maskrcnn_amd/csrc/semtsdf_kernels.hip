@@ -286,13 +286,25 @@ hipError_t launch_depth_pyramid(const uint16_t* depth, const uint8_t* rgb, const
 // integrate
 // ------------------------------------------------------------------------------------
 // ---- work decomposition ------------------------------------------------------------
-// Cull unit = UX(x) x UY(y) x UZ(z) voxels, tested once per frame by one lane of the cull
-// pass against the frustum and the depth pyramid (a byte flag per unit, no atomics).
-// Integrate work item = one unit, handled by one wavefront: lane = (zq, y) = (lane & 7,
-// lane >> 3) owns planes 4zq..4zq+3 of row y for the UX x-planes, so every state access is
-// one 16-byte vector per lane.  Items are dealt round-robin to persistent waves, so live
-// items spread evenly over the chip and waves never synchronise with each other.
-constexpr int UX = 1, UY = 8, UZ = 32;
+// Cull unit = UX(x) x UY(y) x UZ(z) = 256 voxels, tested once per frame by one lane of the
+// cull pass against the frustum and the depth pyramid.  Integrate work item = one unit,
+// handled by one wavefront: lane = (zq, y, x) owns planes 4zq..4zq+3 of row (x, y), so
+// every state access is one 16-byte vector per lane and a z-row of the unit is UZ*4 bytes
+// contiguous.  1 x 8 x 32 makes every z-row one whole 128-B line: tighter shapes visit
+// fewer voxels (2 x 8 x 16: 75 % against 63 % of the visited voxels are touched on the
+// synthetic stream) but split lines between units and measured 9 % (2x8x16), 15 %
+// (1x16x16) and 64 % (4x8x8) slower on MI355X.
+#ifndef SEMTSDF_UNIT_X
+#define SEMTSDF_UNIT_X 1
+#define SEMTSDF_UNIT_Y 8
+#define SEMTSDF_UNIT_Z 32
+#endif
+constexpr int UX = SEMTSDF_UNIT_X, UY = SEMTSDF_UNIT_Y, UZ = SEMTSDF_UNIT_Z;
+constexpr int LZQ = UZ / 4;  // lanes along z
+static_assert(UX * UY * UZ == 256 && UZ % 4 == 0, "a unit is 64 lanes x 4 z-voxels");
+__device__ __forceinline__ int lane_zq(int lane) { return lane % LZQ; }
+__device__ __forceinline__ int lane_y(int lane) { return (lane / LZQ) % UY; }
+__device__ __forceinline__ int lane_x(int lane) { return lane / (LZQ * UY); }
 
 // floor(a / b) with the IEEE quotient, through v_rcp when the result is provably the same:
 // |a*rcp(b) - RN(a/b)| < |q| 2^-20, so a q farther than |q| 2^-19 from an integer floors the
@@ -430,12 +442,14 @@ __global__ __launch_bounds__(256) void k_cull_units(IntegrateArgs a, UnitGrid ug
         const int ux = (int)(u % ug.nux), uy = (int)((u / ug.nux) % ug.nuy), uz = (int)(u / (ug.nux * ug.nuy));
         live = a.cull ? !unit_cull(a, ux * UX, uy * UY, uz * UZ) : 1;
         a.unit_flags[u] = (uint8_t)live;
-        if (live && a.b.bdirty) {  // the bricks this unit overlaps may change (empty-space map)
-            static_assert(UX == 1 && UY == 8 && UZ == 32, "brick marking assumes 1x8x32 units");
+        if (live && a.b.bdirty) {  // the 8^3 bricks this unit overlaps may change (empty-space map)
             const VolGeom& g = a.g;
-            const unsigned base = ((unsigned)(ux >> 3) * (unsigned)g.nby + (unsigned)uy) * (unsigned)g.nbz;
-            for (int j = 0; j < 4; ++j)
-                if (uz * 4 + j < g.nbz) a.b.bdirty[base + (unsigned)uz * 4u + (unsigned)j] = 1;
+            const int bx1 = min(ux * UX + UX - 1, g.dimx - 1) >> 3, by1 = min(uy * UY + UY - 1, g.dimy - 1) >> 3;
+            const int bz1 = min(uz * UZ + UZ - 1, g.lz - 1) >> 3;
+            for (int bx = (ux * UX) >> 3; bx <= bx1; ++bx)
+                for (int by = (uy * UY) >> 3; by <= by1; ++by)
+                    for (int bz = (uz * UZ) >> 3; bz <= bz1; ++bz)
+                        a.b.bdirty[((unsigned)bx * (unsigned)g.nby + (unsigned)by) * (unsigned)g.nbz + (unsigned)bz] = 1;
         }
     }
     const int lane = (int)(threadIdx.x & 63u), wv = (int)(threadIdx.x >> 6);
@@ -475,9 +489,8 @@ __device__ __forceinline__ unsigned avg_u8(unsigned c, unsigned x, unsigned w, f
 }
 
 // ---- the integrate of one unit in stages ---------------------------------------------------
-// A unit (UX x UY x UZ voxels) is handled by one wavefront: lane = (zq, y) = (lane & 7,
-// lane >> 3) owns planes 4zq..4zq+3 of row y, so every state access is one 16-byte vector
-// per lane.  Stages:
+// A unit (UX x UY x UZ voxels) is handled by one wavefront: lane = (zq, y, x) owns planes
+// 4zq..4zq+3 of row (x, y), so every state access is one 16-byte vector per lane.  Stages:
 //   project  — screen position, exact pixel, gather of the pixel records (depth, rgb, label)
 //   classify — tsdf.cu:46-52 tests
 //   load     — state of the touched lanes (sdf, weight; colour and histogram words of the
@@ -508,14 +521,14 @@ __device__ __forceinline__ UnitPos unit_pos(const UnitGrid& ug, unsigned u) {
 }
 
 __device__ __forceinline__ uint64_t unit_base(const VolGeom& g, const UnitPos& up) {
-    return (uint64_t)up.x * ((uint64_t)g.dimy * (uint64_t)g.zs) + (uint64_t)(up.uy * UY) * (uint64_t)g.zs +
+    return (uint64_t)(up.x * UX) * ((uint64_t)g.dimy * (uint64_t)g.zs) + (uint64_t)(up.uy * UY) * (uint64_t)g.zs +
            (uint64_t)(up.uz * UZ);
 }
 
 struct Proj {
     float qz[4];
-    uint2 rec[4];  // gathered pixel record {metres bits, rgbl}, valid where img >= 0
-    int img[4];    // pixel index, -1 off-image (or an invalid plane)
+    uint2 rec[4];  // gathered pixel record {metres bits, rgbl}
+    int img[4];    // pixel index; W*H (the zero record) off-image or on an invalid plane
 };
 
 struct Cls {
@@ -564,10 +577,12 @@ struct Out {
 template <bool SHARD, bool PIN>
 __device__ __forceinline__ void stage_project(const IntegrateArgs& a, const UnitPos& up, int lane, Proj& P) {
     const VolGeom& g = a.g;
-    const int y = up.uy * UY + (lane >> 3);
-    const int l0 = up.uz * UZ + (lane & 7) * 4;
-    const bool row_ok = (y < g.dimy) & (l0 < g.lz);
-    const float px = fmaf((float)up.x, g.voxel[0], g.start[0]);
+    const int npx = a.width * a.height;
+    const int x = up.x * UX + lane_x(lane);
+    const int y = up.uy * UY + lane_y(lane);
+    const int l0 = up.uz * UZ + lane_zq(lane) * 4;
+    const bool row_ok = (x < g.dimx) & (y < g.dimy) & (l0 < g.lz);
+    const float px = fmaf((float)x, g.voxel[0], g.start[0]);
     const float py = fmaf((float)y, g.voxel[1], g.start[1]);
     const float bsx = fmaf(a.M[1], py, fmaf(a.M[0], px, a.m[0]));
     const float bsy = fmaf(a.M[4], py, fmaf(a.M[3], px, a.m[1]));
@@ -598,7 +613,7 @@ __device__ __forceinline__ void stage_project(const IntegrateArgs& a, const Unit
         const int iu = (int)floorf(qu), iv = (int)floorf(qv);
         slow |= ((zok & !fast) ? 1u : 0u) << k;
         const bool in = zok & fast & ((unsigned)iu < (unsigned)a.width) & ((unsigned)iv < (unsigned)a.height);
-        P.img[k] = in ? (int)__umul24((unsigned)iv, (unsigned)a.width) + iu : -1;
+        P.img[k] = in ? (int)__umul24((unsigned)iv, (unsigned)a.width) + iu : npx;
     }
     if (slow) {  // rare: exact IEEE quotients (the screen position is recomputed)
 #pragma unroll
@@ -609,12 +624,12 @@ __device__ __forceinline__ void stage_project(const IntegrateArgs& a, const Unit
             const float sx = fmaf(a.M[2], pz, bsx), sy = fmaf(a.M[5], pz, bsy), sz = fmaf(a.M[8], pz, bsz);
             const int ix = f2i_rd(sx / sz), iy = f2i_rd(sy / sz);
             const bool in = ix >= 0 && ix < a.width && iy >= 0 && iy < a.height;
-            P.img[k] = in ? iy * a.width + ix : -1;
+            P.img[k] = in ? iy * a.width + ix : npx;
         }
     }
-    // unconditional gathers (off-image lanes read pixel 0 and ignore it)
+    // unconditional gathers; an off-image voxel reads the zero record past the image (depth 0)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) P.rec[k] = a.pyr.px[max(P.img[k], 0)];
+    for (int k = 0; k < 4; ++k) P.rec[k] = a.pyr.px[P.img[k]];
 }
 
 template <bool SEM, bool GATE, bool VOTE, bool COUNT>
@@ -625,7 +640,7 @@ __device__ __forceinline__ void stage_classify(const IntegrateArgs& a, const Pro
     float dm[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const float d = P.img[k] >= 0 ? __uint_as_float(P.rec[k].x) : 0.0f;
+        const float d = __uint_as_float(P.rec[k].x);
         dm[k] = d;
         const float diff = d - P.qz[k];
         const bool t = (d != 0.0f) & (diff > -g.mu);
@@ -689,7 +704,7 @@ __device__ __forceinline__ void stage_load(const IntegrateArgs& a, const UnitPos
         L.vc4 = *(t ? reinterpret_cast<const int4*>(a.b.cls + v) : reinterpret_cast<const int4*>(dummy));
         L.vn4 = *(t ? reinterpret_cast<const int4*>(a.b.cls_cnt + v) : reinterpret_cast<const int4*>(dummy));
 #pragma unroll
-        for (int k = 0; k < 4; ++k) L.vin[k] = a.cls[max(C.img[k], 0)];
+        for (int k = 0; k < 4; ++k) L.vin[k] = a.cls[C.img[k] < a.width * a.height ? C.img[k] : 0];
     }
 }
 
@@ -840,7 +855,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_INT
     for (int i = (int)threadIdx.x; i < kRcpTable; i += (int)blockDim.x) s_rcp[i] = a.rcp_table[i];
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const unsigned loff = (unsigned)(lane >> 3) * (unsigned)a.g.zs + (unsigned)(lane & 7) * 4u;
+    // the lane's offset from the unit origin (a volume has < 2^31 stored voxels per x-plane pair)
+    const unsigned loff = (unsigned)lane_x(lane) * (unsigned)a.g.dimy * (unsigned)a.g.zs +
+                          (unsigned)lane_y(lane) * (unsigned)a.g.zs + (unsigned)lane_zq(lane) * 4u;
     const unsigned wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     const unsigned nwaves = gridDim.x * (blockDim.x >> 6);
     // segment counts, one per lane; inclusive prefix over the lanes (kListSegs == 64)
