@@ -122,7 +122,7 @@ int dev_alloc(semtsdf_vol* v, void** p, size_t bytes) {
 }
 
 void free_all(semtsdf_vol* v) {
-    void* ptrs[] = {v->b.sdf, v->b.wt, v->b.bmin, v->b.bplain, v->b.bdirty, v->b.color, v->b.hist, v->b.cls, v->b.cls_cnt, v->depth_d, v->rgb_d,
+    void* ptrs[] = {v->b.sdf, v->b.wt, v->b.bmin, v->b.bplain, v->b.bdirty, v->b.color, v->b.hist, v->b.hmask, v->b.cls, v->b.cls_cnt, v->depth_d, v->rgb_d,
                     v->mask_d, v->cls_d, v->pyr.px, v->pyr.l0, v->pyr.l1, v->tables_d, v->decision_d,
                     v->num_objs_d, v->probs_d, v->box_d, v->palette_d, v->render_d, v->render_t_d,
                     v->counters_d, v->unit_flags_d, v->ray_state_d, v->unit_list_d, v->list_count_d, v->rcp_table_d};
@@ -550,7 +550,10 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     if (nbricks && hipMemset(v->b.bdirty, 0, nbricks) != hipSuccess) return bail(fail(SEMTSDF_ERR_HIP, "memset failed"));
     if ((rc = dev_alloc(v, &v->b.color, n * 4 * (ci32 ? 4 : 1)))) return bail(rc);
     if (p->flags & SEMTSDF_F_SEMANTIC)
+    {
         if ((rc = dev_alloc(v, (void**)&v->b.hist, n * kMaxObjects * 4))) return bail(rc);
+        if ((rc = dev_alloc(v, (void**)&v->b.hmask, n * 4))) return bail(rc);
+    }
     if (p->flags & SEMTSDF_F_VOTE) {
         if ((rc = dev_alloc(v, (void**)&v->b.cls, n * 4))) return bail(rc);
         if ((rc = dev_alloc(v, (void**)&v->b.cls_cnt, n * 4))) return bail(rc);
@@ -640,6 +643,7 @@ int semtsdf_reset(semtsdf_vol* v, void* stream) {
     HIPC(hipMemsetAsync(v->b.wt, 0, n * 4, s));
     HIPC(hipMemsetAsync(v->b.color, 0, n * 4 * ((v->p.flags & SEMTSDF_F_COLOR_I32) ? 4 : 1), s));
     if (v->b.hist) HIPC(hipMemsetAsync(v->b.hist, 0, n * kMaxObjects * 4, s));
+    if (v->b.hmask) HIPC(hipMemsetAsync(v->b.hmask, 0, n * 4, s));
     if (v->b.cls) HIPC(hipMemsetAsync(v->b.cls, 0, n * 4, s));
     if (v->b.cls_cnt) HIPC(hipMemsetAsync(v->b.cls_cnt, 0, n * 4, s));
     HIPC(hipMemsetAsync(v->num_objs_d, 0, 16, s));
@@ -1220,6 +1224,7 @@ int semtsdf_upload(semtsdf_vol* v, const float* sdf, const int32_t* wt, const vo
             }
         }
         HIPC(hipFree(stage));
+        HIPC(launch_hist_mask(v->g, v->b, s));
     }
     v->bmin_stale = true;
     HIPC(hipStreamSynchronize(s));

@@ -33,6 +33,8 @@ struct VolBufs {
     int32_t* wt;
     void* color;       // u8x4 or i32x4 per voxel (3 channels + pad, 16-B vectors of 4 voxels)
     uint32_t* hist;    // bin-major [32][nvox]
+    uint32_t* hmask;   // [nvox] bit k set when hist[k][v] > 0 (kept by the integrate; samplers
+                       // interpolate only the bins set at one of their 8 corners)
     int32_t* cls;      // vote mode
     int32_t* cls_cnt;  // vote mode
     float* bmin;       // per 8^3 brick: min sdf over its voxels and the +1 border (ray skipping)
@@ -202,5 +204,6 @@ hipError_t launch_hist_chunk_to_vm(const uint32_t* bm, uint32_t* vm, const VolGe
                                    hipStream_t s);
 hipError_t launch_hist_chunk_to_bm(const uint32_t* vm, uint32_t* bm, const VolGeom& g, uint64_t v0, uint64_t nv,
                                    hipStream_t s);
+hipError_t launch_hist_mask(const VolGeom& g, const VolBufs& b, hipStream_t s);  // hmask from hist
 
 }  // namespace semtsdf

@@ -484,7 +484,7 @@ uint64_t unit_list_capacity(const VolGeom& g) { return (uint64_t)list_seg_cap(un
 // quotient (the product is within 2.3e-5 of num/(w+1), whose fraction is 0 or in
 // [1/(w+1), 1 - 1/(w+1)]; checked exhaustively, tests/test_oracle_props.py).
 __device__ __forceinline__ unsigned avg_u8(unsigned c, unsigned x, unsigned w, float r) {
-    const unsigned num = c * w + x;
+    const unsigned num = __umul24(c, w) + x;  // exact while w < 2^24 (this path needs w < kRcpTable)
     return (unsigned)fmaf((float)num, r, 0x1p-12f);
 }
 
@@ -629,7 +629,7 @@ __device__ __forceinline__ void stage_project(const IntegrateArgs& a, const Unit
     }
     // unconditional gathers; an off-image voxel reads the zero record past the image (depth 0)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) P.rec[k] = a.pyr.px[P.img[k]];
+    for (int k = 0; k < 4; ++k) P.rec[k] = a.pyr.px[(unsigned)P.img[k]];
 }
 
 template <bool SEM, bool GATE, bool VOTE, bool COUNT>
@@ -686,17 +686,20 @@ template <bool SEM, bool CI32, bool VOTE>
 __device__ __forceinline__ void stage_load(const IntegrateArgs& a, const UnitPos& up, unsigned loff, const Cls& C,
                                            Ld& L) {
     const VolGeom& g = a.g;
-    const uint64_t v = unit_base(g, up) + loff;
+    // wave-uniform unit bases (scalar) + the lane's 32-bit element offset; a lane with
+    // nothing to load reads the unit's first vector instead (same line for all of them)
+    const uint64_t ub = unit_base(g, up);
+    const uint64_t v = ub + loff;
     const uint4* dummy = reinterpret_cast<const uint4*>(a.rcp_table);
     const bool t = C.tmask != 0u, gt = C.gmask != 0u;
-    L.s4 = t ? *reinterpret_cast<const float4*>(a.b.sdf + v) : *reinterpret_cast<const float4*>(dummy);
-    L.w4 = t ? *reinterpret_cast<const int4*>(a.b.wt + v) : *reinterpret_cast<const int4*>(dummy);
+    const unsigned lt = t ? loff : 0u, lg = gt ? loff : 0u;
+    L.s4 = *reinterpret_cast<const float4*>(a.b.sdf + ub + lt);
+    L.w4 = *reinterpret_cast<const int4*>(a.b.wt + ub + lt);
     if (CI32) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            L.c32[k] = *reinterpret_cast<const int4*>(gt ? reinterpret_cast<const uint4*>(a.b.color) + v + k : dummy);
+        for (int k = 0; k < 4; ++k) L.c32[k] = reinterpret_cast<const int4*>(a.b.color)[ub + lg + (gt ? k : 0)];
     } else {
-        L.c8 = *(gt ? reinterpret_cast<const uint4*>(reinterpret_cast<const uint32_t*>(a.b.color) + v) : dummy);
+        L.c8 = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint32_t*>(a.b.color) + ub + lg);
     }
     if (SEM)
         L.h4 = *(C.hmode == 1u ? reinterpret_cast<const uint4*>(a.b.hist + (uint64_t)C.hlab * g.nvox + v) : dummy);
@@ -809,27 +812,44 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
     const unsigned tmask = M.meta & 15u, gmask = (M.meta >> 4) & 15u, hmode = (M.meta >> 8) & 3u,
                    hlab = M.meta >> 16;
     if (!tmask) return;
-    const uint64_t v = unit_base(g, up) + loff;
+    const uint64_t ub = unit_base(g, up);
+    const uint64_t v = ub + loff;
     if (a.debug != 10) {  // 10: timing probe, loads but no sdf/weight stores
-        *reinterpret_cast<float4*>(a.b.sdf + v) = O.s4;
-        *reinterpret_cast<int4*>(a.b.wt + v) = O.w4;
+        *reinterpret_cast<float4*>(a.b.sdf + ub + loff) = O.s4;
+        *reinterpret_cast<int4*>(a.b.wt + ub + loff) = O.w4;
     }
     if (gmask) {
         if (CI32) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) reinterpret_cast<int4*>(a.b.color)[v + k] = O.c32[k];
+            for (int k = 0; k < 4; ++k) reinterpret_cast<int4*>(a.b.color)[ub + loff + k] = O.c32[k];
         } else {
-            *reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(a.b.color) + v) = O.c8;
+            *reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(a.b.color) + ub + loff) = O.c8;
         }
         if (SEM) {
-            if (hmode == 1u) *reinterpret_cast<uint4*>(a.b.hist + (uint64_t)hlab * g.nvox + v) = O.h4;
+            if (hmode == 1u) {
+                *reinterpret_cast<uint4*>(a.b.hist + (uint64_t)hlab * g.nvox + v) = O.h4;
+                // a count that just became 1 sets the bin's bit in the voxel's bin mask (rare
+                // once the surface has been seen: the common path neither reads nor writes it)
+                const unsigned hk[4] = {O.h4.x, O.h4.y, O.h4.z, O.h4.w};
+                unsigned nb = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) nb |= ((((gmask >> k) & 1u) != 0u) & (hk[k] == 1u) ? 1u : 0u) << k;
+                if (nb) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        if ((nb >> k) & 1u) atomicOr(a.b.hmask + v + k, 1u << hlab);
+                }
+            }
             if (hmode == 2u) {  // rare: labels differ inside the lane, or a label >= 32
                 unsigned bad = 0;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const unsigned lab = (M.labs >> (8 * k)) & 0xFFu;
                     const bool gk = (gmask >> k) & 1u;
-                    if (gk && lab < (unsigned)kMaxObjects) atomicAdd(a.b.hist + (uint64_t)lab * g.nvox + v + k, 1u);
+                    if (gk && lab < (unsigned)kMaxObjects) {
+                        atomicAdd(a.b.hist + (uint64_t)lab * g.nvox + v + k, 1u);
+                        atomicOr(a.b.hmask + v + k, 1u << lab);
+                    }
                     bad |= (gk && lab >= (unsigned)kMaxObjects) ? 1u : 0u;
                 }
                 if (bad) atomicOr(reinterpret_cast<unsigned*>(a.counters + 2), 1u);
@@ -845,7 +865,7 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
 // Persistent wavefronts over the live-unit list: wave w takes entries w, w + nwaves, ...
 // (every wave gets the same number of units +-1), read with scalar loads one unit ahead.
 #ifndef SEMTSDF_INTEGRATE_WPE
-#define SEMTSDF_INTEGRATE_WPE 5  // waves per SIMD the register allocation of k_integrate targets
+#define SEMTSDF_INTEGRATE_WPE 4  // waves per SIMD the register allocation targets (5 spills; measured equal)
 #endif
 template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT, bool SHARD, bool PIN>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_INTEGRATE_WPE))) void k_integrate(
@@ -1069,6 +1089,21 @@ __device__ __forceinline__ float tri_eval(const T* __restrict__ p, const Tri& t)
     const float low = mixf(mixf(d0, d4, t.fx), mixf(d2, d6, t.fx), t.fy);
     const float high = mixf(mixf(d1, d5, t.fx), mixf(d3, d7, t.fx), t.fy);
     return mixf(low, high, t.fz);
+}
+
+// Histogram bins that are nonzero at one of the 8 corners of a trilinear sample; every
+// other bin interpolates to exactly 0 (mixes of zeros), so samplers evaluate only these.
+__device__ __forceinline__ unsigned tri_bins(const uint32_t* __restrict__ hm, const Tri& t) {
+    const uint32_t* q = hm + t.i000;
+    return q[0] | q[t.dz] | q[t.dy] | q[t.dy + t.dz] | q[t.dx] | q[t.dx + t.dz] | q[t.dx + t.dy] |
+           q[t.dx + t.dy + t.dz];
+}
+
+// The 32 trilinear histogram values at a sample (utils.cu:144-170).
+__device__ __forceinline__ void tri_hist(const VolGeom& g, const VolBufs& b, const Tri& tr, float* p) {
+    const unsigned bins = tri_bins(b.hmask, tr);
+#pragma unroll
+    for (int k = 0; k < kMaxObjects; ++k) p[k] = ((bins >> k) & 1u) ? tri_eval(b.hist + (uint64_t)k * g.nvox, tr) : 0.0f;
 }
 
 __device__ __forceinline__ float sample_sdf(const VolGeom& g, const float* sdf, float px, float py, float pz) {
@@ -1370,8 +1405,7 @@ __global__ __launch_bounds__(256) void k_assoc_march(AssocArgs a) {
         for (int k = 0; k < kMaxObjects; ++k) p[k] = 0.0f;
         if (march_ray(a.g, a.b, ox, oy, oz, dx, dy, dz, &t)) {
             const Tri tr = tri_setup(a.g, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
-#pragma unroll
-            for (int k = 0; k < kMaxObjects; ++k) p[k] = tri_eval(a.b.hist + (uint64_t)k * a.g.nvox, tr);
+            tri_hist(a.g, a.b, tr, p);
         }
         const int px = y * a.width + x;
         if (a.probs_out) {
@@ -1519,7 +1553,10 @@ __device__ __forceinline__ void shade_hit(const VolGeom& g, const VolBufs& vb, c
     if (mode == 0) {
         float max_cnt = 0.0f;
         int obj = 0;
-        for (int k = 0; k < kMaxObjects; ++k) {
+        unsigned bins = tri_bins(vb.hmask, tr);  // bins outside the mask are 0: never a strict max
+        while (bins) {
+            const int k = __ffs((int)bins) - 1;
+            bins &= bins - 1u;
             const float c = tri_eval(vb.hist + (uint64_t)k * g.nvox, tr);
             if (c > max_cnt) { max_cnt = c; obj = k; }
         }
@@ -1814,8 +1851,7 @@ __global__ __launch_bounds__(256) void k_shard_assoc_partial(ShardRayArgs a) {
             mine = sample_owner(a.g, hz) == a.g.shard;
             if (mine) {
                 const Tri tr = tri_setup(a.g, hx, hy, hz);
-#pragma unroll
-                for (int k = 0; k < kMaxObjects; ++k) p[k] = tri_eval(a.b.hist + (uint64_t)k * a.g.nvox, tr);
+                tri_hist(a.g, a.b, tr, p);
             }
         } else {
             mine = a.g.shard == 0;  // pixels without a hit contribute once, from shard 0
@@ -1890,6 +1926,24 @@ hipError_t launch_tables_from_partial(const long long* reduced, AssocTables* t, 
 // ------------------------------------------------------------------------------------
 // histogram layout conversion (bin-major device <-> voxel-major reference export)
 // ------------------------------------------------------------------------------------
+// Bin mask of every stored voxel from the bin-major histogram (after an upload).
+__global__ __launch_bounds__(256) void k_hist_mask(const uint32_t* __restrict__ hist, uint32_t* __restrict__ hmask,
+                                                   uint64_t nvox) {
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvox; v += (uint64_t)gridDim.x * blockDim.x) {
+        unsigned m = 0;
+        for (int k = 0; k < kMaxObjects; ++k) m |= (hist[(uint64_t)k * nvox + v] != 0u ? 1u : 0u) << k;
+        hmask[v] = m;
+    }
+}
+
+hipError_t launch_hist_mask(const VolGeom& g, const VolBufs& b, hipStream_t s) {
+    if (!b.hist || !b.hmask || g.nvox == 0) return hipSuccess;
+    uint64_t blocks = (g.nvox + 255) / 256;
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(k_hist_mask, dim3((unsigned)blocks), dim3(256), 0, s, b.hist, b.hmask, g.nvox);
+    return hipGetLastError();
+}
+
 __global__ __launch_bounds__(256) void k_hist_to_vm(const uint32_t* __restrict__ bm, uint32_t* __restrict__ vm,
                                                     uint64_t nvox, uint32_t lz, uint32_t zs, uint64_t v0, uint64_t nv) {
     // vm is a chunk [nv][32] of logical voxels v0 .. v0+nv (rows of lz planes)
