@@ -24,6 +24,7 @@ struct VolGeom {
     float mu;
     uint64_t nvox;             // dimx * dimy * zs (stored voxels, padding planes included)
     int nbx, nby, nbz;         // 8^3 bricks of the local storage (empty-space map)
+    int nsx, nsy, nsz;         // 64^3 super-bricks (8^3 bricks each)
     float rvox[3];             // RN(1 / voxel) per axis (exact divisions by the voxel size)
 };
 
@@ -39,6 +40,7 @@ struct VolBufs {
     int32_t* cls_cnt;  // vote mode
     float* bmin;       // per 8^3 brick: min sdf over its voxels and the +1 border (ray skipping)
     float* bplain;     // per 8^3 brick: min sdf over its own voxels
+    float* sbmin;      // per 64^3 super-brick (8^3 bricks): min of bmin over its bricks
     uint8_t* bdirty;   // per 8^3 brick: overlaps a unit integrated since the last map update
 };
 

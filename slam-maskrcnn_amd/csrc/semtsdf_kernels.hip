@@ -179,11 +179,30 @@ __global__ __launch_bounds__(256) void k_brick_dilate(VolGeom g, const float* __
     bmin[br] = m;
 }
 
+// Super-brick level: sbmin[s] = min of bmin over the (up to) 8^3 bricks of super-brick s,
+// so it bounds every trilinear sample based in its 64^3 voxels.  One wave per super-brick.
+__global__ __launch_bounds__(256) void k_brick_super(VolGeom g, const float* __restrict__ bmin, float* __restrict__ sbmin) {
+    const unsigned ns = (unsigned)g.nsx * g.nsy * g.nsz;
+    const unsigned sb = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (sb >= ns) return;
+    const int lane = threadIdx.x & 63;
+    const int sz = sb % g.nsz, sy = (sb / g.nsz) % g.nsy, sx = sb / (g.nsz * g.nsy);
+    float m = 3.0e38f;
+    const int bx = sx * 8 + (lane >> 3), by = sy * 8 + (lane & 7);  // lane = one (x, y) brick column
+    if (bx < g.nbx && by < g.nby)
+        for (int k = 0; k < 8 && sz * 8 + k < g.nbz; ++k)
+            m = fminf(m, bmin[((unsigned)bx * g.nby + (unsigned)by) * g.nbz + (unsigned)(sz * 8 + k)]);
+    for (int off = 32; off > 0; off >>= 1) m = fminf(m, __shfl_xor(m, off, 64));
+    if (lane == 0) sbmin[sb] = m;
+}
+
 hipError_t launch_brick_min(const VolGeom& g, const VolBufs& b, bool all, hipStream_t s) {
     const unsigned nb = (unsigned)g.nbx * g.nby * g.nbz;
     if (nb == 0) return hipSuccess;
     hipLaunchKernelGGL(k_brick_plain, dim3((nb + 3) / 4), dim3(256), 0, s, g, b.sdf, b.bplain, b.bdirty, all ? 1 : 0);
     hipLaunchKernelGGL(k_brick_dilate, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.bplain, b.bmin);
+    const unsigned ns = (unsigned)g.nsx * g.nsy * g.nsz;
+    if (b.sbmin && ns) hipLaunchKernelGGL(k_brick_super, dim3((ns + 3) / 4), dim3(256), 0, s, g, b.bmin, b.sbmin);
     return hipGetLastError();
 }
 
@@ -1136,9 +1155,11 @@ __device__ __forceinline__ float skip_threshold(const VolGeom& g) { return g.vox
 // Sample evaluator with the brick map: returns false (and no value) when the sample's
 // brick is known to hold only values >= thr.  Caches the last brick looked up.
 struct SkipCursor {
-    int brick = -1;
+    int brick = -1;      // brick of the last lookup, or -2 - s while super-brick s is skipped
     bool skip = false;
-    float lo[3], hi[3];  // approximate voxel-coordinate box surely inside the skippable brick
+    int sb = -1;         // super-brick of the last lookup
+    bool sskip = false;
+    float lo[3], hi[3];  // approximate voxel-coordinate box surely inside the skippable (super-)brick
 };
 
 // Approximate voxel coordinates of a ray point (|error| ~1e-4 voxel; only used to prove
@@ -1157,6 +1178,21 @@ __device__ __forceinline__ RayVox ray_vox(const VolGeom& g, float ox, float oy, 
     return r;
 }
 
+// Ray parameter where the ray leaves the cursor's box (computed with the same approximate
+// voxel coordinates; samples before it are inside the box, which is itself a margin inside
+// the skippable brick).
+__device__ __forceinline__ float skip_box_exit(const SkipCursor& cur, const RayVox& rv) {
+    float te = 3.0e38f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float k = rv.k[i];
+        const float bound = k > 0.0f ? cur.hi[i] : cur.lo[i];
+        const float ti = (bound - rv.c[i]) / k;  // k == 0: +-inf or NaN, ignored by fminf / the > test
+        te = (k != 0.0f && ti < te) ? ti : te;
+    }
+    return te * (1.0f - 0x1p-16f);
+}
+
 __device__ __forceinline__ bool in_skip_box(const SkipCursor& cur, const RayVox& rv, float t) {
     const float ax = fmaf(t, rv.k[0], rv.c[0]), ay = fmaf(t, rv.k[1], rv.c[1]), az = fmaf(t, rv.k[2], rv.c[2]);
     return (ax > cur.lo[0]) & (ax < cur.hi[0]) & (ay > cur.lo[1]) & (ay < cur.hi[1]) & (az > cur.lo[2]) &
@@ -1166,26 +1202,49 @@ __device__ __forceinline__ bool in_skip_box(const SkipCursor& cur, const RayVox&
 // Evaluates the sample at p unless the brick map proves it >= voxel/2 (returns false).
 // Caches the last brick looked up and, with `box`, the conservative voxel-coordinate box
 // of a skippable brick for in_skip_box.
+__device__ __forceinline__ void skip_box(const VolGeom& g, SkipCursor& cur, int x0, int y0, int z0, int n, bool lx,
+                                         bool hx, bool ly, bool hy, bool lz, bool hz) {
+    // (super-)brick bounds in voxel coordinates, shrunk by a margin far above the
+    // approximation error of RayVox; the outer faces of the volume extend to infinity
+    // (samples there clamp into the edge brick)
+    const float m = 0.01f;
+    cur.lo[0] = lx ? -1e30f : (float)x0 + m;
+    cur.hi[0] = hx ? 1e30f : (float)(x0 + n) - m;
+    cur.lo[1] = ly ? -1e30f : (float)y0 + m;
+    cur.hi[1] = hy ? 1e30f : (float)(y0 + n) - m;
+    cur.lo[2] = lz ? -1e30f : (float)z0 + m;
+    cur.hi[2] = hz ? 1e30f : (float)(z0 + n) - m;
+}
+
 __device__ __forceinline__ bool sample_or_skip(const VolGeom& g, const VolBufs& b, float thr, SkipCursor& cur,
                                                float px, float py, float pz, float* f, bool box = false) {
     const TriCoord c = tri_coord(g, px, py, pz);
     if (b.bmin) {
+        if (box && b.sbmin) {  // super-brick level first: one lookup per 64^3 voxels of free space
+            const int sx = c.xc >> 6, sy = c.yc >> 6, sz = c.zl >> 6;
+            const int sb = (sx * g.nsy + sy) * g.nsz + sz;
+            if (sb != cur.sb) {
+                cur.sb = sb;
+                cur.sskip = b.sbmin[sb] >= thr;
+            }
+            if (cur.sskip) {
+                if (cur.brick != -2 - sb) {
+                    cur.brick = -2 - sb;
+                    cur.skip = true;
+                    skip_box(g, cur, sx * 64, sy * 64, sz * 64, 64, sx == 0, sx == g.nsx - 1, sy == 0, sy == g.nsy - 1,
+                             sz == 0, sz == g.nsz - 1);
+                }
+                return false;
+            }
+        }
         const int br = brick_of(g, c);
         if (br != cur.brick) {
             cur.brick = br;
             cur.skip = b.bmin[br] >= thr;
             if (cur.skip && box) {
-                // brick bounds in voxel coordinates, shrunk by a margin far above the
-                // approximation error of RayVox; the outer faces of the volume extend to
-                // infinity (samples there clamp into the edge brick)
                 const int bx = c.xc >> 3, by = c.yc >> 3, bz = c.zl >> 3;
-                const float m = 0.01f;
-                cur.lo[0] = bx == 0 ? -1e30f : 8.0f * bx + m;
-                cur.hi[0] = bx == g.nbx - 1 ? 1e30f : 8.0f * bx + 8.0f - m;
-                cur.lo[1] = by == 0 ? -1e30f : 8.0f * by + m;
-                cur.hi[1] = by == g.nby - 1 ? 1e30f : 8.0f * by + 8.0f - m;
-                cur.lo[2] = bz == 0 ? -1e30f : 8.0f * bz + m;
-                cur.hi[2] = bz == g.nbz - 1 ? 1e30f : 8.0f * bz + 8.0f - m;
+                skip_box(g, cur, bx * 8, by * 8, bz * 8, 8, bx == 0, bx == g.nbx - 1, by == 0, by == g.nby - 1,
+                         bz == 0, bz == g.nbz - 1);
             }
         }
         if (cur.skip) return false;
@@ -1228,11 +1287,19 @@ __device__ bool march_ray(const VolGeom& g, const VolBufs& b, float ox, float oy
     while (t < tfar) {
         if (st) st->iters++;
         if (box && cur.skip && in_skip_box(cur, rv, t)) {
+            // the same additions as sample-by-sample stepping (the hit position depends on
+            // them), tested against the box's exit parameter, then exactly near the exit
+            const float tend = fminf(tfar, skip_box_exit(cur, rv));
             do {
                 t_prev = t;
                 t += step;
                 if (st) st->skipped++;
-            } while (t < tfar && in_skip_box(cur, rv, t));
+            } while (t < tend);
+            while (t < tfar && in_skip_box(cur, rv, t)) {
+                t_prev = t;
+                t += step;
+                if (st) st->skipped++;
+            }
             prev_skipped = true;  // those samples are >= voxel/2: no hit, no step switch
             f_tt = 1.0f;
             if (!(t < tfar)) break;
