@@ -315,6 +315,10 @@ int associate_impl(semtsdf_vol* v, uint8_t* mask_d, const float E[16], hipStream
     a.box_thresh = v->p.box_thresh;
     a.mask = mask_d;
     a.tables = v->tables_d;
+    {
+        static const char* dbg = getenv("SEMTSDF_DEBUG_ASSOC");  // timing probes only
+        a.debug = dbg ? atoi(dbg) : 0;
+    }
     HIPC(launch_assoc_march(a, s));
     HIPC(launch_assoc_decide(v->tables_d, v->decision_d, 0, v->p.prior_mrcnn_err_rate, v->num_objs_d, s));
     HIPC(launch_relabel(mask_d, (int)npx(v), v->decision_d, s));

@@ -130,6 +130,7 @@ struct AssocArgs {
     AssocTables* tables;
     float* probs_out;       // optional debug [H*W*32]
     uint8_t* box_out;       // optional debug [H*W*32]
+    int debug;              // timing probes (SEMTSDF_DEBUG_ASSOC): 1 no accumulation, 2 no march
 };
 
 struct RenderArgs {

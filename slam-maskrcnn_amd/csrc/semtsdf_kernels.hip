@@ -1259,6 +1259,11 @@ struct MarchStats {
     unsigned iters = 0, lookups = 0, evals = 0, skipped = 0;
 };
 
+#ifndef SEMTSDF_MARCH_SPEC
+#define SEMTSDF_MARCH_SPEC 3
+#endif
+constexpr int kMarchSpec = SEMTSDF_MARCH_SPEC;  // speculative samples per evaluated sample
+
 __device__ bool march_ray(const VolGeom& g, const VolBufs& b, float ox, float oy, float oz, float dx, float dy,
                           float dz, float* t_hit, MarchStats* st = nullptr) {
     float t, tfar;
@@ -1321,10 +1326,46 @@ __device__ bool march_ray(const VolGeom& g, const VolBufs& b, float ox, float oy
         }
         f_tt = f;
         if (f_tt < 0.0f) break;
-        if (f_tt < vx / 2.0f) step = vx / 4.0f;
         f_t = f_tt;
         prev_skipped = false;
+        if (f_tt < vx / 2.0f) {  // sticky quarter step
+            step = vx / 4.0f;
+            t += step;
+            continue;
+        }
         t += step;
+        if (kMarchSpec > 0) {
+            // An evaluated sample means the ray is near a surface: evaluate the next
+            // kMarchSpec samples of the same step in one round trip (no map lookups: a sample
+            // the map would skip evaluates to >= voxel/2, which is no event either), then
+            // run the march logic over them in order; a step switch or a hit ends the batch.
+            float fs[kMarchSpec > 0 ? kMarchSpec : 1];
+            float tn = t;
+#pragma unroll
+            for (int j = 0; j < kMarchSpec; ++j) {
+                fs[j] = sample_sdf(g, b.sdf, fmaf(tn, dx, ox), fmaf(tn, dy, oy), fmaf(tn, dz, oz));
+                tn += step;
+            }
+            if (st) st->evals += kMarchSpec;
+            bool hit = false;
+#pragma unroll
+            for (int j = 0; j < kMarchSpec; ++j) {
+                if (!(t < tfar)) break;
+                f_tt = fs[j];
+                if (f_tt < 0.0f) {
+                    hit = true;
+                    break;
+                }
+                f_t = f_tt;
+                if (f_tt < vx / 2.0f) {
+                    step = vx / 4.0f;
+                    t += step;
+                    break;
+                }
+                t += step;
+            }
+            if (hit) break;
+        }
     }
     if (!(f_tt < 0.0f)) return false;
     if (prev_skipped) f_t = sample_sdf(g, b.sdf, fmaf(t_prev, dx, ox), fmaf(t_prev, dy, oy), fmaf(t_prev, dz, oz));
@@ -1470,7 +1511,7 @@ __global__ __launch_bounds__(256) void k_assoc_march(AssocArgs a) {
         float p[kMaxObjects];
 #pragma unroll
         for (int k = 0; k < kMaxObjects; ++k) p[k] = 0.0f;
-        if (march_ray(a.g, a.b, ox, oy, oz, dx, dy, dz, &t)) {
+        if (a.debug != 2 && march_ray(a.g, a.b, ox, oy, oz, dx, dy, dz, &t)) {
             const Tri tr = tri_setup(a.g, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
             tri_hist(a.g, a.b, tr, p);
         }
@@ -1482,7 +1523,7 @@ __global__ __launch_bounds__(256) void k_assoc_march(AssocArgs a) {
                 a.box_out[(size_t)px * kMaxObjects + k] = p[k] > a.box_thresh ? 1 : 0;
             }
         }
-        assoc_accumulate(s, p, a.mask[px], a.n_obs, a.eps, a.box_thresh);
+        if (a.debug != 1) assoc_accumulate(s, p, a.mask[px], a.n_obs, a.eps, a.box_thresh);
     }
     __syncthreads();
     AssocTables* T = a.tables;
