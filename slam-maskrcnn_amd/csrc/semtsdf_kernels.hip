@@ -140,27 +140,45 @@ hipError_t launch_copy_f4(const void* src, void* dst, size_t n16, hipStream_t s)
 // sample based in brick b reads.
 __global__ __launch_bounds__(256) void k_brick_plain(VolGeom g, const float* __restrict__ sdf, float* __restrict__ plain,
                                                      uint8_t* __restrict__ dirty, int all) {
-    const unsigned nb = (unsigned)g.nbx * g.nby * g.nbz;
-    const unsigned br = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (br >= nb) return;
-    if (!all && !dirty[br]) return;
+    // one wave per 4 z-consecutive bricks: lane = one (x, y) row of 32 voxels = one whole
+    // 128-B line (a row of a single brick is only 32 B of a line)
+    const unsigned nbq = (unsigned)(g.nbz + 3) / 4;
+    const unsigned nq = (unsigned)g.nbx * g.nby * nbq;
+    const unsigned q = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq) return;
     const int lane = threadIdx.x & 63;
-    const int bz = br % g.nbz, by = (br / g.nbz) % g.nby, bx = br / (g.nbz * g.nby);
-    const int x = bx * 8 + (lane >> 3), y = by * 8 + (lane & 7), z0 = bz * 8;
-    float m = 3.0e38f;
+    const int bq = q % nbq, by = (q / nbq) % g.nby, bx = q / (nbq * g.nby);
+    const unsigned br0 = ((unsigned)bx * g.nby + (unsigned)by) * g.nbz + (unsigned)bq * 4;
+    const int nbr = min(4, g.nbz - bq * 4);
+    unsigned want = 0;
+    for (int j = 0; j < nbr; ++j) want |= ((all || dirty[br0 + j]) ? 1u : 0u) << j;
+    if (!want) return;  // wave-uniform
+    const int x = bx * 8 + (lane >> 3), y = by * 8 + (lane & 7), z0 = bq * 32;
+    float m[4] = {3.0e38f, 3.0e38f, 3.0e38f, 3.0e38f};
     if (x < g.dimx && y < g.dimy) {
         const float* p = sdf + (uint64_t)x * ((uint64_t)g.dimy * g.zs) + (uint64_t)y * g.zs + z0;
-        if (z0 + 8 <= g.lz) {
-            const float4 a = *reinterpret_cast<const float4*>(p), c = *reinterpret_cast<const float4*>(p + 4);
-            m = fminf(fminf(fminf(a.x, a.y), fminf(a.z, a.w)), fminf(fminf(c.x, c.y), fminf(c.z, c.w)));
+        if (z0 + 32 <= g.lz) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float4 a = *reinterpret_cast<const float4*>(p + 8 * j);
+                const float4 c = *reinterpret_cast<const float4*>(p + 8 * j + 4);
+                m[j] = fminf(fminf(fminf(a.x, a.y), fminf(a.z, a.w)), fminf(fminf(c.x, c.y), fminf(c.z, c.w)));
+            }
         } else {
-            for (int k = 0; k < g.lz - z0; ++k) m = fminf(m, p[k]);
+            for (int k = 0; k < g.lz - z0; ++k) {
+                const float v = p[k];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) m[j] = (k >> 3) == j ? fminf(m[j], v) : m[j];
+            }
         }
     }
-    for (int off = 32; off > 0; off >>= 1) m = fminf(m, __shfl_xor(m, off, 64));
-    if (lane == 0) {
-        plain[br] = m;
-        dirty[br] = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        for (int off = 32; off > 0; off >>= 1) m[j] = fminf(m[j], __shfl_xor(m[j], off, 64));
+    if (lane < nbr && ((want >> lane) & 1u)) {
+        const float mj = lane == 0 ? m[0] : lane == 1 ? m[1] : lane == 2 ? m[2] : m[3];
+        plain[br0 + lane] = mj;
+        dirty[br0 + lane] = 0;
     }
 }
 
@@ -199,7 +217,8 @@ __global__ __launch_bounds__(256) void k_brick_super(VolGeom g, const float* __r
 hipError_t launch_brick_min(const VolGeom& g, const VolBufs& b, bool all, hipStream_t s) {
     const unsigned nb = (unsigned)g.nbx * g.nby * g.nbz;
     if (nb == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_brick_plain, dim3((nb + 3) / 4), dim3(256), 0, s, g, b.sdf, b.bplain, b.bdirty, all ? 1 : 0);
+    const unsigned nq = (unsigned)g.nbx * g.nby * (unsigned)((g.nbz + 3) / 4);
+    hipLaunchKernelGGL(k_brick_plain, dim3((nq + 3) / 4), dim3(256), 0, s, g, b.sdf, b.bplain, b.bdirty, all ? 1 : 0);
     hipLaunchKernelGGL(k_brick_dilate, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.bplain, b.bmin);
     const unsigned ns = (unsigned)g.nsx * g.nsy * g.nsz;
     if (b.sbmin && ns) hipLaunchKernelGGL(k_brick_super, dim3((ns + 3) / 4), dim3(256), 0, s, g, b.bmin, b.sbmin);
