@@ -199,6 +199,11 @@ def main():
     args = ap.parse_args()
 
     rank, world, local, pg = dist_setup(args.gpus)
+    # probe: one rank's shard of an N-way volume in a single process (per-rank cost of the
+    # N-GPU weak-scaling run, measurable on one GPU); not a scaling result
+    emu_world = int(os.environ.get("BENCH_EMULATE_WORLD", "0"))
+    emu_rank = int(os.environ.get("BENCH_EMULATE_RANK", "0"))
+    shard_world, shard_rank = (emu_world, emu_rank) if (emu_world > 1 and world == 1) else (world, rank)
     import semtsdf
     from semtsdf import _lib as L
     from semtsdf.synth import SyntheticStream
@@ -214,12 +219,12 @@ def main():
     log(f"[bench rank {rank}] generated {len(frames) + 1} frames in {time.perf_counter() - t_gen:.1f}s")
 
     p = semtsdf.default_params(D, KI, W, H)
-    p.dim[2] = D * world
+    p.dim[2] = D * shard_world
     semtsdf.place_from_frame(p, f0.depth, float(np.mean(f0.depth[f0.depth > 0])) / 5000.0, L.PLACE_SFM)
     p.flags = L.F_SEMANTIC | L.F_GATE_COLOR | (L.F_NO_CULL if args.no_cull else 0)
-    if world > 1:
-        p.z_nshards = world
-        p.z_shard = rank
+    if shard_world > 1:
+        p.z_nshards = shard_world
+        p.z_shard = shard_rank
         p.z_chunk = args.z_chunk
     # CPU baseline first: the forked N-core workers then start from a process that has not
     # touched the GPU yet.
