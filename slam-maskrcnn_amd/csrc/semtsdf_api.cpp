@@ -256,10 +256,13 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
     HIPC(launch_cull(a, s));
     timing_end(v, v->ev_prep, s, &epp);
     v->n_prep++;
-    EventPair ep;  // events bracket the integrate kernel alone (the roofline kernel)
-    timing_begin(v, v->ev_integrate, s, &ep);
-    HIPC(launch_integrate(a, s));
-    timing_end(v, v->ev_integrate, s, &ep);
+    // timing: the integrate kernel's own start/end (events recorded by its dispatch, the
+    // duration rocprofv3 reports for the same kernel)
+    EventPair ep{nullptr, nullptr};
+    if ((v->instr & 1) && (hipEventCreate(&ep.a) != hipSuccess || hipEventCreate(&ep.b) != hipSuccess))
+        ep.a = ep.b = nullptr;
+    HIPC(launch_integrate(a, s, ep.a, ep.b));
+    if (ep.a) v->ev_integrate.push_back(ep);
     v->bmin_dirty = true;
     v->n_integrate++;
     return SEMTSDF_OK;

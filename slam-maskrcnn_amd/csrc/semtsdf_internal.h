@@ -191,7 +191,8 @@ hipError_t launch_depth_pyramid(const uint16_t* depth, const uint8_t* rgb, const
                                 float scale, const DepthPyramid& p, unsigned* list_count, hipStream_t s);
 hipError_t launch_color_chunk(const void* src, void* dst, bool to_ref, bool i32, const VolGeom& g, uint64_t v0,
                               uint64_t nv, hipStream_t s);
-hipError_t launch_integrate(const IntegrateArgs& a, hipStream_t s); // persistent cull + integrate
+hipError_t launch_integrate(const IntegrateArgs& a, hipStream_t s, hipEvent_t e0 = nullptr,
+                            hipEvent_t e1 = nullptr);  // e0/e1: kernel start/end events (timing)
 uint64_t unit_count(const VolGeom& g);
 uint64_t unit_list_capacity(const VolGeom& g);
 hipError_t launch_cull(const IntegrateArgs& a, hipStream_t s);       // per-unit cull flags

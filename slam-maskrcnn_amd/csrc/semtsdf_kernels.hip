@@ -22,6 +22,7 @@
 // contiguous 128-B runs of the sdf/weight planes.  The histogram is bin-major
 // ([32][voxels]) so lanes that see the same instance label update contiguous words.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <limits.h>
 #include <stdlib.h>
@@ -1000,7 +1001,7 @@ static unsigned resident_grid(K kernel) {
 }
 
 template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT, bool SHARD, bool PIN>
-static hipError_t launch_integrate_k(const IntegrateArgs& a, hipStream_t s) {
+static hipError_t launch_integrate_k(const IntegrateArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const UnitGrid ug = unit_grid(a.g);
     if (ug.n == 0) return hipSuccess;
     // persistent grid of the resident capacity; the waves share the list evenly, so a grid
@@ -1012,49 +1013,54 @@ static hipError_t launch_integrate_k(const IntegrateArgs& a, hipStream_t s) {
     if (a.debug >= 100) grid = grid0 * (unsigned)(a.debug - 100) / 8u;  // probe: fraction of residency
     static const char* gpc = getenv("SEMTSDF_GRID_PER_CU");              // probe: blocks per CU
     if (gpc && atoi(gpc) > 0) grid = ncu * (unsigned)atoi(gpc);
-    hipLaunchKernelGGL((k_integrate<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>), dim3(grid), dim3(256), 0, s, a, ug,
-                       list_seg_cap(ug));
+    if (e0) {  // timing: events recorded by the dispatch itself (kernel start / end)
+        hipExtLaunchKernelGGL((k_integrate<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>), dim3(grid), dim3(256), 0, s, e0,
+                              e1, 0, a, ug, list_seg_cap(ug));
+    } else {
+        hipLaunchKernelGGL((k_integrate<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>), dim3(grid), dim3(256), 0, s, a, ug,
+                           list_seg_cap(ug));
+    }
     return hipGetLastError();
 }
 
 template <bool SEM, bool GATE, bool CI32, bool VOTE>
-static hipError_t launch_integrate_t(const IntegrateArgs& a, bool count, hipStream_t s) {
+static hipError_t launch_integrate_t(const IntegrateArgs& a, bool count, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const bool shard = a.g.nshards > 1, pin = a.pinhole != 0;
     if (count) {  // measurement pass: pinhole only is not assumed
-        if (shard) return launch_integrate_k<SEM, GATE, CI32, VOTE, true, true, false>(a, s);
-        return launch_integrate_k<SEM, GATE, CI32, VOTE, true, false, false>(a, s);
+        if (shard) return launch_integrate_k<SEM, GATE, CI32, VOTE, true, true, false>(a, s, e0, e1);
+        return launch_integrate_k<SEM, GATE, CI32, VOTE, true, false, false>(a, s, e0, e1);
     }
     if (shard) {
-        if (pin) return launch_integrate_k<SEM, GATE, CI32, VOTE, false, true, true>(a, s);
-        return launch_integrate_k<SEM, GATE, CI32, VOTE, false, true, false>(a, s);
+        if (pin) return launch_integrate_k<SEM, GATE, CI32, VOTE, false, true, true>(a, s, e0, e1);
+        return launch_integrate_k<SEM, GATE, CI32, VOTE, false, true, false>(a, s, e0, e1);
     }
-    if (pin) return launch_integrate_k<SEM, GATE, CI32, VOTE, false, false, true>(a, s);
-    return launch_integrate_k<SEM, GATE, CI32, VOTE, false, false, false>(a, s);
+    if (pin) return launch_integrate_k<SEM, GATE, CI32, VOTE, false, false, true>(a, s, e0, e1);
+    return launch_integrate_k<SEM, GATE, CI32, VOTE, false, false, false>(a, s, e0, e1);
 }
 
-hipError_t launch_integrate(const IntegrateArgs& a, hipStream_t s) {
+hipError_t launch_integrate(const IntegrateArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const bool count = a.counters != nullptr && (a.flags & 0x80000000u);
     const bool sem = a.flags & 0x1u, gate = a.flags & 0x2u, ci32 = a.flags & 0x4u, vote = a.flags & 0x8u;
     // Instantiated mode combinations: SfM semantic (u8 colour, gated), TSDF+colour (NumPy
     // rule: i32 colour, ungated), TSDF_Python vote, plus their neighbours.
     if (vote) {
-        if (ci32) return launch_integrate_t<false, false, true, true>(a, count, s);
-        return launch_integrate_t<false, false, false, true>(a, count, s);
+        if (ci32) return launch_integrate_t<false, false, true, true>(a, count, s, e0, e1);
+        return launch_integrate_t<false, false, false, true>(a, count, s, e0, e1);
     }
     if (sem) {
         if (gate) {
-            if (ci32) return launch_integrate_t<true, true, true, false>(a, count, s);
-            return launch_integrate_t<true, true, false, false>(a, count, s);
+            if (ci32) return launch_integrate_t<true, true, true, false>(a, count, s, e0, e1);
+            return launch_integrate_t<true, true, false, false>(a, count, s, e0, e1);
         }
-        if (ci32) return launch_integrate_t<true, false, true, false>(a, count, s);
-        return launch_integrate_t<true, false, false, false>(a, count, s);
+        if (ci32) return launch_integrate_t<true, false, true, false>(a, count, s, e0, e1);
+        return launch_integrate_t<true, false, false, false>(a, count, s, e0, e1);
     }
     if (gate) {
-        if (ci32) return launch_integrate_t<false, true, true, false>(a, count, s);
-        return launch_integrate_t<false, true, false, false>(a, count, s);
+        if (ci32) return launch_integrate_t<false, true, true, false>(a, count, s, e0, e1);
+        return launch_integrate_t<false, true, false, false>(a, count, s, e0, e1);
     }
-    if (ci32) return launch_integrate_t<false, false, true, false>(a, count, s);
-    return launch_integrate_t<false, false, false, false>(a, count, s);
+    if (ci32) return launch_integrate_t<false, false, true, false>(a, count, s, e0, e1);
+    return launch_integrate_t<false, false, false, false>(a, count, s, e0, e1);
 }
 
 // ------------------------------------------------------------------------------------
