@@ -177,6 +177,58 @@ def test_render_matches_oracle(S, oracle, stream, mode):
     vol.close()
 
 
+def test_integrate_general_intrinsics(S, oracle, stream):
+    """A K with skew and a non-unit last row (not the pinhole fast path): the general
+    screen map s = M p + m with a separate camera depth row, bit-exact."""
+    st, frames = stream
+    semtsdf, L = S
+    dims = (48, 40, 56)
+    p, vol, g, ost = make(S, oracle, dims, frames[0], 0x3)
+    vol.close()
+    p.K[1] = 2.5     # skew
+    p.K[10] = 1.001  # K[2][2]
+    vol = semtsdf.Volume(p, 0)
+    for k in range(1, 4):
+        fr = frames[k]
+        E = (fr.w2c @ frames[0].c2w).astype(np.float32)
+        vol.integrate(fr.depth, fr.rgb, fr.gt_ids, E)
+        oracle.integrate(g, ost, list(p.K), E, fr.depth, fr.rgb, fr.gt_ids, flags=0x3)
+    assert (ost.wt > 0).sum() > 1000
+    assert_same(vol, ost, hist=True)
+    vol.close()
+
+
+def test_uploaded_volume_raycasts_and_associates(S, oracle, stream):
+    """A volume state integrated by the oracle alone and uploaded through the ABI: the
+    histogram bin mask and the empty-space maps are rebuilt by the upload, so label render
+    and association probabilities match the oracle on it."""
+    st, frames = stream
+    semtsdf, L = S
+    p, vol, g, ost = make(S, oracle, (64, 64, 64), frames[0], 0x3)
+    for k in range(1, 4):
+        fr = frames[k]
+        E = (fr.w2c @ frames[0].c2w).astype(np.float32)
+        oracle.integrate(g, ost, list(p.K), E, fr.depth, fr.rgb, fr.gt_ids, flags=0x3)
+    vol.upload(sdf=ost.sdf, wt=ost.wt, color=ost.color, hist=ost.hist)
+    vol.set_state(3, int(frames[1].gt_ids.max()) + 1)
+    back = vol.download(hist=True)
+    assert np.array_equal(back["hist"], ost.hist)
+    dist = float(np.mean(frames[0].depth[frames[0].depth > 0]) / 5000.0)
+    s2w, c = semtsdf.orbit_camera(list(p.Kinv), 0.1, dist)
+    img, t = vol.raycast(s2w, c, L.RENDER_LABEL, want_t=True)
+    ref, t_ref = oracle.render(g, s2w, c, 640, 480, 0, ost.sdf, ost.hist, ost.color)
+    assert (img == ref).all(axis=-1).mean() >= 0.995
+    assert np.array_equal(t.view(np.uint32), t_ref.view(np.uint32))
+    fr = frames[4]
+    E = (fr.w2c @ frames[0].c2w).astype(np.float32)
+    probs_g, box_g = vol.assoc_probs(E)
+    probs_o, box_o = oracle.march_probs(g, list(p.Kinv), E, 640, 480, ost.sdf, ost.hist, p.box_thresh)
+    assert (probs_o > 0).sum() > 1000  # the scene is actually hit and labelled
+    assert np.array_equal(probs_g.reshape(-1).view(np.uint32), probs_o.view(np.uint32))
+    assert np.array_equal(box_g.reshape(-1), box_o)
+    vol.close()
+
+
 def test_gpu_vs_numpy_reference_golden(S, oracle):
     """GPU integrate (TSDF+colour mode, NumPy rule: i32 colour, ungated) against the
     executed reference block: |dsdf| <= 1e-4 on all but <= 1e-4 of the voxels."""

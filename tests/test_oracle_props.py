@@ -168,3 +168,18 @@ def test_reciprocal_division_is_correctly_rounded(oracle):
     for den in list(range(1, 70)) + rng.integers(70, 4097, 60).tolist():
         a = rng.uniform(-den, den, 20000).astype(np.float32)
         assert oracle.div_rcp_mismatches(a, float(den)) == 0, den
+
+
+def test_colour_mean_reciprocal_floor_is_exact():
+    """k_integrate's u8 colour running mean (avg_u8): floor(RN(num * RN(1/d) + 2^-12)) equals
+    the reference's integer quotient (c*w + x) / (w + 1) (tsdf.cu:57-60) for every c, x in
+    0..255 and every d = w + 1 <= 1024 (the reciprocal table), exhaustively (67M cases).
+    The product num * r is exact in float64, so adding 2^-12 and rounding once to float32
+    is exactly the kernel's fma."""
+    o = np.arange(256, dtype=np.int64)[:, None]
+    x = np.arange(256, dtype=np.int64)[None, :]
+    for den in range(1, 1025):
+        num = (o * (den - 1) + x).ravel()
+        r = np.float64(np.float32(1.0) / np.float32(den))
+        v = (num.astype(np.float64) * r + 2.0 ** -12).astype(np.float32)
+        assert np.array_equal(np.floor(v).astype(np.int64), num // den), den
