@@ -428,11 +428,28 @@ __device__ int unit_cull(const IntegrateArgs& a, int x0, int y0, int lz0) {
     const int v0 = (int)fmaxf(floorf(vmin) - 1.0f, 0.0f);
     const int v1 = (int)fminf(floorf(vmax) + 1.0f, H - 1.0f);
     if (u0 > u1 || v0 > v1) return 1;
-    // max depth over the footprint, on the finest pyramid level with <= 16 tiles
+    // max depth over the footprint, on the finest pyramid level covering it with <= 4x4
+    // tiles: the 16 loads are issued together (predicated), one round trip
     unsigned m = 0;
-    if (((u1 >> 3) - (u0 >> 3) + 1) * ((v1 >> 3) - (v0 >> 3) + 1) <= 16) {
+    const bool fit0 = ((u1 >> 3) - (u0 >> 3)) < 4 && ((v1 >> 3) - (v0 >> 3)) < 4;
+    const bool fit1 = ((u1 >> 5) - (u0 >> 5)) < 4 && ((v1 >> 5) - (v0 >> 5)) < 4;
+    if (!fit0 && ((u1 >> 3) - (u0 >> 3) + 1) * ((v1 >> 3) - (v0 >> 3) + 1) <= 16) {  // thin footprints
         for (int ty = v0 >> 3; ty <= (v1 >> 3); ++ty)
             for (int tx = u0 >> 3; tx <= (u1 >> 3); ++tx) m = max(m, (unsigned)a.pyr.l0[ty * a.pyr.w0 + tx]);
+    } else if (fit0 || fit1) {
+        const int sh = fit0 ? 3 : 5;
+        const uint16_t* lv = fit0 ? a.pyr.l0 : a.pyr.l1;
+        const int wl = fit0 ? a.pyr.w0 : a.pyr.w1;
+        const int tx0 = u0 >> sh, ty0 = v0 >> sh, nx = (u1 >> sh) - tx0, ny = (v1 >> sh) - ty0;
+        unsigned t[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const bool ok = (j & 3) <= nx && (j >> 2) <= ny;
+            t[j] = lv[ok ? (ty0 + (j >> 2)) * wl + tx0 + (j & 3) : 0];
+            t[j] = ok ? t[j] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) m = max(m, t[j]);
     } else if (((u1 >> 5) - (u0 >> 5) + 1) * ((v1 >> 5) - (v0 >> 5) + 1) <= 64) {
         for (int ty = v0 >> 5; ty <= (v1 >> 5); ++ty)
             for (int tx = u0 >> 5; tx <= (u1 >> 5); ++tx) m = max(m, (unsigned)a.pyr.l1[ty * a.pyr.w1 + tx]);
@@ -710,13 +727,17 @@ __device__ __forceinline__ void stage_classify(const IntegrateArgs& a, const Pro
     C.tmask = tmask;
     C.gmask = gmask;
     // histogram mode of the lane: the label of its first gated voxel, shared by all of them?
-    unsigned lab = 0xFFu, same = 1u;
+    C.hlab = 0xFFu;
+    C.hmode = 0u;
+    if (SEM && gmask && a.debug != 6) {  // ~2/3 of the units have no gated lane: skipped
+        unsigned lab = 0xFFu, same = 1u;
 #pragma unroll
-    for (int k = 3; k >= 0; --k) lab = ((gmask >> k) & 1u) ? (C.pix[k] >> 24) : lab;
+        for (int k = 3; k >= 0; --k) lab = ((gmask >> k) & 1u) ? (C.pix[k] >> 24) : lab;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) same &= (((gmask >> k) & 1u) == 0u) | ((C.pix[k] >> 24) == lab);
-    C.hlab = lab;
-    C.hmode = (!SEM || !gmask || a.debug == 6) ? 0u : ((same && lab < (unsigned)kMaxObjects) ? 1u : 2u);
+        for (int k = 0; k < 4; ++k) same &= (((gmask >> k) & 1u) == 0u) | ((C.pix[k] >> 24) == lab);
+        C.hlab = lab;
+        C.hmode = (same && lab < (unsigned)kMaxObjects) ? 1u : 2u;
+    }
 }
 
 // Unconditional loads: a lane with nothing to load reads the dummy line (one 16-B vector
