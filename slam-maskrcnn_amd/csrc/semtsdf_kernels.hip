@@ -1239,6 +1239,42 @@ __device__ __forceinline__ float skip_box_exit(const SkipCursor& cur, const RayV
     return te * (1.0f - 0x1p-16f);
 }
 
+// t += step repeated while t < tend, as the march's single additions would do it, in O(1)
+// per binade of t: inside a binade [2^e, 2^(e+1)) every t is a multiple of its ulp, so
+// RN(t + step) = t + d with the same d = RN_ulp(step) for every t there (unless step is an
+// exact tie between two multiples of the ulp, which takes single steps), and t + n d is
+// exact while it stays below 2^(e+1).  The addition that crosses into the next binade is
+// done singly.  On return t >= tend (or t is unchanged when it already was) and t_prev is
+// the value before the last addition.
+__device__ __forceinline__ void skip_steps(float& t, float& t_prev, float step, float tend) {
+    while (t < tend) {
+        const float t1 = t + step;
+        if (!(t1 < tend)) {  // one more sample ends the run
+            t_prev = t;
+            t = t1;
+            break;
+        }
+        const int eb = __float_as_int(t) & 0x7F800000;
+        const float ulp = __int_as_float(eb - (23 << 23)), top = __int_as_float(eb + (1 << 23));
+        const float d = t1 - t;  // exact (t1 within a factor 2 of t)
+        const float lim = fminf(tend, top);
+        int n = 0;
+        if (fabsf(step - d) * 2.0f != ulp && t1 < top) {
+            n = (int)((lim - t) * __builtin_amdgcn_rcpf(d));  // estimate, fixed up exactly below
+            n = max(n, 1);
+            while (n > 1 && !(t + (float)n * d < lim)) --n;
+            while (t + (float)(n + 1) * d < lim) ++n;
+        }
+        if (n <= 1) {  // a tie, or the next addition leaves the binade: single step
+            t_prev = t;
+            t = t1;
+            continue;
+        }
+        t_prev = t + (float)(n - 1) * d;
+        t = t + (float)n * d;
+    }
+}
+
 __device__ __forceinline__ bool in_skip_box(const SkipCursor& cur, const RayVox& rv, float t) {
     const float ax = fmaf(t, rv.k[0], rv.c[0]), ay = fmaf(t, rv.k[1], rv.c[1]), az = fmaf(t, rv.k[2], rv.c[2]);
     return (ax > cur.lo[0]) & (ax < cur.hi[0]) & (ay > cur.lo[1]) & (ay < cur.hi[1]) & (az > cur.lo[2]) &
@@ -1341,11 +1377,7 @@ __device__ bool march_ray(const VolGeom& g, const VolBufs& b, float ox, float oy
             // the same additions as sample-by-sample stepping (the hit position depends on
             // them), tested against the box's exit parameter, then exactly near the exit
             const float tend = fminf(tfar, skip_box_exit(cur, rv));
-            do {
-                t_prev = t;
-                t += step;
-                if (st) st->skipped++;
-            } while (t < tend);
+            skip_steps(t, t_prev, step, tend);
             while (t < tfar && in_skip_box(cur, rv, t)) {
                 t_prev = t;
                 t += step;
