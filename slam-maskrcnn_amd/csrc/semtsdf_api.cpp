@@ -142,7 +142,7 @@ int check_params(const semtsdf_params* p) {
         if (!(p->voxel[i] > 0.0f) || !std::isfinite(p->voxel[i]))
             return fail(SEMTSDF_ERR_INVALID, "voxel[%d]=%g must be > 0 (place the volume first)", i, p->voxel[i]);
     }
-    if ((int64_t)p->dim[1] * (p->dim[2] + 4) >= (int64_t)1 << 30)  // 32-bit lane offsets of k_integrate
+    if ((int64_t)p->dim[1] * (p->dim[2] + kZAlign) >= (int64_t)1 << 30)  // 32-bit lane offsets of k_integrate
         return fail(SEMTSDF_ERR_INVALID, "dim[1] * dim[2] = %lld too large (< 2^30)", (long long)p->dim[1] * p->dim[2]);
     if (!(p->mu > 0.0f)) return fail(SEMTSDF_ERR_INVALID, "mu=%g must be > 0", p->mu);
     if (p->width <= 0 || p->height <= 0 || (int64_t)p->width * p->height > (1 << 28))
@@ -535,7 +535,7 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     VolGeom& g = v->g;
     g.dimx = p->dim[0]; g.dimy = p->dim[1]; g.dimz = p->dim[2];
     g.lz = lz;
-    g.zs = (lz + 3) & ~3;
+    g.zs = (lz + kZAlign - 1) & ~(kZAlign - 1);  // whole 128-B lines per unit z-row
     g.shard = p->z_shard; g.nshards = p->z_nshards; g.chunk = chunk; g.halo = halo;
     for (int i = 0; i < 3; ++i) { g.start[i] = p->vol_start[i]; g.end[i] = p->vol_end[i]; g.voxel[i] = p->voxel[i]; }
     g.mu = p->mu;

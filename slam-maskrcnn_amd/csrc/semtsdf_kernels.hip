@@ -341,6 +341,7 @@ hipError_t launch_depth_pyramid(const uint16_t* depth, const uint8_t* rgb, const
 constexpr int UX = SEMTSDF_UNIT_X, UY = SEMTSDF_UNIT_Y, UZ = SEMTSDF_UNIT_Z;
 constexpr int LZQ = UZ / 4;  // lanes along z
 static_assert(UX * UY * UZ == 256 && UZ % 4 == 0, "a unit is 64 lanes x 4 z-voxels");
+static_assert(kZAlign % UZ == 0, "unit z-rows are whole lines of the stored column (row_any)");
 __device__ __forceinline__ int lane_zq(int lane) { return lane % LZQ; }
 __device__ __forceinline__ int lane_y(int lane) { return (lane / LZQ) % UY; }
 __device__ __forceinline__ int lane_x(int lane) { return lane / (LZQ * UY); }
@@ -740,6 +741,50 @@ __device__ __forceinline__ void stage_classify(const IntegrateArgs& a, const Pro
     }
 }
 
+#ifndef SEMTSDF_FULLROW
+#define SEMTSDF_FULLROW 1
+#endif
+// Whole-line state traffic: a z-row of the unit (LZQ lanes, one 128-B line of sdf, weight
+// or colour) with any updated lane is loaded and stored by all of its lanes, unchanged
+// values included, so every line written back is fully dirty.
+__device__ __forceinline__ bool row_any(bool p) {
+    if (!SEMTSDF_FULLROW) return p;
+    const uint64_t b = __ballot(p);
+    const int lane = (int)__lane_id();
+    return ((b >> (lane & ~(LZQ - 1))) & ((1ull << LZQ) - 1ull)) != 0ull;
+}
+
+#ifndef SEMTSDF_NT_LOAD
+#define SEMTSDF_NT_LOAD 1
+#endif
+#ifndef SEMTSDF_NT_STORE
+#define SEMTSDF_NT_STORE 1
+#endif
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+// 16-B state accesses (sdf, weight, colour, histogram), optionally non-temporal
+template <class T>
+__device__ __forceinline__ T ld_state(const void* p) {
+    static_assert(sizeof(T) == 16, "16-byte vectors");
+    if (SEMTSDF_NT_LOAD) {
+        const u32x4 r = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+        T t;
+        __builtin_memcpy(&t, &r, 16);
+        return t;
+    }
+    return *reinterpret_cast<const T*>(p);
+}
+template <class T>
+__device__ __forceinline__ void st_state(void* p, const T& v) {
+    static_assert(sizeof(T) == 16, "16-byte vectors");
+    if (SEMTSDF_NT_STORE) {
+        u32x4 r;
+        __builtin_memcpy(&r, &v, 16);
+        __builtin_nontemporal_store(r, reinterpret_cast<u32x4*>(p));
+        return;
+    }
+    *reinterpret_cast<T*>(p) = v;
+}
+
 // Unconditional loads: a lane with nothing to load reads the dummy line (one 16-B vector
 // shared by all such lanes), so the issue count is the same on every path.
 template <bool SEM, bool CI32, bool VOTE>
@@ -751,18 +796,18 @@ __device__ __forceinline__ void stage_load(const IntegrateArgs& a, const UnitPos
     const uint64_t ub = unit_base(g, up);
     const uint64_t v = ub + loff;
     const uint4* dummy = reinterpret_cast<const uint4*>(a.rcp_table);
-    const bool t = C.tmask != 0u, gt = C.gmask != 0u;
+    const bool t = row_any(C.tmask != 0u), gt = row_any(C.gmask != 0u);
     const unsigned lt = t ? loff : 0u, lg = gt ? loff : 0u;
-    L.s4 = *reinterpret_cast<const float4*>(a.b.sdf + ub + lt);
-    L.w4 = *reinterpret_cast<const int4*>(a.b.wt + ub + lt);
+    L.s4 = ld_state<float4>(a.b.sdf + ub + lt);
+    L.w4 = ld_state<int4>(a.b.wt + ub + lt);
     if (CI32) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) L.c32[k] = reinterpret_cast<const int4*>(a.b.color)[ub + lg + (gt ? k : 0)];
     } else {
-        L.c8 = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint32_t*>(a.b.color) + ub + lg);
+        L.c8 = ld_state<uint4>(reinterpret_cast<const uint32_t*>(a.b.color) + ub + lg);
     }
     if (SEM)
-        L.h4 = *(C.hmode == 1u ? reinterpret_cast<const uint4*>(a.b.hist + (uint64_t)C.hlab * g.nvox + v) : dummy);
+        L.h4 = ld_state<uint4>(C.hmode == 1u ? reinterpret_cast<const uint4*>(a.b.hist + (uint64_t)C.hlab * g.nvox + v) : dummy);
     if (VOTE) {
         L.vc4 = *(t ? reinterpret_cast<const int4*>(a.b.cls + v) : reinterpret_cast<const int4*>(dummy));
         L.vn4 = *(t ? reinterpret_cast<const int4*>(a.b.cls_cnt + v) : reinterpret_cast<const int4*>(dummy));
@@ -800,6 +845,12 @@ __device__ __forceinline__ void stage_compute(const IntegrateArgs& a, const floa
     }
     O.s4 = make_float4(sn[0], sn[1], sn[2], sn[3]);
     O.w4 = make_int4(wn[0], wn[1], wn[2], wn[3]);
+    if (CI32) {  // unchanged lines of a stored row
+#pragma unroll
+        for (int k = 0; k < 4; ++k) O.c32[k] = L.c32[k];
+    } else {
+        O.c8 = L.c8;
+    }
     if (gmask) {  // tsdf.cu:57-62
         if (CI32) {
 #pragma unroll
@@ -871,29 +922,30 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
     const VolGeom& g = a.g;
     const unsigned tmask = M.meta & 15u, gmask = (M.meta >> 4) & 15u, hmode = (M.meta >> 8) & 3u,
                    hlab = M.meta >> 16;
-    if (!tmask) return;
+    const bool trow = row_any(tmask != 0u), grow = row_any(gmask != 0u);
+    if (!trow) return;
     const uint64_t ub = unit_base(g, up);
     const uint64_t v = ub + loff;
     if (a.debug != 10) {  // 10: timing probe, loads but no sdf/weight stores
-        *reinterpret_cast<float4*>(a.b.sdf + ub + loff) = O.s4;
-        *reinterpret_cast<int4*>(a.b.wt + ub + loff) = O.w4;
+        st_state(a.b.sdf + ub + loff, O.s4);
+        st_state(a.b.wt + ub + loff, O.w4);
     }
-    if (gmask) {
+    if (grow) {
         if (CI32) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) reinterpret_cast<int4*>(a.b.color)[ub + loff + k] = O.c32[k];
         } else {
-            *reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(a.b.color) + ub + loff) = O.c8;
+            st_state(reinterpret_cast<uint32_t*>(a.b.color) + ub + loff, O.c8);
         }
-        if (SEM) {
+        if (SEM && gmask) {
             if (hmode == 1u) {
-                *reinterpret_cast<uint4*>(a.b.hist + (uint64_t)hlab * g.nvox + v) = O.h4;
+                st_state(a.b.hist + (uint64_t)hlab * g.nvox + v, O.h4);
                 // a count that just became 1 sets the bin's bit in the voxel's bin mask (rare
                 // once the surface has been seen: the common path neither reads nor writes it)
                 const unsigned hk[4] = {O.h4.x, O.h4.y, O.h4.z, O.h4.w};
                 unsigned nb = 0;
 #pragma unroll
-                for (int k = 0; k < 4; ++k) nb |= ((((gmask >> k) & 1u) != 0u) & (hk[k] == 1u) ? 1u : 0u) << k;
+                for (int k = 0; k < 4; ++k) nb |= (((((gmask >> k) & 1u) != 0u) & (hk[k] == 1u)) ? 1u : 0u) << k;
                 if (nb) {
 #pragma unroll
                     for (int k = 0; k < 4; ++k)
@@ -916,7 +968,7 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
             }
         }
     }
-    if (VOTE) {
+    if (VOTE && tmask) {
         *reinterpret_cast<int4*>(a.b.cls + v) = O.vc4;
         *reinterpret_cast<int4*>(a.b.cls_cnt + v) = O.vn4;
     }
@@ -979,7 +1031,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_INT
             const UnitPos nxt = has ? unit_pos(ug, un) : cur;
             un = (i + 2u * nwaves < total) ? entry(i + 2u * nwaves) : 0u;
             stage_project<SHARD, PIN>(a, nxt, lane, P);
-            if (C.tmask) stage_compute<SEM, GATE, CI32, VOTE>(a, s_rcp, C, L, O);  // wave-level skip
+            if (SEMTSDF_FULLROW || C.tmask) stage_compute<SEM, GATE, CI32, VOTE>(a, s_rcp, C, L, O);
             const StoreMeta Mc = store_meta(C);
             stage_classify<SEM, GATE, VOTE, COUNT>(a, P, C, has, n_touch, n_gate);
             stage_store<SEM, CI32, VOTE>(a, cur, loff, Mc, O);

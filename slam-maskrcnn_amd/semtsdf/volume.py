@@ -57,6 +57,11 @@ class DeviceBuffer:
         assert offset + a.nbytes <= self.nbytes
         L.check(L.load().semtsdf_memcpy(C.c_void_p(self.ptr + offset), L.ptr(a), a.nbytes, 1, stream))
 
+    def copy_from(self, src_ptr: int, nbytes: int, stream=None, offset: int = 0):
+        """Device-to-device copy into this buffer (asynchronous on ``stream``)."""
+        assert offset + nbytes <= self.nbytes
+        L.check(L.load().semtsdf_memcpy(C.c_void_p(self.ptr + offset), C.c_void_p(src_ptr), int(nbytes), 3, stream))
+
     def download(self, out: np.ndarray, stream=None, offset: int = 0):
         assert out.flags["C_CONTIGUOUS"] and offset + out.nbytes <= self.nbytes
         L.check(L.load().semtsdf_memcpy(L.ptr(out), C.c_void_p(self.ptr + offset), out.nbytes, 2, stream))
