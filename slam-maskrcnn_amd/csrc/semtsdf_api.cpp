@@ -540,6 +540,9 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     for (int i = 0; i < 3; ++i) { g.start[i] = p->vol_start[i]; g.end[i] = p->vol_end[i]; g.voxel[i] = p->voxel[i]; }
     g.mu = p->mu;
     g.nvox = (uint64_t)g.dimx * (uint64_t)g.dimy * (uint64_t)g.zs;
+    g.nuy = (uint32_t)(g.dimy + 7) / 8;
+    g.nuz = (uint32_t)g.zs / 32;
+    g.ntile = (uint64_t)g.dimx * g.nuy * g.nuz * 256u;
     g.nbx = (g.dimx + 7) / 8; g.nby = (g.dimy + 7) / 8; g.nbz = (g.lz + 7) / 8;
     g.nsx = (g.nbx + 7) / 8; g.nsy = (g.nby + 7) / 8; g.nsz = (g.nbz + 7) / 8;
     for (int i = 0; i < 3; ++i) g.rvox[i] = 1.0f / g.voxel[i];  // IEEE: correctly rounded
@@ -557,10 +560,10 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     if ((rc = dev_alloc(v, (void**)&v->b.sbmin, (size_t)g.nsx * g.nsy * g.nsz * 4))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->b.bdirty, nbricks))) return bail(rc);
     if (nbricks && hipMemset(v->b.bdirty, 0, nbricks) != hipSuccess) return bail(fail(SEMTSDF_ERR_HIP, "memset failed"));
-    if ((rc = dev_alloc(v, &v->b.color, n * 4 * (ci32 ? 4 : 1)))) return bail(rc);
+    if ((rc = dev_alloc(v, &v->b.color, g.ntile * 4 * (ci32 ? 4 : 1)))) return bail(rc);
     if (p->flags & SEMTSDF_F_SEMANTIC)
     {
-        if ((rc = dev_alloc(v, (void**)&v->b.hist, n * kMaxObjects * 4))) return bail(rc);
+        if ((rc = dev_alloc(v, (void**)&v->b.hist, g.ntile * kMaxObjects * 4))) return bail(rc);
         if ((rc = dev_alloc(v, (void**)&v->b.hmask, n * 4))) return bail(rc);
     }
     if (p->flags & SEMTSDF_F_VOTE) {
@@ -650,8 +653,8 @@ int semtsdf_reset(semtsdf_vol* v, void* stream) {
     const size_t n = v->g.nvox;
     HIPC(launch_fill_volume(v->g, v->b, v->p.flags, s));
     HIPC(hipMemsetAsync(v->b.wt, 0, n * 4, s));
-    HIPC(hipMemsetAsync(v->b.color, 0, n * 4 * ((v->p.flags & SEMTSDF_F_COLOR_I32) ? 4 : 1), s));
-    if (v->b.hist) HIPC(hipMemsetAsync(v->b.hist, 0, n * kMaxObjects * 4, s));
+    HIPC(hipMemsetAsync(v->b.color, 0, v->g.ntile * 4 * ((v->p.flags & SEMTSDF_F_COLOR_I32) ? 4 : 1), s));
+    if (v->b.hist) HIPC(hipMemsetAsync(v->b.hist, 0, v->g.ntile * kMaxObjects * 4, s));
     if (v->b.hmask) HIPC(hipMemsetAsync(v->b.hmask, 0, n * 4, s));
     if (v->b.cls) HIPC(hipMemsetAsync(v->b.cls, 0, n * 4, s));
     if (v->b.cls_cnt) HIPC(hipMemsetAsync(v->b.cls_cnt, 0, n * 4, s));

@@ -582,6 +582,12 @@ __device__ __forceinline__ uint64_t unit_base(const VolGeom& g, const UnitPos& u
            (uint64_t)(up.uz * UZ);
 }
 
+// First voxel of the unit in the tiled colour/histogram layout (a unit is one tile).
+__device__ __forceinline__ uint64_t unit_tile(const VolGeom& g, const UnitPos& up) {
+    static_assert(UX == 1 && UY == 8 && UZ == 32, "a unit is one 256-voxel tile (tile_index)");
+    return tile_xterm(g, up.x) + ((uint64_t)up.uy * g.nuz + (uint64_t)up.uz) * 256u;
+}
+
 struct Proj {
     float qz[4];
     uint2 rec[4];  // gathered pixel record {metres bits, rgbl}
@@ -753,6 +759,14 @@ __device__ __forceinline__ bool row_any(bool p) {
     const int lane = (int)__lane_id();
     return ((b >> (lane & ~(LZQ - 1))) & ((1ull << LZQ) - 1ull)) != 0ull;
 }
+// The same for the tiled colour layout: a 128-B line is the 8 lanes of one z-quad (lane % 8).
+__device__ __forceinline__ bool tile_line_any(bool p) {
+    static_assert(LZQ == 8 && UY == 8 && UX == 1, "lane = zq + 8 y");
+    if (!SEMTSDF_FULLROW) return p;
+    const uint64_t b = __ballot(p);
+    const int lane = (int)__lane_id();
+    return ((b >> (lane & 7)) & 0x0101010101010101ull) != 0ull;
+}
 
 #ifndef SEMTSDF_NT_LOAD
 #define SEMTSDF_NT_LOAD 1
@@ -760,12 +774,15 @@ __device__ __forceinline__ bool row_any(bool p) {
 #ifndef SEMTSDF_NT_STORE
 #define SEMTSDF_NT_STORE 1
 #endif
+#ifndef SEMTSDF_NT_HIST
+#define SEMTSDF_NT_HIST 0  // histogram lines are partial (one bin plane per lane): default policy
+#endif
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 // 16-B state accesses (sdf, weight, colour, histogram), optionally non-temporal
-template <class T>
+template <class T, bool NT = SEMTSDF_NT_LOAD>
 __device__ __forceinline__ T ld_state(const void* p) {
     static_assert(sizeof(T) == 16, "16-byte vectors");
-    if (SEMTSDF_NT_LOAD) {
+    if (NT) {
         const u32x4 r = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
         T t;
         __builtin_memcpy(&t, &r, 16);
@@ -773,10 +790,10 @@ __device__ __forceinline__ T ld_state(const void* p) {
     }
     return *reinterpret_cast<const T*>(p);
 }
-template <class T>
+template <class T, bool NT = SEMTSDF_NT_STORE>
 __device__ __forceinline__ void st_state(void* p, const T& v) {
     static_assert(sizeof(T) == 16, "16-byte vectors");
-    if (SEMTSDF_NT_STORE) {
+    if (NT) {
         u32x4 r;
         __builtin_memcpy(&r, &v, 16);
         __builtin_nontemporal_store(r, reinterpret_cast<u32x4*>(p));
@@ -788,26 +805,28 @@ __device__ __forceinline__ void st_state(void* p, const T& v) {
 // Unconditional loads: a lane with nothing to load reads the dummy line (one 16-B vector
 // shared by all such lanes), so the issue count is the same on every path.
 template <bool SEM, bool CI32, bool VOTE>
-__device__ __forceinline__ void stage_load(const IntegrateArgs& a, const UnitPos& up, unsigned loff, const Cls& C,
-                                           Ld& L) {
+__device__ __forceinline__ void stage_load(const IntegrateArgs& a, const UnitPos& up, unsigned loff, unsigned coff,
+                                           const Cls& C, Ld& L) {
     const VolGeom& g = a.g;
     // wave-uniform unit bases (scalar) + the lane's 32-bit element offset; a lane with
     // nothing to load reads the unit's first vector instead (same line for all of them)
     const uint64_t ub = unit_base(g, up);
     const uint64_t v = ub + loff;
     const uint4* dummy = reinterpret_cast<const uint4*>(a.rcp_table);
-    const bool t = row_any(C.tmask != 0u), gt = row_any(C.gmask != 0u);
-    const unsigned lt = t ? loff : 0u, lg = gt ? loff : 0u;
+    const bool t = row_any(C.tmask != 0u), gt = tile_line_any(C.gmask != 0u);
+    const uint64_t ut = unit_tile(g, up);
+    const unsigned lt = t ? loff : 0u, lg = gt ? coff : 0u;
     L.s4 = ld_state<float4>(a.b.sdf + ub + lt);
     L.w4 = ld_state<int4>(a.b.wt + ub + lt);
     if (CI32) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) L.c32[k] = reinterpret_cast<const int4*>(a.b.color)[ub + lg + (gt ? k : 0)];
+        for (int k = 0; k < 4; ++k) L.c32[k] = reinterpret_cast<const int4*>(a.b.color)[ut + lg + (gt ? k : 0)];
     } else {
-        L.c8 = ld_state<uint4>(reinterpret_cast<const uint32_t*>(a.b.color) + ub + lg);
+        L.c8 = ld_state<uint4>(reinterpret_cast<const uint32_t*>(a.b.color) + ut + lg);
     }
     if (SEM)
-        L.h4 = ld_state<uint4>(C.hmode == 1u ? reinterpret_cast<const uint4*>(a.b.hist + (uint64_t)C.hlab * g.nvox + v) : dummy);
+        L.h4 = ld_state<uint4, SEMTSDF_NT_HIST>(C.hmode == 1u ? reinterpret_cast<const uint4*>(a.b.hist + (uint64_t)C.hlab * g.ntile + ut + coff)
+                                             : dummy);
     if (VOTE) {
         L.vc4 = *(t ? reinterpret_cast<const int4*>(a.b.cls + v) : reinterpret_cast<const int4*>(dummy));
         L.vn4 = *(t ? reinterpret_cast<const int4*>(a.b.cls_cnt + v) : reinterpret_cast<const int4*>(dummy));
@@ -917,15 +936,16 @@ __device__ __forceinline__ void stage_compute(const IntegrateArgs& a, const floa
 }
 
 template <bool SEM, bool CI32, bool VOTE>
-__device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPos& up, unsigned loff,
+__device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPos& up, unsigned loff, unsigned coff,
                                             const StoreMeta& M, const Out& O) {
     const VolGeom& g = a.g;
     const unsigned tmask = M.meta & 15u, gmask = (M.meta >> 4) & 15u, hmode = (M.meta >> 8) & 3u,
                    hlab = M.meta >> 16;
-    const bool trow = row_any(tmask != 0u), grow = row_any(gmask != 0u);
+    const bool trow = row_any(tmask != 0u), grow = tile_line_any(gmask != 0u);
     if (!trow) return;
     const uint64_t ub = unit_base(g, up);
     const uint64_t v = ub + loff;
+    const uint64_t vt = unit_tile(g, up) + coff;
     if (a.debug != 10) {  // 10: timing probe, loads but no sdf/weight stores
         st_state(a.b.sdf + ub + loff, O.s4);
         st_state(a.b.wt + ub + loff, O.w4);
@@ -933,13 +953,13 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
     if (grow) {
         if (CI32) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) reinterpret_cast<int4*>(a.b.color)[ub + loff + k] = O.c32[k];
+            for (int k = 0; k < 4; ++k) reinterpret_cast<int4*>(a.b.color)[vt + k] = O.c32[k];
         } else {
-            st_state(reinterpret_cast<uint32_t*>(a.b.color) + ub + loff, O.c8);
+            st_state(reinterpret_cast<uint32_t*>(a.b.color) + vt, O.c8);
         }
         if (SEM && gmask) {
             if (hmode == 1u) {
-                st_state(a.b.hist + (uint64_t)hlab * g.nvox + v, O.h4);
+                st_state<uint4, SEMTSDF_NT_HIST>(a.b.hist + (uint64_t)hlab * g.ntile + vt, O.h4);
                 // a count that just became 1 sets the bin's bit in the voxel's bin mask (rare
                 // once the surface has been seen: the common path neither reads nor writes it)
                 const unsigned hk[4] = {O.h4.x, O.h4.y, O.h4.z, O.h4.w};
@@ -959,7 +979,7 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
                     const unsigned lab = (M.labs >> (8 * k)) & 0xFFu;
                     const bool gk = (gmask >> k) & 1u;
                     if (gk && lab < (unsigned)kMaxObjects) {
-                        atomicAdd(a.b.hist + (uint64_t)lab * g.nvox + v + k, 1u);
+                        atomicAdd(a.b.hist + (uint64_t)lab * g.ntile + vt + k, 1u);
                         atomicOr(a.b.hmask + v + k, 1u << lab);
                     }
                     bad |= (gk && lab >= (unsigned)kMaxObjects) ? 1u : 0u;
@@ -990,6 +1010,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_INT
     // the lane's offset from the unit origin (a volume has < 2^31 stored voxels per x-plane pair)
     const unsigned loff = (unsigned)lane_x(lane) * (unsigned)a.g.dimy * (unsigned)a.g.zs +
                           (unsigned)lane_y(lane) * (unsigned)a.g.zs + (unsigned)lane_zq(lane) * 4u;
+    const unsigned coff = (unsigned)lane_zq(lane) * 32u + (unsigned)lane_y(lane) * 4u;  // tiled colour/histogram
     const unsigned wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     const unsigned nwaves = gridDim.x * (blockDim.x >> 6);
     // segment counts, one per lane; inclusive prefix over the lanes (kListSegs == 64)
@@ -1023,7 +1044,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_INT
         Out O;
         stage_project<SHARD, PIN>(a, cur, lane, P);
         stage_classify<SEM, GATE, VOTE, COUNT>(a, P, C, true, n_touch, n_gate);
-        stage_load<SEM, CI32, VOTE>(a, cur, loff, C, L);
+        stage_load<SEM, CI32, VOTE>(a, cur, loff, coff, C, L);
         while (true) {
             const bool has = i + nwaves < total;
             // the last iteration projects a copy of the current unit, so the memory
@@ -1034,9 +1055,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_INT
             if (SEMTSDF_FULLROW || C.tmask) stage_compute<SEM, GATE, CI32, VOTE>(a, s_rcp, C, L, O);
             const StoreMeta Mc = store_meta(C);
             stage_classify<SEM, GATE, VOTE, COUNT>(a, P, C, has, n_touch, n_gate);
-            stage_store<SEM, CI32, VOTE>(a, cur, loff, Mc, O);
+            stage_store<SEM, CI32, VOTE>(a, cur, loff, coff, Mc, O);
             if (!has) break;
-            stage_load<SEM, CI32, VOTE>(a, nxt, loff, C, L);
+            stage_load<SEM, CI32, VOTE>(a, nxt, loff, coff, C, L);
             cur = nxt;
             i += nwaves;
         }
@@ -1190,6 +1211,28 @@ __device__ __forceinline__ Tri tri_setup(const VolGeom& g, float px, float py, f
     return tri_from(g, tri_coord(g, px, py, pz));
 }
 
+// The same 8 corners in the tiled colour/histogram layout (the index is a sum of per-axis
+// terms, so the corner offsets are differences of those terms).
+__device__ __forceinline__ Tri tri_tile_from(const VolGeom& g, const TriCoord& c) {
+    Tri t;
+    const uint32_t y0 = tile_yterm(g, c.yc), z0 = tile_zterm(c.zl);
+    t.i000 = tile_xterm(g, c.xc) + y0 + z0;
+    t.dx = (uint64_t)c.dxv * ((uint64_t)g.nuy * g.nuz * 256u);
+    t.dy = (uint64_t)(tile_yterm(g, c.yc + c.dyv) - y0);
+    t.dz = tile_zterm(c.zl + c.dzv) - z0;
+    t.fx = c.fx; t.fy = c.fy; t.fz = c.fz;
+    return t;
+}
+
+// A hit's samplers: voxel layout (sdf, bin mask) and tiled layout (colour, histogram).
+struct HitTri {
+    Tri v, t;
+};
+__device__ __forceinline__ HitTri hit_setup(const VolGeom& g, float px, float py, float pz) {
+    const TriCoord c = tri_coord(g, px, py, pz);
+    return HitTri{tri_from(g, c), tri_tile_from(g, c)};
+}
+
 // Empty-space map: brick of 8^3 local voxels holding the sample's 8 corners.
 __device__ __forceinline__ int brick_of(const VolGeom& g, const TriCoord& c) {
     return ((c.xc >> 3) * g.nby + (c.yc >> 3)) * g.nbz + (c.zl >> 3);
@@ -1217,10 +1260,10 @@ __device__ __forceinline__ unsigned tri_bins(const uint32_t* __restrict__ hm, co
 }
 
 // The 32 trilinear histogram values at a sample (utils.cu:144-170).
-__device__ __forceinline__ void tri_hist(const VolGeom& g, const VolBufs& b, const Tri& tr, float* p) {
-    const unsigned bins = tri_bins(b.hmask, tr);
+__device__ __forceinline__ void tri_hist(const VolGeom& g, const VolBufs& b, const HitTri& h, float* p) {
+    const unsigned bins = tri_bins(b.hmask, h.v);
 #pragma unroll
-    for (int k = 0; k < kMaxObjects; ++k) p[k] = ((bins >> k) & 1u) ? tri_eval(b.hist + (uint64_t)k * g.nvox, tr) : 0.0f;
+    for (int k = 0; k < kMaxObjects; ++k) p[k] = ((bins >> k) & 1u) ? tri_eval(b.hist + (uint64_t)k * g.ntile, h.t) : 0.0f;
 }
 
 __device__ __forceinline__ float sample_sdf(const VolGeom& g, const float* sdf, float px, float py, float pz) {
@@ -1642,8 +1685,8 @@ __global__ __launch_bounds__(256) void k_assoc_march(AssocArgs a) {
 #pragma unroll
         for (int k = 0; k < kMaxObjects; ++k) p[k] = 0.0f;
         if (a.debug != 2 && march_ray(a.g, a.b, ox, oy, oz, dx, dy, dz, &t)) {
-            const Tri tr = tri_setup(a.g, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
-            tri_hist(a.g, a.b, tr, p);
+            const HitTri h = hit_setup(a.g, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
+            tri_hist(a.g, a.b, h, p);
         }
         const int px = y * a.width + x;
         if (a.probs_out) {
@@ -1786,16 +1829,17 @@ hipError_t launch_relabel(uint8_t* mask, int npx, const AssocDecision* d, hipStr
 // render raycast (show_tsdf_kernel viewer.cu:17-86; colour mode tsdf_render.frag:125-131)
 // ------------------------------------------------------------------------------------
 // Shade one hit (viewer.cu:66-84 label mode; tsdf_render.frag:125-131 colour mode).
-__device__ __forceinline__ void shade_hit(const VolGeom& g, const VolBufs& vb, const Tri& tr, int mode, int color_i32,
+__device__ __forceinline__ void shade_hit(const VolGeom& g, const VolBufs& vb, const HitTri& h, int mode, int color_i32,
                                           const uint8_t* __restrict__ palette, uint8_t* b, uint8_t* gch, uint8_t* r) {
+    const Tri& tr = h.t;
     if (mode == 0) {
         float max_cnt = 0.0f;
         int obj = 0;
-        unsigned bins = tri_bins(vb.hmask, tr);  // bins outside the mask are 0: never a strict max
+        unsigned bins = tri_bins(vb.hmask, h.v);  // bins outside the mask are 0: never a strict max
         while (bins) {
             const int k = __ffs((int)bins) - 1;
             bins &= bins - 1u;
-            const float c = tri_eval(vb.hist + (uint64_t)k * g.nvox, tr);
+            const float c = tri_eval(vb.hist + (uint64_t)k * g.ntile, tr);
             if (c > max_cnt) { max_cnt = c; obj = k; }
         }
         if (obj > 0) {
@@ -1838,8 +1882,8 @@ __global__ __launch_bounds__(256) void k_render(RenderArgs a) {
     const uint64_t t_start = a.ray_stats ? __builtin_amdgcn_s_memrealtime() : 0;
     if (march_ray(a.g, a.b, ox, oy, oz, dx, dy, dz, &t, a.ray_stats ? &ms : nullptr)) {
         th = t;
-        const Tri tr = tri_setup(a.g, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
-        shade_hit(a.g, a.b, tr, a.mode, a.color_i32, a.palette, &b, &gch, &r);
+        const HitTri h = hit_setup(a.g, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
+        shade_hit(a.g, a.b, h, a.mode, a.color_i32, a.palette, &b, &gch, &r);
     }
     a.out_bgr[(size_t)px * 3 + 0] = b;
     a.out_bgr[(size_t)px * 3 + 1] = gch;
@@ -2048,7 +2092,7 @@ __global__ __launch_bounds__(256) void k_shard_render_final(ShardRayArgs a) {
         const float hx = fmaf(t, r.dx, r.ox), hy = fmaf(t, r.dy, r.oy), hz = fmaf(t, r.dz, r.oz);
         if (sample_owner(a.g, hz) == a.g.shard) {
             uint8_t b = 0, gch = 0, rr = 0;
-            shade_hit(a.g, a.b, tri_setup(a.g, hx, hy, hz), a.kind, a.color_i32, a.palette, &b, &gch, &rr);
+            shade_hit(a.g, a.b, hit_setup(a.g, hx, hy, hz), a.kind, a.color_i32, a.palette, &b, &gch, &rr);
             rec = make_int2(0, (int)((unsigned)b | ((unsigned)gch << 8) | ((unsigned)rr << 16)));
         }
     } else {
@@ -2088,8 +2132,7 @@ __global__ __launch_bounds__(256) void k_shard_assoc_partial(ShardRayArgs a) {
             const float hx = fmaf(t, r.dx, r.ox), hy = fmaf(t, r.dy, r.oy), hz = fmaf(t, r.dz, r.oz);
             mine = sample_owner(a.g, hz) == a.g.shard;
             if (mine) {
-                const Tri tr = tri_setup(a.g, hx, hy, hz);
-                tri_hist(a.g, a.b, tr, p);
+                tri_hist(a.g, a.b, hit_setup(a.g, hx, hy, hz), p);
             }
         } else {
             mine = a.g.shard == 0;  // pixels without a hit contribute once, from shard 0
@@ -2165,11 +2208,28 @@ hipError_t launch_tables_from_partial(const long long* reduced, AssocTables* t, 
 // histogram layout conversion (bin-major device <-> voxel-major reference export)
 // ------------------------------------------------------------------------------------
 // Bin mask of every stored voxel from the bin-major histogram (after an upload).
-__global__ __launch_bounds__(256) void k_hist_mask(const uint32_t* __restrict__ hist, uint32_t* __restrict__ hmask,
-                                                   uint64_t nvox) {
-    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvox; v += (uint64_t)gridDim.x * blockDim.x) {
+// Stored voxel v = (x * dimy + y) * zs + z of the voxel layout -> its tiled index.
+__device__ __forceinline__ uint64_t tile_of_stored(const VolGeom& g, uint64_t v) {
+    const uint64_t row = v / (uint64_t)g.zs;
+    const int z = (int)(v - row * (uint64_t)g.zs);
+    const int x = (int)(row / (uint64_t)g.dimy), y = (int)(row - (uint64_t)x * g.dimy);
+    return tile_index(g, x, y, z);
+}
+
+// Reference voxel v = (x * dimy + y) * lz + z (rows of lz planes) -> its tiled index.
+__device__ __forceinline__ uint64_t tile_of_ref(const VolGeom& g, uint64_t v) {
+    const uint64_t row = v / (uint64_t)g.lz;
+    const int z = (int)(v - row * (uint64_t)g.lz);
+    const int x = (int)(row / (uint64_t)g.dimy), y = (int)(row - (uint64_t)x * g.dimy);
+    return tile_index(g, x, y, z);
+}
+
+__global__ __launch_bounds__(256) void k_hist_mask(VolGeom g, const uint32_t* __restrict__ hist,
+                                                   uint32_t* __restrict__ hmask) {
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < g.nvox; v += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t t = tile_of_stored(g, v);
         unsigned m = 0;
-        for (int k = 0; k < kMaxObjects; ++k) m |= (hist[(uint64_t)k * nvox + v] != 0u ? 1u : 0u) << k;
+        for (int k = 0; k < kMaxObjects; ++k) m |= (hist[(uint64_t)k * g.ntile + t] != 0u ? 1u : 0u) << k;
         hmask[v] = m;
     }
 }
@@ -2178,26 +2238,26 @@ hipError_t launch_hist_mask(const VolGeom& g, const VolBufs& b, hipStream_t s) {
     if (!b.hist || !b.hmask || g.nvox == 0) return hipSuccess;
     uint64_t blocks = (g.nvox + 255) / 256;
     if (blocks > 16384) blocks = 16384;
-    hipLaunchKernelGGL(k_hist_mask, dim3((unsigned)blocks), dim3(256), 0, s, b.hist, b.hmask, g.nvox);
+    hipLaunchKernelGGL(k_hist_mask, dim3((unsigned)blocks), dim3(256), 0, s, g, b.hist, b.hmask);
     return hipGetLastError();
 }
 
-__global__ __launch_bounds__(256) void k_hist_to_vm(const uint32_t* __restrict__ bm, uint32_t* __restrict__ vm,
-                                                    uint64_t nvox, uint32_t lz, uint32_t zs, uint64_t v0, uint64_t nv) {
+__global__ __launch_bounds__(256) void k_hist_to_vm(VolGeom g, const uint32_t* __restrict__ bm, uint32_t* __restrict__ vm,
+                                                    uint64_t v0, uint64_t nv) {
     // vm is a chunk [nv][32] of logical voxels v0 .. v0+nv (rows of lz planes)
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv * kMaxObjects;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t v = v0 + i / kMaxObjects, k = i % kMaxObjects;
-        vm[i] = bm[k * nvox + (v / lz) * zs + v % lz];
+        vm[i] = bm[k * g.ntile + tile_of_ref(g, v)];
     }
 }
 
-__global__ __launch_bounds__(256) void k_hist_to_bm(const uint32_t* __restrict__ vm, uint32_t* __restrict__ bm,
-                                                    uint64_t nvox, uint32_t lz, uint32_t zs, uint64_t v0, uint64_t nv) {
+__global__ __launch_bounds__(256) void k_hist_to_bm(VolGeom g, const uint32_t* __restrict__ vm, uint32_t* __restrict__ bm,
+                                                    uint64_t v0, uint64_t nv) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv * kMaxObjects;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t k = i / nv, v = v0 + i % nv;
-        bm[k * nvox + (v / lz) * zs + v % lz] = vm[(v - v0) * kMaxObjects + k];
+        bm[k * g.ntile + tile_of_ref(g, v)] = vm[(v - v0) * kMaxObjects + k];
     }
 }
 
@@ -2205,8 +2265,7 @@ hipError_t launch_hist_chunk_to_vm(const uint32_t* bm, uint32_t* vm, const VolGe
                                    hipStream_t s) {
     uint64_t blocks = (nv * kMaxObjects + 255) / 256;
     if (blocks > 16384) blocks = 16384;
-    hipLaunchKernelGGL(k_hist_to_vm, dim3((unsigned)blocks), dim3(256), 0, s, bm, vm, g.nvox, (uint32_t)g.lz,
-                       (uint32_t)g.zs, v0, nv);
+    hipLaunchKernelGGL(k_hist_to_vm, dim3((unsigned)blocks), dim3(256), 0, s, g, bm, vm, v0, nv);
     return hipGetLastError();
 }
 
@@ -2214,27 +2273,26 @@ hipError_t launch_hist_chunk_to_bm(const uint32_t* vm, uint32_t* bm, const VolGe
                                    hipStream_t s) {
     uint64_t blocks = (nv * kMaxObjects + 255) / 256;
     if (blocks > 16384) blocks = 16384;
-    hipLaunchKernelGGL(k_hist_to_bm, dim3((unsigned)blocks), dim3(256), 0, s, vm, bm, g.nvox, (uint32_t)g.lz,
-                       (uint32_t)g.zs, v0, nv);
+    hipLaunchKernelGGL(k_hist_to_bm, dim3((unsigned)blocks), dim3(256), 0, s, g, vm, bm, v0, nv);
     return hipGetLastError();
 }
 
 // colour: device storage is padded to 4 channels (u8x4 / i32x4), the reference layout has 3
 template <typename T>
-__global__ __launch_bounds__(256) void k_color_to_ref(const T* __restrict__ dev, T* __restrict__ ref, uint32_t lz,
-                                                      uint32_t zs, uint64_t v0, uint64_t nv) {
+__global__ __launch_bounds__(256) void k_color_to_ref(VolGeom g, const T* __restrict__ dev, T* __restrict__ ref,
+                                                      uint64_t v0, uint64_t nv) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv * 3; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t v = v0 + i / 3, c = i % 3;
-        ref[i] = dev[((v / lz) * zs + v % lz) * 4 + c];
+        ref[i] = dev[tile_of_ref(g, v) * 4 + c];
     }
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void k_color_from_ref(const T* __restrict__ ref, T* __restrict__ dev, uint32_t lz,
-                                                        uint32_t zs, uint64_t v0, uint64_t nv) {
+__global__ __launch_bounds__(256) void k_color_from_ref(VolGeom g, const T* __restrict__ ref, T* __restrict__ dev,
+                                                        uint64_t v0, uint64_t nv) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv * 3; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t v = v0 + i / 3, c = i % 3;
-        dev[((v / lz) * zs + v % lz) * 4 + c] = ref[i];
+        dev[tile_of_ref(g, v) * 4 + c] = ref[i];
     }
 }
 
@@ -2245,18 +2303,14 @@ hipError_t launch_color_chunk(const void* src, void* dst, bool to_ref, bool i32,
     const dim3 gr((unsigned)blocks), bl(256);
     if (i32) {
         if (to_ref)
-            hipLaunchKernelGGL(k_color_to_ref<int32_t>, gr, bl, 0, s, (const int32_t*)src, (int32_t*)dst, (uint32_t)g.lz,
-                               (uint32_t)g.zs, v0, nv);
+            hipLaunchKernelGGL(k_color_to_ref<int32_t>, gr, bl, 0, s, g, (const int32_t*)src, (int32_t*)dst, v0, nv);
         else
-            hipLaunchKernelGGL(k_color_from_ref<int32_t>, gr, bl, 0, s, (const int32_t*)src, (int32_t*)dst,
-                               (uint32_t)g.lz, (uint32_t)g.zs, v0, nv);
+            hipLaunchKernelGGL(k_color_from_ref<int32_t>, gr, bl, 0, s, g, (const int32_t*)src, (int32_t*)dst, v0, nv);
     } else {
         if (to_ref)
-            hipLaunchKernelGGL(k_color_to_ref<uint8_t>, gr, bl, 0, s, (const uint8_t*)src, (uint8_t*)dst, (uint32_t)g.lz,
-                               (uint32_t)g.zs, v0, nv);
+            hipLaunchKernelGGL(k_color_to_ref<uint8_t>, gr, bl, 0, s, g, (const uint8_t*)src, (uint8_t*)dst, v0, nv);
         else
-            hipLaunchKernelGGL(k_color_from_ref<uint8_t>, gr, bl, 0, s, (const uint8_t*)src, (uint8_t*)dst,
-                               (uint32_t)g.lz, (uint32_t)g.zs, v0, nv);
+            hipLaunchKernelGGL(k_color_from_ref<uint8_t>, gr, bl, 0, s, g, (const uint8_t*)src, (uint8_t*)dst, v0, nv);
     }
     return hipGetLastError();
 }
