@@ -535,14 +535,13 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     VolGeom& g = v->g;
     g.dimx = p->dim[0]; g.dimy = p->dim[1]; g.dimz = p->dim[2];
     g.lz = lz;
-    g.zs = (lz + kZAlign - 1) & ~(kZAlign - 1);  // whole 128-B lines per unit z-row
+    g.zs = (lz + kZAlign - 1) & ~(kZAlign - 1);  // whole tiles of 32 planes (tile_index)
     g.shard = p->z_shard; g.nshards = p->z_nshards; g.chunk = chunk; g.halo = halo;
     for (int i = 0; i < 3; ++i) { g.start[i] = p->vol_start[i]; g.end[i] = p->vol_end[i]; g.voxel[i] = p->voxel[i]; }
     g.mu = p->mu;
-    g.nvox = (uint64_t)g.dimx * (uint64_t)g.dimy * (uint64_t)g.zs;
     g.nuy = (uint32_t)(g.dimy + 7) / 8;
     g.nuz = (uint32_t)g.zs / 32;
-    g.ntile = (uint64_t)g.dimx * g.nuy * g.nuz * 256u;
+    g.nvox = (uint64_t)g.dimx * g.nuy * g.nuz * 256u;  // tiled layout (tile_index)
     g.nbx = (g.dimx + 7) / 8; g.nby = (g.dimy + 7) / 8; g.nbz = (g.lz + 7) / 8;
     g.nsx = (g.nbx + 7) / 8; g.nsy = (g.nby + 7) / 8; g.nsz = (g.nbz + 7) / 8;
     for (int i = 0; i < 3; ++i) g.rvox[i] = 1.0f / g.voxel[i];  // IEEE: correctly rounded
@@ -560,10 +559,10 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     if ((rc = dev_alloc(v, (void**)&v->b.sbmin, (size_t)g.nsx * g.nsy * g.nsz * 4))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->b.bdirty, nbricks))) return bail(rc);
     if (nbricks && hipMemset(v->b.bdirty, 0, nbricks) != hipSuccess) return bail(fail(SEMTSDF_ERR_HIP, "memset failed"));
-    if ((rc = dev_alloc(v, &v->b.color, g.ntile * 4 * (ci32 ? 4 : 1)))) return bail(rc);
+    if ((rc = dev_alloc(v, &v->b.color, g.nvox * 4 * (ci32 ? 4 : 1)))) return bail(rc);
     if (p->flags & SEMTSDF_F_SEMANTIC)
     {
-        if ((rc = dev_alloc(v, (void**)&v->b.hist, g.ntile * kMaxObjects * 4))) return bail(rc);
+        if ((rc = dev_alloc(v, (void**)&v->b.hist, g.nvox * kMaxObjects * 4))) return bail(rc);
         if ((rc = dev_alloc(v, (void**)&v->b.hmask, n * 4))) return bail(rc);
     }
     if (p->flags & SEMTSDF_F_VOTE) {
@@ -653,8 +652,8 @@ int semtsdf_reset(semtsdf_vol* v, void* stream) {
     const size_t n = v->g.nvox;
     HIPC(launch_fill_volume(v->g, v->b, v->p.flags, s));
     HIPC(hipMemsetAsync(v->b.wt, 0, n * 4, s));
-    HIPC(hipMemsetAsync(v->b.color, 0, v->g.ntile * 4 * ((v->p.flags & SEMTSDF_F_COLOR_I32) ? 4 : 1), s));
-    if (v->b.hist) HIPC(hipMemsetAsync(v->b.hist, 0, v->g.ntile * kMaxObjects * 4, s));
+    HIPC(hipMemsetAsync(v->b.color, 0, v->g.nvox * 4 * ((v->p.flags & SEMTSDF_F_COLOR_I32) ? 4 : 1), s));
+    if (v->b.hist) HIPC(hipMemsetAsync(v->b.hist, 0, v->g.nvox * kMaxObjects * 4, s));
     if (v->b.hmask) HIPC(hipMemsetAsync(v->b.hmask, 0, n * 4, s));
     if (v->b.cls) HIPC(hipMemsetAsync(v->b.cls, 0, n * 4, s));
     if (v->b.cls_cnt) HIPC(hipMemsetAsync(v->b.cls_cnt, 0, n * 4, s));
@@ -1115,16 +1114,33 @@ int semtsdf_raycast_dev(semtsdf_vol* v, const float s2w[16], const float c[3], i
     return raycast_impl(v, s2w, c, mode, out_bgr_d, out_t_d, pick(v, stream));
 }
 
-// Copy a per-voxel array between the reference layout (rows of lz planes, dense) and the
-// device storage (rows padded to zs planes).  eb = bytes per voxel.
-static hipError_t copy_rows(const semtsdf_vol* v, void* dst, const void* src, size_t eb, bool to_host, hipStream_t s) {
-    const size_t rows = (size_t)v->g.dimx * v->g.dimy;
-    if (v->g.lz == 0) return hipSuccess;
-    const size_t w = (size_t)v->g.lz * eb, pitch_dev = (size_t)v->g.zs * eb;
-    if (v->g.lz == v->g.zs)
-        return hipMemcpyAsync(dst, src, rows * w, to_host ? hipMemcpyDeviceToHost : hipMemcpyHostToDevice, s);
-    if (to_host) return hipMemcpy2DAsync(dst, w, src, pitch_dev, w, rows, hipMemcpyDeviceToHost, s);
-    return hipMemcpy2DAsync(dst, pitch_dev, src, w, w, rows, hipMemcpyHostToDevice, s);
+// A 4-byte per-voxel array between the reference layout (rows of lz planes, dense) and the
+// tiled device storage, chunked through a device staging buffer.
+static int vox_xfer(semtsdf_vol* v, void* host, void* dev, bool to_host, const char* what, hipStream_t s) {
+    const uint64_t n = (uint64_t)v->g.dimx * v->g.dimy * v->g.lz;
+    if (n == 0) return SEMTSDF_OK;
+    const uint64_t chunk = std::min<uint64_t>(n, 1ull << 26);  // <= 256 MiB staging
+    void* stage = nullptr;
+    HIPC(hipMalloc(&stage, chunk * 4));
+    for (uint64_t v0 = 0; v0 < n; v0 += chunk) {
+        const uint64_t nv = std::min<uint64_t>(chunk, n - v0);
+        char* h = static_cast<char*>(host) + v0 * 4;
+        hipError_t e;
+        if (to_host) {
+            e = launch_vox_chunk(dev, stage, true, v->g, v0, nv, s);
+            if (e == hipSuccess) e = hipMemcpyAsync(h, stage, nv * 4, hipMemcpyDeviceToHost, s);
+        } else {
+            e = hipMemcpyAsync(stage, h, nv * 4, hipMemcpyHostToDevice, s);
+            if (e == hipSuccess) e = launch_vox_chunk(stage, dev, false, v->g, v0, nv, s);
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) {
+            (void)hipFree(stage);
+            return fail(SEMTSDF_ERR_HIP, "%s transfer: %s", what, hipGetErrorString(e));
+        }
+    }
+    HIPC(hipFree(stage));
+    return SEMTSDF_OK;
 }
 
 // colour between the padded device layout and the reference [N][3] layout, chunked
@@ -1162,19 +1178,20 @@ int semtsdf_download(semtsdf_vol* v, float* sdf, int32_t* wt, void* color, uint3
     if (!v) return fail(SEMTSDF_ERR_INVALID, "NULL handle");
     HIPC(hipSetDevice(v->device));
     hipStream_t s = v->stream;
-    if (sdf) HIPC(copy_rows(v, sdf, v->b.sdf, 4, true, s));
-    if (wt) HIPC(copy_rows(v, wt, v->b.wt, 4, true, s));
+    int rc;
+    if (sdf && (rc = vox_xfer(v, sdf, v->b.sdf, true, "sdf", s))) return rc;
+    if (wt && (rc = vox_xfer(v, wt, v->b.wt, true, "weight", s))) return rc;
     if (color) {
-        int rc = color_xfer(v, color, true, s);
+        rc = color_xfer(v, color, true, s);
         if (rc) return rc;
     }
     if (cls) {
         if (!(v->p.flags & SEMTSDF_F_VOTE)) return fail(SEMTSDF_ERR_STATE, "not a VOTE volume");
-        HIPC(copy_rows(v, cls, v->b.cls, 4, true, s));
+        if ((rc = vox_xfer(v, cls, v->b.cls, true, "cls", s))) return rc;
     }
     if (cls_cnt) {
         if (!(v->p.flags & SEMTSDF_F_VOTE)) return fail(SEMTSDF_ERR_STATE, "not a VOTE volume");
-        HIPC(copy_rows(v, cls_cnt, v->b.cls_cnt, 4, true, s));
+        if ((rc = vox_xfer(v, cls_cnt, v->b.cls_cnt, true, "cls_cnt", s))) return rc;
     }
     if (hist) {
         if (!(v->p.flags & SEMTSDF_F_SEMANTIC)) return fail(SEMTSDF_ERR_STATE, "not a SEMANTIC volume");
@@ -1204,19 +1221,20 @@ int semtsdf_upload(semtsdf_vol* v, const float* sdf, const int32_t* wt, const vo
     if (!v) return fail(SEMTSDF_ERR_INVALID, "NULL handle");
     HIPC(hipSetDevice(v->device));
     hipStream_t s = v->stream;
-    if (sdf) HIPC(copy_rows(v, v->b.sdf, sdf, 4, false, s));
-    if (wt) HIPC(copy_rows(v, v->b.wt, wt, 4, false, s));
+    int rc;
+    if (sdf && (rc = vox_xfer(v, const_cast<float*>(sdf), v->b.sdf, false, "sdf", s))) return rc;
+    if (wt && (rc = vox_xfer(v, const_cast<int32_t*>(wt), v->b.wt, false, "weight", s))) return rc;
     if (color) {
-        int rc = color_xfer(v, const_cast<void*>(color), false, s);
+        rc = color_xfer(v, const_cast<void*>(color), false, s);
         if (rc) return rc;
     }
     if (cls) {
         if (!(v->p.flags & SEMTSDF_F_VOTE)) return fail(SEMTSDF_ERR_STATE, "not a VOTE volume");
-        HIPC(copy_rows(v, v->b.cls, cls, 4, false, s));
+        if ((rc = vox_xfer(v, const_cast<int32_t*>(cls), v->b.cls, false, "cls", s))) return rc;
     }
     if (cls_cnt) {
         if (!(v->p.flags & SEMTSDF_F_VOTE)) return fail(SEMTSDF_ERR_STATE, "not a VOTE volume");
-        HIPC(copy_rows(v, v->b.cls_cnt, cls_cnt, 4, false, s));
+        if ((rc = vox_xfer(v, const_cast<int32_t*>(cls_cnt), v->b.cls_cnt, false, "cls_cnt", s))) return rc;
     }
     if (hist) {
         if (!(v->p.flags & SEMTSDF_F_SEMANTIC)) return fail(SEMTSDF_ERR_STATE, "not a SEMANTIC volume");

@@ -23,18 +23,18 @@ struct VolGeom {
     float end[3];              // vol_end
     float voxel[3];
     float mu;
-    uint64_t nvox;             // dimx * dimy * zs (stored voxels, padding planes included)
-    uint64_t ntile;            // dimx * nuy * nuz * 256: voxels of the tiled colour/histogram layout
+    uint64_t nvox;             // dimx * nuy * nuz * 256: stored voxels of the tiled layout (padding included)
     uint32_t nuy, nuz;         // 8-row y groups and 32-plane z groups (one 256-voxel tile each)
     int nbx, nby, nbz;         // 8^3 bricks of the local storage (empty-space map)
     int nsx, nsy, nsz;         // 64^3 super-bricks (8^3 bricks each)
     float rvox[3];             // RN(1 / voxel) per axis (exact divisions by the voxel size)
 };
 
-// Tiled layout of the colour and histogram arrays: the 1 x 8 x 32 (x, y, z) block of an
-// integrate unit is 256 consecutive voxels, ordered (z/4, y, z%4): the 4 z-neighbours of a
-// lane are one 16-B vector and 8 y-rows of 4 planes fill one 128-B line, so a thin band of
-// gated voxels reads and writes few lines (z-rows of 32 voxels would cost a line per row).
+// Tiled layout of every per-voxel array: the 1 x 8 x 32 (x, y, z) block of an integrate
+// unit is 256 consecutive voxels, ordered (z/4, y, z%4).  The 4 z-neighbours of a lane are
+// one 16-B vector and 8 y-rows of 4 planes fill one 128-B line, so the ends of a column's
+// updated run and thin bands of gated voxels touch few lines (z-rows of 32 voxels would
+// cost a whole line per row), and a trilinear sample's 8 corners span ~2 lines, not 4.
 __host__ __device__ inline uint64_t tile_xterm(const VolGeom& g, int x) { return (uint64_t)x * g.nuy * g.nuz * 256u; }
 __host__ __device__ inline uint32_t tile_yterm(const VolGeom& g, int y) { return (uint32_t)(y >> 3) * g.nuz * 256u + (uint32_t)(y & 7) * 4u; }
 __host__ __device__ inline uint32_t tile_zterm(int zl) { return (uint32_t)(zl >> 5) * 256u + (uint32_t)((zl >> 2) & 7) * 32u + (uint32_t)(zl & 3); }
@@ -46,8 +46,8 @@ __host__ __device__ inline uint64_t tile_index(const VolGeom& g, int x, int y, i
 struct VolBufs {
     float* sdf;
     int32_t* wt;
-    void* color;       // u8x4 or i32x4 per voxel (3 channels + pad), tiled layout (tile_index)
-    uint32_t* hist;    // bin-major [32][ntile], tiled layout (tile_index)
+    void* color;       // u8x4 or i32x4 per voxel (3 channels + pad)
+    uint32_t* hist;    // bin-major [32][nvox]
     uint32_t* hmask;   // [nvox] bit k set when hist[k][v] > 0 (kept by the integrate; samplers
                        // interpolate only the bins set at one of their 8 corners)
     int32_t* cls;      // vote mode
@@ -203,6 +203,8 @@ hipError_t launch_brick_min(const VolGeom& g, const VolBufs& b, bool all, hipStr
 hipError_t launch_fill_volume(const VolGeom& g, const VolBufs& b, uint32_t flags, hipStream_t s);
 hipError_t launch_depth_pyramid(const uint16_t* depth, const uint8_t* rgb, const uint8_t* mask, int w, int h,
                                 float scale, const DepthPyramid& p, unsigned* list_count, hipStream_t s);
+hipError_t launch_vox_chunk(const void* src, void* dst, bool to_ref, const VolGeom& g, uint64_t v0, uint64_t nv,
+                            hipStream_t s);
 hipError_t launch_color_chunk(const void* src, void* dst, bool to_ref, bool i32, const VolGeom& g, uint64_t v0,
                               uint64_t nv, hipStream_t s);
 hipError_t launch_integrate(const IntegrateArgs& a, hipStream_t s, hipEvent_t e0 = nullptr,

@@ -157,17 +157,18 @@ __global__ __launch_bounds__(256) void k_brick_plain(VolGeom g, const float* __r
     const int x = bx * 8 + (lane >> 3), y = by * 8 + (lane & 7), z0 = bq * 32;
     float m[4] = {3.0e38f, 3.0e38f, 3.0e38f, 3.0e38f};
     if (x < g.dimx && y < g.dimy) {
-        const float* p = sdf + (uint64_t)x * ((uint64_t)g.dimy * g.zs) + (uint64_t)y * g.zs + z0;
+        // the row's 32 planes are the tile's 8 z-quads, 32 floats apart (8 y-lanes = one line)
+        const float* p = sdf + tile_index(g, x, y, z0);
         if (z0 + 32 <= g.lz) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const float4 a = *reinterpret_cast<const float4*>(p + 8 * j);
-                const float4 c = *reinterpret_cast<const float4*>(p + 8 * j + 4);
+                const float4 a = *reinterpret_cast<const float4*>(p + 64 * j);
+                const float4 c = *reinterpret_cast<const float4*>(p + 64 * j + 32);
                 m[j] = fminf(fminf(fminf(a.x, a.y), fminf(a.z, a.w)), fminf(fminf(c.x, c.y), fminf(c.z, c.w)));
             }
         } else {
             for (int k = 0; k < g.lz - z0; ++k) {
-                const float v = p[k];
+                const float v = p[tile_zterm(k)];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) m[j] = (k >> 3) == j ? fminf(m[j], v) : m[j];
             }
@@ -341,7 +342,7 @@ hipError_t launch_depth_pyramid(const uint16_t* depth, const uint8_t* rgb, const
 constexpr int UX = SEMTSDF_UNIT_X, UY = SEMTSDF_UNIT_Y, UZ = SEMTSDF_UNIT_Z;
 constexpr int LZQ = UZ / 4;  // lanes along z
 static_assert(UX * UY * UZ == 256 && UZ % 4 == 0, "a unit is 64 lanes x 4 z-voxels");
-static_assert(kZAlign % UZ == 0, "unit z-rows are whole lines of the stored column (row_any)");
+static_assert(kZAlign % UZ == 0, "the stored z extent is whole tiles");
 __device__ __forceinline__ int lane_zq(int lane) { return lane % LZQ; }
 __device__ __forceinline__ int lane_y(int lane) { return (lane / LZQ) % UY; }
 __device__ __forceinline__ int lane_x(int lane) { return lane / (LZQ * UY); }
@@ -577,12 +578,8 @@ __device__ __forceinline__ UnitPos unit_pos(const UnitGrid& ug, unsigned u) {
     return p;
 }
 
-__device__ __forceinline__ uint64_t unit_base(const VolGeom& g, const UnitPos& up) {
-    return (uint64_t)(up.x * UX) * ((uint64_t)g.dimy * (uint64_t)g.zs) + (uint64_t)(up.uy * UY) * (uint64_t)g.zs +
-           (uint64_t)(up.uz * UZ);
-}
 
-// First voxel of the unit in the tiled colour/histogram layout (a unit is one tile).
+// First voxel of the unit in the tiled layout (a unit is one tile).
 __device__ __forceinline__ uint64_t unit_tile(const VolGeom& g, const UnitPos& up) {
     static_assert(UX == 1 && UY == 8 && UZ == 32, "a unit is one 256-voxel tile (tile_index)");
     return tile_xterm(g, up.x) + ((uint64_t)up.uy * g.nuz + (uint64_t)up.uz) * 256u;
@@ -750,16 +747,9 @@ __device__ __forceinline__ void stage_classify(const IntegrateArgs& a, const Pro
 #ifndef SEMTSDF_FULLROW
 #define SEMTSDF_FULLROW 1
 #endif
-// Whole-line state traffic: a z-row of the unit (LZQ lanes, one 128-B line of sdf, weight
-// or colour) with any updated lane is loaded and stored by all of its lanes, unchanged
-// values included, so every line written back is fully dirty.
-__device__ __forceinline__ bool row_any(bool p) {
-    if (!SEMTSDF_FULLROW) return p;
-    const uint64_t b = __ballot(p);
-    const int lane = (int)__lane_id();
-    return ((b >> (lane & ~(LZQ - 1))) & ((1ull << LZQ) - 1ull)) != 0ull;
-}
-// The same for the tiled colour layout: a 128-B line is the 8 lanes of one z-quad (lane % 8).
+// Whole-line state traffic: a 128-B line of a per-voxel array is the 8 lanes of one
+// z-quad (lane % 8); when any of them updates, all 8 load and store it (unchanged values
+// included), so every line written back is fully dirty.
 __device__ __forceinline__ bool tile_line_any(bool p) {
     static_assert(LZQ == 8 && UY == 8 && UX == 1, "lane = zq + 8 y");
     if (!SEMTSDF_FULLROW) return p;
@@ -805,28 +795,27 @@ __device__ __forceinline__ void st_state(void* p, const T& v) {
 // Unconditional loads: a lane with nothing to load reads the dummy line (one 16-B vector
 // shared by all such lanes), so the issue count is the same on every path.
 template <bool SEM, bool CI32, bool VOTE>
-__device__ __forceinline__ void stage_load(const IntegrateArgs& a, const UnitPos& up, unsigned loff, unsigned coff,
-                                           const Cls& C, Ld& L) {
+__device__ __forceinline__ void stage_load(const IntegrateArgs& a, const UnitPos& up, unsigned coff, const Cls& C,
+                                           Ld& L) {
     const VolGeom& g = a.g;
     // wave-uniform unit bases (scalar) + the lane's 32-bit element offset; a lane with
     // nothing to load reads the unit's first vector instead (same line for all of them)
-    const uint64_t ub = unit_base(g, up);
-    const uint64_t v = ub + loff;
+    const uint64_t ub = unit_tile(g, up);
+    const uint64_t v = ub + coff;
     const uint4* dummy = reinterpret_cast<const uint4*>(a.rcp_table);
-    const bool t = row_any(C.tmask != 0u), gt = tile_line_any(C.gmask != 0u);
-    const uint64_t ut = unit_tile(g, up);
-    const unsigned lt = t ? loff : 0u, lg = gt ? coff : 0u;
+    const bool t = tile_line_any(C.tmask != 0u), gt = tile_line_any(C.gmask != 0u);
+    const unsigned lt = t ? coff : 0u, lg = gt ? coff : 0u;
     L.s4 = ld_state<float4>(a.b.sdf + ub + lt);
     L.w4 = ld_state<int4>(a.b.wt + ub + lt);
     if (CI32) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) L.c32[k] = reinterpret_cast<const int4*>(a.b.color)[ut + lg + (gt ? k : 0)];
+        for (int k = 0; k < 4; ++k) L.c32[k] = reinterpret_cast<const int4*>(a.b.color)[ub + lg + (gt ? k : 0)];
     } else {
-        L.c8 = ld_state<uint4>(reinterpret_cast<const uint32_t*>(a.b.color) + ut + lg);
+        L.c8 = ld_state<uint4>(reinterpret_cast<const uint32_t*>(a.b.color) + ub + lg);
     }
     if (SEM)
-        L.h4 = ld_state<uint4, SEMTSDF_NT_HIST>(C.hmode == 1u ? reinterpret_cast<const uint4*>(a.b.hist + (uint64_t)C.hlab * g.ntile + ut + coff)
-                                             : dummy);
+        L.h4 = ld_state<uint4, SEMTSDF_NT_HIST>(
+            C.hmode == 1u ? reinterpret_cast<const uint4*>(a.b.hist + (uint64_t)C.hlab * g.nvox + v) : dummy);
     if (VOTE) {
         L.vc4 = *(t ? reinterpret_cast<const int4*>(a.b.cls + v) : reinterpret_cast<const int4*>(dummy));
         L.vn4 = *(t ? reinterpret_cast<const int4*>(a.b.cls_cnt + v) : reinterpret_cast<const int4*>(dummy));
@@ -936,30 +925,28 @@ __device__ __forceinline__ void stage_compute(const IntegrateArgs& a, const floa
 }
 
 template <bool SEM, bool CI32, bool VOTE>
-__device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPos& up, unsigned loff, unsigned coff,
+__device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPos& up, unsigned coff,
                                             const StoreMeta& M, const Out& O) {
     const VolGeom& g = a.g;
     const unsigned tmask = M.meta & 15u, gmask = (M.meta >> 4) & 15u, hmode = (M.meta >> 8) & 3u,
                    hlab = M.meta >> 16;
-    const bool trow = row_any(tmask != 0u), grow = tile_line_any(gmask != 0u);
+    const bool trow = tile_line_any(tmask != 0u), grow = tile_line_any(gmask != 0u);
     if (!trow) return;
-    const uint64_t ub = unit_base(g, up);
-    const uint64_t v = ub + loff;
-    const uint64_t vt = unit_tile(g, up) + coff;
+    const uint64_t v = unit_tile(g, up) + coff;
     if (a.debug != 10) {  // 10: timing probe, loads but no sdf/weight stores
-        st_state(a.b.sdf + ub + loff, O.s4);
-        st_state(a.b.wt + ub + loff, O.w4);
+        st_state(a.b.sdf + v, O.s4);
+        st_state(a.b.wt + v, O.w4);
     }
     if (grow) {
         if (CI32) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) reinterpret_cast<int4*>(a.b.color)[vt + k] = O.c32[k];
+            for (int k = 0; k < 4; ++k) reinterpret_cast<int4*>(a.b.color)[v + k] = O.c32[k];
         } else {
-            st_state(reinterpret_cast<uint32_t*>(a.b.color) + vt, O.c8);
+            st_state(reinterpret_cast<uint32_t*>(a.b.color) + v, O.c8);
         }
         if (SEM && gmask) {
             if (hmode == 1u) {
-                st_state<uint4, SEMTSDF_NT_HIST>(a.b.hist + (uint64_t)hlab * g.ntile + vt, O.h4);
+                st_state<uint4, SEMTSDF_NT_HIST>(a.b.hist + (uint64_t)hlab * g.nvox + v, O.h4);
                 // a count that just became 1 sets the bin's bit in the voxel's bin mask (rare
                 // once the surface has been seen: the common path neither reads nor writes it)
                 const unsigned hk[4] = {O.h4.x, O.h4.y, O.h4.z, O.h4.w};
@@ -979,7 +966,7 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
                     const unsigned lab = (M.labs >> (8 * k)) & 0xFFu;
                     const bool gk = (gmask >> k) & 1u;
                     if (gk && lab < (unsigned)kMaxObjects) {
-                        atomicAdd(a.b.hist + (uint64_t)lab * g.ntile + vt + k, 1u);
+                        atomicAdd(a.b.hist + (uint64_t)lab * g.nvox + v + k, 1u);
                         atomicOr(a.b.hmask + v + k, 1u << lab);
                     }
                     bad |= (gk && lab >= (unsigned)kMaxObjects) ? 1u : 0u;
@@ -1008,9 +995,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_INT
     __syncthreads();
     const int lane = threadIdx.x & 63;
     // the lane's offset from the unit origin (a volume has < 2^31 stored voxels per x-plane pair)
-    const unsigned loff = (unsigned)lane_x(lane) * (unsigned)a.g.dimy * (unsigned)a.g.zs +
-                          (unsigned)lane_y(lane) * (unsigned)a.g.zs + (unsigned)lane_zq(lane) * 4u;
-    const unsigned coff = (unsigned)lane_zq(lane) * 32u + (unsigned)lane_y(lane) * 4u;  // tiled colour/histogram
+    const unsigned coff = (unsigned)lane_zq(lane) * 32u + (unsigned)lane_y(lane) * 4u;  // lane's offset in the tile
     const unsigned wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     const unsigned nwaves = gridDim.x * (blockDim.x >> 6);
     // segment counts, one per lane; inclusive prefix over the lanes (kListSegs == 64)
@@ -1044,7 +1029,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_INT
         Out O;
         stage_project<SHARD, PIN>(a, cur, lane, P);
         stage_classify<SEM, GATE, VOTE, COUNT>(a, P, C, true, n_touch, n_gate);
-        stage_load<SEM, CI32, VOTE>(a, cur, loff, coff, C, L);
+        stage_load<SEM, CI32, VOTE>(a, cur, coff, C, L);
         while (true) {
             const bool has = i + nwaves < total;
             // the last iteration projects a copy of the current unit, so the memory
@@ -1055,9 +1040,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_INT
             if (SEMTSDF_FULLROW || C.tmask) stage_compute<SEM, GATE, CI32, VOTE>(a, s_rcp, C, L, O);
             const StoreMeta Mc = store_meta(C);
             stage_classify<SEM, GATE, VOTE, COUNT>(a, P, C, has, n_touch, n_gate);
-            stage_store<SEM, CI32, VOTE>(a, cur, loff, coff, Mc, O);
+            stage_store<SEM, CI32, VOTE>(a, cur, coff, Mc, O);
             if (!has) break;
-            stage_load<SEM, CI32, VOTE>(a, nxt, loff, coff, C, L);
+            stage_load<SEM, CI32, VOTE>(a, nxt, coff, C, L);
             cur = nxt;
             i += nwaves;
         }
@@ -1196,24 +1181,9 @@ __device__ __forceinline__ TriCoord tri_coord(const VolGeom& g, float px, float 
     return c;
 }
 
+// Corner indices in the tiled layout: the index is a sum of per-axis terms, so the
+// offsets to the +1 neighbours are differences of those terms.
 __device__ __forceinline__ Tri tri_from(const VolGeom& g, const TriCoord& c) {
-    Tri t;
-    const uint64_t plane = (uint64_t)g.dimy * (uint64_t)g.zs;
-    t.i000 = (uint64_t)c.xc * plane + (uint64_t)c.yc * g.zs + (uint64_t)c.zl;
-    t.dx = (uint64_t)c.dxv * plane;
-    t.dy = (uint64_t)c.dyv * (uint64_t)g.zs;
-    t.dz = (uint32_t)c.dzv;
-    t.fx = c.fx; t.fy = c.fy; t.fz = c.fz;
-    return t;
-}
-
-__device__ __forceinline__ Tri tri_setup(const VolGeom& g, float px, float py, float pz) {
-    return tri_from(g, tri_coord(g, px, py, pz));
-}
-
-// The same 8 corners in the tiled colour/histogram layout (the index is a sum of per-axis
-// terms, so the corner offsets are differences of those terms).
-__device__ __forceinline__ Tri tri_tile_from(const VolGeom& g, const TriCoord& c) {
     Tri t;
     const uint32_t y0 = tile_yterm(g, c.yc), z0 = tile_zterm(c.zl);
     t.i000 = tile_xterm(g, c.xc) + y0 + z0;
@@ -1224,13 +1194,8 @@ __device__ __forceinline__ Tri tri_tile_from(const VolGeom& g, const TriCoord& c
     return t;
 }
 
-// A hit's samplers: voxel layout (sdf, bin mask) and tiled layout (colour, histogram).
-struct HitTri {
-    Tri v, t;
-};
-__device__ __forceinline__ HitTri hit_setup(const VolGeom& g, float px, float py, float pz) {
-    const TriCoord c = tri_coord(g, px, py, pz);
-    return HitTri{tri_from(g, c), tri_tile_from(g, c)};
+__device__ __forceinline__ Tri tri_setup(const VolGeom& g, float px, float py, float pz) {
+    return tri_from(g, tri_coord(g, px, py, pz));
 }
 
 // Empty-space map: brick of 8^3 local voxels holding the sample's 8 corners.
@@ -1260,10 +1225,10 @@ __device__ __forceinline__ unsigned tri_bins(const uint32_t* __restrict__ hm, co
 }
 
 // The 32 trilinear histogram values at a sample (utils.cu:144-170).
-__device__ __forceinline__ void tri_hist(const VolGeom& g, const VolBufs& b, const HitTri& h, float* p) {
-    const unsigned bins = tri_bins(b.hmask, h.v);
+__device__ __forceinline__ void tri_hist(const VolGeom& g, const VolBufs& b, const Tri& tr, float* p) {
+    const unsigned bins = tri_bins(b.hmask, tr);
 #pragma unroll
-    for (int k = 0; k < kMaxObjects; ++k) p[k] = ((bins >> k) & 1u) ? tri_eval(b.hist + (uint64_t)k * g.ntile, h.t) : 0.0f;
+    for (int k = 0; k < kMaxObjects; ++k) p[k] = ((bins >> k) & 1u) ? tri_eval(b.hist + (uint64_t)k * g.nvox, tr) : 0.0f;
 }
 
 __device__ __forceinline__ float sample_sdf(const VolGeom& g, const float* sdf, float px, float py, float pz) {
@@ -1685,8 +1650,8 @@ __global__ __launch_bounds__(256) void k_assoc_march(AssocArgs a) {
 #pragma unroll
         for (int k = 0; k < kMaxObjects; ++k) p[k] = 0.0f;
         if (a.debug != 2 && march_ray(a.g, a.b, ox, oy, oz, dx, dy, dz, &t)) {
-            const HitTri h = hit_setup(a.g, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
-            tri_hist(a.g, a.b, h, p);
+            const Tri tr = tri_setup(a.g, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
+            tri_hist(a.g, a.b, tr, p);
         }
         const int px = y * a.width + x;
         if (a.probs_out) {
@@ -1829,17 +1794,16 @@ hipError_t launch_relabel(uint8_t* mask, int npx, const AssocDecision* d, hipStr
 // render raycast (show_tsdf_kernel viewer.cu:17-86; colour mode tsdf_render.frag:125-131)
 // ------------------------------------------------------------------------------------
 // Shade one hit (viewer.cu:66-84 label mode; tsdf_render.frag:125-131 colour mode).
-__device__ __forceinline__ void shade_hit(const VolGeom& g, const VolBufs& vb, const HitTri& h, int mode, int color_i32,
+__device__ __forceinline__ void shade_hit(const VolGeom& g, const VolBufs& vb, const Tri& tr, int mode, int color_i32,
                                           const uint8_t* __restrict__ palette, uint8_t* b, uint8_t* gch, uint8_t* r) {
-    const Tri& tr = h.t;
     if (mode == 0) {
         float max_cnt = 0.0f;
         int obj = 0;
-        unsigned bins = tri_bins(vb.hmask, h.v);  // bins outside the mask are 0: never a strict max
+        unsigned bins = tri_bins(vb.hmask, tr);  // bins outside the mask are 0: never a strict max
         while (bins) {
             const int k = __ffs((int)bins) - 1;
             bins &= bins - 1u;
-            const float c = tri_eval(vb.hist + (uint64_t)k * g.ntile, tr);
+            const float c = tri_eval(vb.hist + (uint64_t)k * g.nvox, tr);
             if (c > max_cnt) { max_cnt = c; obj = k; }
         }
         if (obj > 0) {
@@ -1882,8 +1846,8 @@ __global__ __launch_bounds__(256) void k_render(RenderArgs a) {
     const uint64_t t_start = a.ray_stats ? __builtin_amdgcn_s_memrealtime() : 0;
     if (march_ray(a.g, a.b, ox, oy, oz, dx, dy, dz, &t, a.ray_stats ? &ms : nullptr)) {
         th = t;
-        const HitTri h = hit_setup(a.g, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
-        shade_hit(a.g, a.b, h, a.mode, a.color_i32, a.palette, &b, &gch, &r);
+        const Tri tr = tri_setup(a.g, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
+        shade_hit(a.g, a.b, tr, a.mode, a.color_i32, a.palette, &b, &gch, &r);
     }
     a.out_bgr[(size_t)px * 3 + 0] = b;
     a.out_bgr[(size_t)px * 3 + 1] = gch;
@@ -2092,7 +2056,7 @@ __global__ __launch_bounds__(256) void k_shard_render_final(ShardRayArgs a) {
         const float hx = fmaf(t, r.dx, r.ox), hy = fmaf(t, r.dy, r.oy), hz = fmaf(t, r.dz, r.oz);
         if (sample_owner(a.g, hz) == a.g.shard) {
             uint8_t b = 0, gch = 0, rr = 0;
-            shade_hit(a.g, a.b, hit_setup(a.g, hx, hy, hz), a.kind, a.color_i32, a.palette, &b, &gch, &rr);
+            shade_hit(a.g, a.b, tri_setup(a.g, hx, hy, hz), a.kind, a.color_i32, a.palette, &b, &gch, &rr);
             rec = make_int2(0, (int)((unsigned)b | ((unsigned)gch << 8) | ((unsigned)rr << 16)));
         }
     } else {
@@ -2132,7 +2096,7 @@ __global__ __launch_bounds__(256) void k_shard_assoc_partial(ShardRayArgs a) {
             const float hx = fmaf(t, r.dx, r.ox), hy = fmaf(t, r.dy, r.oy), hz = fmaf(t, r.dz, r.oz);
             mine = sample_owner(a.g, hz) == a.g.shard;
             if (mine) {
-                tri_hist(a.g, a.b, hit_setup(a.g, hx, hy, hz), p);
+                tri_hist(a.g, a.b, tri_setup(a.g, hx, hy, hz), p);
             }
         } else {
             mine = a.g.shard == 0;  // pixels without a hit contribute once, from shard 0
@@ -2208,14 +2172,6 @@ hipError_t launch_tables_from_partial(const long long* reduced, AssocTables* t, 
 // histogram layout conversion (bin-major device <-> voxel-major reference export)
 // ------------------------------------------------------------------------------------
 // Bin mask of every stored voxel from the bin-major histogram (after an upload).
-// Stored voxel v = (x * dimy + y) * zs + z of the voxel layout -> its tiled index.
-__device__ __forceinline__ uint64_t tile_of_stored(const VolGeom& g, uint64_t v) {
-    const uint64_t row = v / (uint64_t)g.zs;
-    const int z = (int)(v - row * (uint64_t)g.zs);
-    const int x = (int)(row / (uint64_t)g.dimy), y = (int)(row - (uint64_t)x * g.dimy);
-    return tile_index(g, x, y, z);
-}
-
 // Reference voxel v = (x * dimy + y) * lz + z (rows of lz planes) -> its tiled index.
 __device__ __forceinline__ uint64_t tile_of_ref(const VolGeom& g, uint64_t v) {
     const uint64_t row = v / (uint64_t)g.lz;
@@ -2227,9 +2183,8 @@ __device__ __forceinline__ uint64_t tile_of_ref(const VolGeom& g, uint64_t v) {
 __global__ __launch_bounds__(256) void k_hist_mask(VolGeom g, const uint32_t* __restrict__ hist,
                                                    uint32_t* __restrict__ hmask) {
     for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < g.nvox; v += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t t = tile_of_stored(g, v);
         unsigned m = 0;
-        for (int k = 0; k < kMaxObjects; ++k) m |= (hist[(uint64_t)k * g.ntile + t] != 0u ? 1u : 0u) << k;
+        for (int k = 0; k < kMaxObjects; ++k) m |= (hist[(uint64_t)k * g.nvox + v] != 0u ? 1u : 0u) << k;
         hmask[v] = m;
     }
 }
@@ -2248,7 +2203,7 @@ __global__ __launch_bounds__(256) void k_hist_to_vm(VolGeom g, const uint32_t* _
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv * kMaxObjects;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t v = v0 + i / kMaxObjects, k = i % kMaxObjects;
-        vm[i] = bm[k * g.ntile + tile_of_ref(g, v)];
+        vm[i] = bm[k * g.nvox + tile_of_ref(g, v)];
     }
 }
 
@@ -2257,7 +2212,7 @@ __global__ __launch_bounds__(256) void k_hist_to_bm(VolGeom g, const uint32_t* _
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv * kMaxObjects;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t k = i / nv, v = v0 + i % nv;
-        bm[k * g.ntile + tile_of_ref(g, v)] = vm[(v - v0) * kMaxObjects + k];
+        bm[k * g.nvox + tile_of_ref(g, v)] = vm[(v - v0) * kMaxObjects + k];
     }
 }
 
@@ -2274,6 +2229,31 @@ hipError_t launch_hist_chunk_to_bm(const uint32_t* vm, uint32_t* bm, const VolGe
     uint64_t blocks = (nv * kMaxObjects + 255) / 256;
     if (blocks > 16384) blocks = 16384;
     hipLaunchKernelGGL(k_hist_to_bm, dim3((unsigned)blocks), dim3(256), 0, s, g, vm, bm, v0, nv);
+    return hipGetLastError();
+}
+
+// 4-byte per-voxel arrays (sdf, weight, vote label/count): tiled device <-> reference rows
+__global__ __launch_bounds__(256) void k_vox_to_ref(VolGeom g, const uint32_t* __restrict__ dev, uint32_t* __restrict__ ref,
+                                                    uint64_t v0, uint64_t nv) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (uint64_t)gridDim.x * blockDim.x)
+        ref[i] = dev[tile_of_ref(g, v0 + i)];
+}
+
+__global__ __launch_bounds__(256) void k_vox_from_ref(VolGeom g, const uint32_t* __restrict__ ref, uint32_t* __restrict__ dev,
+                                                      uint64_t v0, uint64_t nv) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (uint64_t)gridDim.x * blockDim.x)
+        dev[tile_of_ref(g, v0 + i)] = ref[i];
+}
+
+hipError_t launch_vox_chunk(const void* src, void* dst, bool to_ref, const VolGeom& g, uint64_t v0, uint64_t nv,
+                            hipStream_t s) {
+    uint64_t blocks = (nv + 255) / 256;
+    if (blocks > 16384) blocks = 16384;
+    if (blocks == 0) return hipSuccess;
+    if (to_ref)
+        hipLaunchKernelGGL(k_vox_to_ref, dim3((unsigned)blocks), dim3(256), 0, s, g, (const uint32_t*)src, (uint32_t*)dst, v0, nv);
+    else
+        hipLaunchKernelGGL(k_vox_from_ref, dim3((unsigned)blocks), dim3(256), 0, s, g, (const uint32_t*)src, (uint32_t*)dst, v0, nv);
     return hipGetLastError();
 }
 
