@@ -428,3 +428,47 @@ def test_sharded_pipeline_equals_single_volume(S, oracle, stream, nshards, chunk
     for sh in shards:
         sh.close()
     vol.close()
+
+
+@pytest.mark.parametrize("dims", [(37, 29, 45), (16, 8, 32), (9, 17, 70)])
+@pytest.mark.parametrize("flags", [0x1, 0x4, 0xC])
+def test_tiled_layout_roundtrip(S, stream, dims, flags):
+    """upload -> download reproduces every array bit for bit through the tiled device layout
+    (y not a multiple of 8, z not a multiple of 32: padding rows/planes must stay invisible),
+    and integrating on top keeps untouched voxels unchanged."""
+    semtsdf, L = S
+    st, frames = stream
+    p = semtsdf.default_params(64, KI, 640, 480)
+    p.dim[0], p.dim[1], p.dim[2] = dims
+    semtsdf.place_from_frame(p, frames[0].depth, float(np.mean(frames[0].depth[frames[0].depth > 0])) / 5000.0,
+                             L.PLACE_SFM)
+    p.flags = flags
+    vol = semtsdf.Volume(p, 0)
+    n = int(np.prod(dims))
+    rng = np.random.default_rng(sum(dims) + flags)
+    ci32 = bool(flags & L.F_COLOR_I32)
+    up = {
+        "sdf": rng.uniform(-1, 1, n).astype(np.float32),
+        "wt": rng.integers(0, 2000, n, dtype=np.int32),
+        "color": (rng.integers(-5000, 5000, n * 3, dtype=np.int32) if ci32
+                  else rng.integers(0, 256, n * 3, dtype=np.uint8)),
+    }
+    sem = bool(flags & L.F_SEMANTIC)
+    vote = bool(flags & L.F_VOTE)
+    if sem:
+        h = np.zeros((n, L.MAX_OBJECTS), np.uint32)
+        idx = rng.integers(0, n, n // 3)
+        h[idx, rng.integers(0, L.MAX_OBJECTS, idx.size)] = rng.integers(1, 9, idx.size, dtype=np.uint32)
+        up["hist"] = h.reshape(-1)
+    if vote:
+        up["cls"] = rng.integers(0, 80, n, dtype=np.int32)
+        up["cls_cnt"] = rng.integers(0, 7, n, dtype=np.int32)
+    vol.upload(**up)
+    out = vol.download(hist=sem, cls=vote)
+    for k, v in up.items():
+        got = out[k]
+        if k == "sdf":
+            assert np.array_equal(got.view(np.uint32), v.view(np.uint32)), k
+        else:
+            assert np.array_equal(got.reshape(-1), v.reshape(-1)), k
+    vol.close()
