@@ -142,8 +142,12 @@ int check_params(const semtsdf_params* p) {
         if (!(p->voxel[i] > 0.0f) || !std::isfinite(p->voxel[i]))
             return fail(SEMTSDF_ERR_INVALID, "voxel[%d]=%g must be > 0 (place the volume first)", i, p->voxel[i]);
     }
-    if ((int64_t)p->dim[1] * (p->dim[2] + kZAlign) >= (int64_t)1 << 30)  // 32-bit lane offsets of k_integrate
-        return fail(SEMTSDF_ERR_INVALID, "dim[1] * dim[2] = %lld too large (< 2^30)", (long long)p->dim[1] * p->dim[2]);
+    {  // 32-bit voxel indices of the tiled layout (tile_index): stored voxels < 2^32, tx < 2^32
+        const uint64_t ny = ((uint64_t)p->dim[1] + 7) / 8 * 8, nz = ((uint64_t)p->dim[2] + 2 * kZAlign) / kZAlign * kZAlign;
+        if ((uint64_t)p->dim[0] * ny * nz >= (1ull << 32) || ny * nz >= (1ull << 32) || nz * 32 >= (1ull << 24))
+            return fail(SEMTSDF_ERR_INVALID, "volume %d x %d x %d too large (2^32 stored voxels or more)", p->dim[0],
+                        p->dim[1], p->dim[2]);
+    }
     if (!(p->mu > 0.0f)) return fail(SEMTSDF_ERR_INVALID, "mu=%g must be > 0", p->mu);
     if (p->width <= 0 || p->height <= 0 || (int64_t)p->width * p->height > (1 << 28))
         return fail(SEMTSDF_ERR_INVALID, "bad frame size %dx%d", p->width, p->height);
@@ -542,6 +546,8 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     g.nuy = (uint32_t)(g.dimy + 7) / 8;
     g.nuz = (uint32_t)g.zs / 32;
     g.nvox = (uint64_t)g.dimx * g.nuy * g.nuz * 256u;  // tiled layout (tile_index)
+    g.ty = g.nuz * 256u;
+    g.tx = g.nuy * g.ty;
     g.nbx = (g.dimx + 7) / 8; g.nby = (g.dimy + 7) / 8; g.nbz = (g.lz + 7) / 8;
     g.nsx = (g.nbx + 7) / 8; g.nsy = (g.nby + 7) / 8; g.nsz = (g.nbz + 7) / 8;
     for (int i = 0; i < 3; ++i) g.rvox[i] = 1.0f / g.voxel[i];  // IEEE: correctly rounded

@@ -25,6 +25,7 @@ struct VolGeom {
     float mu;
     uint64_t nvox;             // dimx * nuy * nuz * 256: stored voxels of the tiled layout (padding included)
     uint32_t nuy, nuz;         // 8-row y groups and 32-plane z groups (one 256-voxel tile each)
+    uint32_t tx, ty;           // tile-index strides of x (nuy * nuz * 256) and of y / 8 (nuz * 256)
     int nbx, nby, nbz;         // 8^3 bricks of the local storage (empty-space map)
     int nsx, nsy, nsz;         // 64^3 super-bricks (8^3 bricks each)
     float rvox[3];             // RN(1 / voxel) per axis (exact divisions by the voxel size)
@@ -35,10 +36,15 @@ struct VolGeom {
 // one 16-B vector and 8 y-rows of 4 planes fill one 128-B line, so the ends of a column's
 // updated run and thin bands of gated voxels touch few lines (z-rows of 32 voxels would
 // cost a whole line per row), and a trilinear sample's 8 corners span ~2 lines, not 4.
-__host__ __device__ inline uint64_t tile_xterm(const VolGeom& g, int x) { return (uint64_t)x * g.nuy * g.nuz * 256u; }
-__host__ __device__ inline uint32_t tile_yterm(const VolGeom& g, int y) { return (uint32_t)(y >> 3) * g.nuz * 256u + (uint32_t)(y & 7) * 4u; }
-__host__ __device__ inline uint32_t tile_zterm(int zl) { return (uint32_t)(zl >> 5) * 256u + (uint32_t)((zl >> 2) & 7) * 32u + (uint32_t)(zl & 3); }
-__host__ __device__ inline uint64_t tile_index(const VolGeom& g, int x, int y, int zl) {
+// Indices are 32-bit (the host rejects volumes of 2^32 stored voxels or more; a histogram
+// plane offset k * nvox is added in 64 bits by the caller).  tx = nuy * nuz * 256 and
+// ty = nuz * 256 < 2^24 (checked at create), so the y term is a full-rate 24-bit product.
+__device__ inline uint32_t tile_xterm(const VolGeom& g, int x) { return (uint32_t)x * g.tx; }
+__device__ inline uint32_t tile_yterm(const VolGeom& g, int y) {
+    return __umul24((uint32_t)(y >> 3), g.ty) + (uint32_t)(y & 7) * 4u;
+}
+__device__ inline uint32_t tile_zterm(int zl) { return (uint32_t)(zl >> 5) * 256u + (uint32_t)((zl >> 2) & 7) * 32u + (uint32_t)(zl & 3); }
+__device__ inline uint32_t tile_index(const VolGeom& g, int x, int y, int zl) {
     return tile_xterm(g, x) + tile_yterm(g, y) + tile_zterm(zl);
 }
 

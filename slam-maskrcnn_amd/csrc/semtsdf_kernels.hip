@@ -582,7 +582,7 @@ __device__ __forceinline__ UnitPos unit_pos(const UnitGrid& ug, unsigned u) {
 // First voxel of the unit in the tiled layout (a unit is one tile).
 __device__ __forceinline__ uint64_t unit_tile(const VolGeom& g, const UnitPos& up) {
     static_assert(UX == 1 && UY == 8 && UZ == 32, "a unit is one 256-voxel tile (tile_index)");
-    return tile_xterm(g, up.x) + ((uint64_t)up.uy * g.nuz + (uint64_t)up.uz) * 256u;
+    return tile_xterm(g, up.x) + __umul24((uint32_t)up.uy, g.ty) + (uint32_t)up.uz * 256u;
 }
 
 struct Proj {
@@ -1147,8 +1147,8 @@ hipError_t launch_integrate(const IntegrateArgs& a, hipStream_t s, hipEvent_t e0
 // range at the far faces; the clamp defines that case).
 // ------------------------------------------------------------------------------------
 struct Tri {
-    uint64_t i000;            // flat index of the base corner
-    uint64_t dx, dy;          // strides to x+1 / y+1 (0 when clamped)
+    uint32_t i000;            // tiled index of the base corner (stored voxels < 2^32)
+    uint32_t dx, dy;          // offsets to x+1 / y+1 (0 when clamped)
     uint32_t dz;
     float fx, fy, fz;
 };
@@ -1187,8 +1187,8 @@ __device__ __forceinline__ Tri tri_from(const VolGeom& g, const TriCoord& c) {
     Tri t;
     const uint32_t y0 = tile_yterm(g, c.yc), z0 = tile_zterm(c.zl);
     t.i000 = tile_xterm(g, c.xc) + y0 + z0;
-    t.dx = (uint64_t)c.dxv * ((uint64_t)g.nuy * g.nuz * 256u);
-    t.dy = (uint64_t)(tile_yterm(g, c.yc + c.dyv) - y0);
+    t.dx = c.dxv ? g.tx : 0u;
+    t.dy = tile_yterm(g, c.yc + c.dyv) - y0;
     t.dz = tile_zterm(c.zl + c.dzv) - z0;
     t.fx = c.fx; t.fy = c.fy; t.fz = c.fz;
     return t;
@@ -1200,7 +1200,8 @@ __device__ __forceinline__ Tri tri_setup(const VolGeom& g, float px, float py, f
 
 // Empty-space map: brick of 8^3 local voxels holding the sample's 8 corners.
 __device__ __forceinline__ int brick_of(const VolGeom& g, const TriCoord& c) {
-    return ((c.xc >> 3) * g.nby + (c.yc >> 3)) * g.nbz + (c.zl >> 3);
+    return (int)__umul24(__umul24((unsigned)(c.xc >> 3), (unsigned)g.nby) + (unsigned)(c.yc >> 3), (unsigned)g.nbz) +
+           (c.zl >> 3);
 }
 
 template <typename T>
@@ -1225,10 +1226,12 @@ __device__ __forceinline__ unsigned tri_bins(const uint32_t* __restrict__ hm, co
 }
 
 // The 32 trilinear histogram values at a sample (utils.cu:144-170).
-__device__ __forceinline__ void tri_hist(const VolGeom& g, const VolBufs& b, const Tri& tr, float* p) {
+// Returns the bins that may be nonzero (the others are 0 in p).
+__device__ __forceinline__ unsigned tri_hist(const VolGeom& g, const VolBufs& b, const Tri& tr, float* p) {
     const unsigned bins = tri_bins(b.hmask, tr);
 #pragma unroll
     for (int k = 0; k < kMaxObjects; ++k) p[k] = ((bins >> k) & 1u) ? tri_eval(b.hist + (uint64_t)k * g.nvox, tr) : 0.0f;
+    return bins;
 }
 
 __device__ __forceinline__ float sample_sdf(const VolGeom& g, const float* sdf, float px, float py, float pz) {
@@ -1271,7 +1274,7 @@ struct SkipCursor {
 // Approximate voxel coordinates of a ray point (|error| ~1e-4 voxel; only used to prove
 // that a sample lies well inside a brick already known to be skippable).
 struct RayVox {
-    float k[3], c[3];
+    float k[3], c[3], rk[3];  // rk = 1 / k (the exit parameter is approximate anyway)
 };
 
 __device__ __forceinline__ RayVox ray_vox(const VolGeom& g, float ox, float oy, float oz, float dx, float dy,
@@ -1281,6 +1284,8 @@ __device__ __forceinline__ RayVox ray_vox(const VolGeom& g, float ox, float oy, 
     r.c[0] = (ox - g.start[0]) * g.rvox[0];
     r.c[1] = (oy - g.start[1]) * g.rvox[1];
     r.c[2] = (oz - g.start[2]) * g.rvox[2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) r.rk[i] = 1.0f / r.k[i];
     return r;
 }
 
@@ -1293,7 +1298,7 @@ __device__ __forceinline__ float skip_box_exit(const SkipCursor& cur, const RayV
     for (int i = 0; i < 3; ++i) {
         const float k = rv.k[i];
         const float bound = k > 0.0f ? cur.hi[i] : cur.lo[i];
-        const float ti = (bound - rv.c[i]) / k;  // k == 0: +-inf or NaN, ignored by fminf / the > test
+        const float ti = (bound - rv.c[i]) * rv.rk[i];  // k == 0: +-inf or NaN, ignored below
         te = (k != 0.0f && ti < te) ? ti : te;
     }
     return te * (1.0f - 0x1p-16f);
@@ -1364,7 +1369,7 @@ __device__ __forceinline__ bool sample_or_skip(const VolGeom& g, const VolBufs& 
     if (b.bmin) {
         if (box && b.sbmin) {  // super-brick level first: one lookup per 64^3 voxels of free space
             const int sx = c.xc >> 6, sy = c.yc >> 6, sz = c.zl >> 6;
-            const int sb = (sx * g.nsy + sy) * g.nsz + sz;
+            const int sb = (int)__umul24(__umul24((unsigned)sx, (unsigned)g.nsy) + (unsigned)sy, (unsigned)g.nsz) + sz;
             if (sb != cur.sb) {
                 cur.sb = sb;
                 cur.sskip = b.sbmin[sb] >= thr;
@@ -1635,11 +1640,42 @@ __device__ __forceinline__ void assoc_accumulate(AssocLds& s, const float* p, un
     }
 }
 
+// The same sums with the bins the sampler found empty folded in: a bin with p[j] == 0 adds
+// F0 = to_fix(logf(eps)) to t1[m][j] (p/n_obs = 0 < eps), so every pixel of label m adds F0
+// to the whole row and the per-pixel work is the few present bins (their to_fix(L) - F0).
+// The row baseline c1[m] * F0 is added when the workgroup flushes its tables; the integer
+// sums are identical.  Requires box_thresh >= 0 (an empty bin is never in the box).
+__device__ __forceinline__ void assoc_accumulate_sparse(AssocLds& s, const float* p, unsigned bins, unsigned m,
+                                                        float n_obs, float eps, float box_thresh, long long F0) {
+    const bool lab = m > 0 && m < (unsigned)kMaxObjects;
+    if (lab) atomicAdd(&s.c1[m], 1u);
+#pragma unroll
+    for (int j = 1; j < kMaxObjects; ++j) {
+        if (!((bins >> j) & 1u) || p[j] == 0.0f) continue;
+        if (lab) {
+            const long long d = to_fix(logf(fmaxf(p[j] / n_obs, eps))) - F0;
+            if (d) atomicAdd(reinterpret_cast<unsigned long long*>(&s.t1[m][j]), (unsigned long long)d);
+        }
+        if (p[j] > box_thresh) {
+            const float L = logf(fmaxf(1.0f - p[j] / n_obs, eps));
+            const unsigned long long f = (unsigned long long)to_fix(L);
+            atomicAdd(reinterpret_cast<unsigned long long*>(&s.t2[j]), f);
+            atomicAdd(&s.c2[j], 1u);
+            if (lab) {
+                atomicAdd(reinterpret_cast<unsigned long long*>(&s.t3[m][j]), f);
+                atomicAdd(&s.c3[m][j], 1u);
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_assoc_march(AssocArgs a) {
     __shared__ AssocLds s;
     const int tid = threadIdx.x;
     assoc_lds_clear(s);
     __syncthreads();
+    const bool sparse = a.box_thresh >= 0.0f && !a.probs_out;  // see assoc_accumulate_sparse
+    const long long F0 = to_fix(logf(fmaxf(0.0f, a.eps)));      // an empty bin's term
 
     const int x = blockIdx.x * 16 + (tid & 15);
     const int y = blockIdx.y * 16 + (tid >> 4);
@@ -1649,9 +1685,10 @@ __global__ __launch_bounds__(256) void k_assoc_march(AssocArgs a) {
         float p[kMaxObjects];
 #pragma unroll
         for (int k = 0; k < kMaxObjects; ++k) p[k] = 0.0f;
+        unsigned bins = 0;
         if (a.debug != 2 && march_ray(a.g, a.b, ox, oy, oz, dx, dy, dz, &t)) {
             const Tri tr = tri_setup(a.g, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
-            tri_hist(a.g, a.b, tr, p);
+            bins = tri_hist(a.g, a.b, tr, p);
         }
         const int px = y * a.width + x;
         if (a.probs_out) {
@@ -1661,12 +1698,18 @@ __global__ __launch_bounds__(256) void k_assoc_march(AssocArgs a) {
                 a.box_out[(size_t)px * kMaxObjects + k] = p[k] > a.box_thresh ? 1 : 0;
             }
         }
-        if (a.debug != 1) assoc_accumulate(s, p, a.mask[px], a.n_obs, a.eps, a.box_thresh);
+        if (a.debug != 1) {
+            if (sparse)
+                assoc_accumulate_sparse(s, p, bins, a.mask[px], a.n_obs, a.eps, a.box_thresh, F0);
+            else
+                assoc_accumulate(s, p, a.mask[px], a.n_obs, a.eps, a.box_thresh);
+        }
     }
     __syncthreads();
     AssocTables* T = a.tables;
     for (int k = tid; k < kMaxObjects * kMaxObjects; k += 256) {
-        const long long v1 = (&s.t1[0][0])[k];
+        const int m = k / kMaxObjects, j = k % kMaxObjects;
+        const long long v1 = (&s.t1[0][0])[k] + ((sparse && m >= 1 && j >= 1) ? (long long)s.c1[m] * F0 : 0ll);
         if (v1) atomicAdd(reinterpret_cast<unsigned long long*>(&T->t1[0][0]) + k, (unsigned long long)v1);
         const long long v3 = (&s.t3[0][0])[k];
         if (v3) atomicAdd(reinterpret_cast<unsigned long long*>(&T->t3[0][0]) + k, (unsigned long long)v3);
@@ -1815,8 +1858,8 @@ __device__ __forceinline__ void shade_hit(const VolGeom& g, const VolBufs& vb, c
         float cc[3];
         for (int ch = 0; ch < 3; ++ch) {
             // colour is stored padded to 4 channels: [v*4 + ch]
-            const uint64_t i000 = tr.i000 * 4 + ch;
-            const uint64_t sx = tr.dx * 4, sy = tr.dy * 4, sz = (uint64_t)tr.dz * 4;
+            const uint64_t i000 = (uint64_t)tr.i000 * 4 + ch;
+            const uint64_t sx = (uint64_t)tr.dx * 4, sy = (uint64_t)tr.dy * 4, sz = (uint64_t)tr.dz * 4;
             float d[8];
             for (int k = 0; k < 8; ++k) {
                 const uint64_t off = ((k & 4) ? sx : 0) + ((k & 2) ? sy : 0) + ((k & 1) ? sz : 0);
