@@ -12,11 +12,11 @@
  * library owns all device memory it allocates.  `stream` arguments are `hipStream_t`
  * passed as `void*` (NULL = the handle's own stream).
  *
- * Volume layout (TSDF_Python tsdf.py:48-52, SfM tsdf.cu:55): flat x-major, z fastest,
- *   idx = x*Dy*Dz + y*Dz + z.  sdf f32, weight i32, colour u8x3 (SfM) or i32x3
- *   (TSDF_Python), histogram 32 x u32 per voxel.  On the device the histogram is kept
- *   bin-major ([32][voxels]) so same-label lanes write coalesced; semtsdf_download()
- *   returns the reference voxel-major [voxels][32] layout.
+ * Volume layout at this boundary (TSDF_Python tsdf.py:48-52, SfM tsdf.cu:55): flat
+ *   x-major, z fastest, idx = x*Dy*Dz + y*Dz + z.  sdf f32, weight i32, colour u8x3 (SfM)
+ *   or i32x3 (TSDF_Python), histogram 32 x u32 per voxel.  The device storage is private:
+ *   1x8x32 tiles of 256 voxels, histogram bin-major;
+ *   semtsdf_download()/semtsdf_upload() convert to and from the reference layouts.
  */
 #ifndef SEMTSDF_H
 #define SEMTSDF_H
