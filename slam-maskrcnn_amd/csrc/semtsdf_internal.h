@@ -10,6 +10,7 @@ namespace semtsdf {
 constexpr int kMaxObjects = 32;
 constexpr int kRcpTable = 1024;  // RN(1/n) table of the running means (w + 1 <= kRcpTable)
 constexpr int kZAlign = 32;      // stored z planes per x,y column: a multiple of the unit z-extent
+constexpr int kBrickDistCap = 8;  // brick distance map: radius of the largest skip box (bricks)
 constexpr int kListSegs = 64;    // segments (and counters) of the live-unit list
 constexpr int kListCountStride = 64;  // counters 256 B apart (separate memory channels)
 
@@ -61,6 +62,9 @@ struct VolBufs {
     float* bmin;       // per 8^3 brick: min sdf over its voxels and the +1 border (ray skipping)
     float* bplain;     // per 8^3 brick: min sdf over its own voxels
     float* sbmin;      // per 64^3 super-brick (8^3 bricks): min of bmin over its bricks
+    uint8_t* bdist;    // per 8^3 brick: L-inf distance in bricks to the nearest non-skippable
+                       // brick (0: not skippable), capped at kBrickDistCap
+    uint8_t* bdtmp;    // scratch of the distance passes
     uint8_t* bdirty;   // per 8^3 brick: overlaps a unit integrated since the last map update
 };
 

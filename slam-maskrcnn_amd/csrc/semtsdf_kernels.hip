@@ -184,7 +184,14 @@ __global__ __launch_bounds__(256) void k_brick_plain(VolGeom g, const float* __r
     }
 }
 
-__global__ __launch_bounds__(256) void k_brick_dilate(VolGeom g, const float* __restrict__ plain, float* __restrict__ bmin) {
+__device__ __forceinline__ float skip_threshold(const VolGeom& g);
+
+#ifndef SEMTSDF_BRICK_DIST
+#define SEMTSDF_BRICK_DIST 1
+#endif
+
+__global__ __launch_bounds__(256) void k_brick_dilate(VolGeom g, const float* __restrict__ plain, float* __restrict__ bmin,
+                                                      uint8_t* __restrict__ d0) {
     const unsigned nb = (unsigned)g.nbx * g.nby * g.nbz;
     const unsigned br = blockIdx.x * blockDim.x + threadIdx.x;
     if (br >= nb) return;
@@ -197,6 +204,28 @@ __global__ __launch_bounds__(256) void k_brick_dilate(VolGeom g, const float* __
                 if (xx < g.nbx && yy < g.nby && zz < g.nbz) m = fminf(m, plain[((unsigned)xx * g.nby + yy) * g.nbz + zz]);
             }
     bmin[br] = m;
+    if (d0) d0[br] = m >= skip_threshold(g) ? (uint8_t)kBrickDistCap : (uint8_t)0;
+}
+
+// Brick distance map, one axis per pass: out[b] = min over |k| < cap of max(|k|, in[b + k e])
+// (neighbours inside the volume).  Three passes (x, y, z) from d0 (0 = not skippable, cap =
+// skippable) give the L-inf distance to the nearest non-skippable brick, capped: every brick
+// closer than d[b] to b is skippable, so the march may step through that whole box.
+__global__ __launch_bounds__(256) void k_brick_dist_axis(VolGeom g, const uint8_t* __restrict__ in,
+                                                         uint8_t* __restrict__ out, int axis) {
+    const unsigned nb = (unsigned)g.nbx * g.nby * g.nbz;
+    const unsigned br = blockIdx.x * blockDim.x + threadIdx.x;
+    if (br >= nb) return;
+    const int bz = br % g.nbz, by = (br / g.nbz) % g.nby, bx = br / (g.nbz * g.nby);
+    const int pos = axis == 0 ? bx : axis == 1 ? by : bz;
+    const int n = axis == 0 ? g.nbx : axis == 1 ? g.nby : g.nbz;
+    const int stride = axis == 0 ? g.nby * g.nbz : axis == 1 ? g.nbz : 1;
+    int d = in[br];
+    for (int k = 1; k < kBrickDistCap && k < d; ++k) {
+        if (pos - k >= 0) d = min(d, max(k, (int)in[(int)br - k * stride]));
+        if (pos + k < n) d = min(d, max(k, (int)in[(int)br + k * stride]));
+    }
+    out[br] = (uint8_t)d;
 }
 
 // Super-brick level: sbmin[s] = min of bmin over the (up to) 8^3 bricks of super-brick s,
@@ -216,14 +245,28 @@ __global__ __launch_bounds__(256) void k_brick_super(VolGeom g, const float* __r
     if (lane == 0) sbmin[sb] = m;
 }
 
+__global__ __launch_bounds__(256) void k_brick_copy_u8(const uint8_t* __restrict__ a, uint8_t* __restrict__ b, unsigned n) {
+    const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) b[i] = a[i];
+}
+
 hipError_t launch_brick_min(const VolGeom& g, const VolBufs& b, bool all, hipStream_t s) {
     const unsigned nb = (unsigned)g.nbx * g.nby * g.nbz;
     if (nb == 0) return hipSuccess;
     const unsigned nq = (unsigned)g.nbx * g.nby * (unsigned)((g.nbz + 3) / 4);
     hipLaunchKernelGGL(k_brick_plain, dim3((nq + 3) / 4), dim3(256), 0, s, g, b.sdf, b.bplain, b.bdirty, all ? 1 : 0);
-    hipLaunchKernelGGL(k_brick_dilate, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.bplain, b.bmin);
-    const unsigned ns = (unsigned)g.nsx * g.nsy * g.nsz;
-    if (b.sbmin && ns) hipLaunchKernelGGL(k_brick_super, dim3((ns + 3) / 4), dim3(256), 0, s, g, b.bmin, b.sbmin);
+    const bool dist = SEMTSDF_BRICK_DIST && b.bdist && b.bdtmp;
+    hipLaunchKernelGGL(k_brick_dilate, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.bplain, b.bmin,
+                       dist ? b.bdist : nullptr);
+    if (dist) {  // bdist -> bdtmp (x) -> bdist (y) -> bdtmp (z) -> copy-free: z pass writes bdist
+        hipLaunchKernelGGL(k_brick_dist_axis, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.bdist, b.bdtmp, 0);
+        hipLaunchKernelGGL(k_brick_dist_axis, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.bdtmp, b.bdist, 1);
+        hipLaunchKernelGGL(k_brick_dist_axis, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.bdist, b.bdtmp, 2);
+        hipLaunchKernelGGL(k_brick_copy_u8, dim3((nb + 255) / 256), dim3(256), 0, s, b.bdtmp, b.bdist, nb);
+    } else {
+        const unsigned ns = (unsigned)g.nsx * g.nsy * g.nsz;
+        if (b.sbmin && ns) hipLaunchKernelGGL(k_brick_super, dim3((ns + 3) / 4), dim3(256), 0, s, g, b.bmin, b.sbmin);
+    }
     return hipGetLastError();
 }
 
@@ -1366,6 +1409,31 @@ __device__ __forceinline__ void skip_box(const VolGeom& g, SkipCursor& cur, int 
 __device__ __forceinline__ bool sample_or_skip(const VolGeom& g, const VolBufs& b, float thr, SkipCursor& cur,
                                                float px, float py, float pz, float* f, bool box = false) {
     const TriCoord c = tri_coord(g, px, py, pz);
+    if (SEMTSDF_BRICK_DIST && box && b.bdist) {
+        // the brick's distance r to the nearest non-skippable brick: the (2r-1)^3 bricks
+        // around it are skippable, one box for the march to step through
+        const int br = brick_of(g, c);
+        if (br != cur.brick) {
+            cur.brick = br;
+            const int r = b.bdist[br];
+            cur.skip = r > 0;
+            if (cur.skip) {
+                const int bx = c.xc >> 3, by = c.yc >> 3, bz = c.zl >> 3;
+                const int x0 = bx - (r - 1), y0 = by - (r - 1), z0 = bz - (r - 1);
+                const int x1 = bx + r, y1 = by + r, z1 = bz + r;  // exclusive
+                const float m = 0.01f;
+                cur.lo[0] = x0 <= 0 ? -1e30f : (float)(x0 * 8) + m;
+                cur.hi[0] = x1 >= g.nbx ? 1e30f : (float)(x1 * 8) - m;
+                cur.lo[1] = y0 <= 0 ? -1e30f : (float)(y0 * 8) + m;
+                cur.hi[1] = y1 >= g.nby ? 1e30f : (float)(y1 * 8) - m;
+                cur.lo[2] = z0 <= 0 ? -1e30f : (float)(z0 * 8) + m;
+                cur.hi[2] = z1 >= g.nbz ? 1e30f : (float)(z1 * 8) - m;
+            }
+        }
+        if (cur.skip) return false;
+        *f = tri_eval(b.sdf, tri_from(g, c));
+        return true;
+    }
     if (b.bmin) {
         if (box && b.sbmin) {  // super-brick level first: one lookup per 64^3 voxels of free space
             const int sx = c.xc >> 6, sy = c.yc >> 6, sz = c.zl >> 6;
