@@ -10,7 +10,10 @@ namespace semtsdf {
 constexpr int kMaxObjects = 32;
 constexpr int kRcpTable = 1024;  // RN(1/n) table of the running means (w + 1 <= kRcpTable)
 constexpr int kZAlign = 32;      // stored z planes per x,y column: a multiple of the unit z-extent
-constexpr int kBrickDistCap = 8;  // brick distance map: radius of the largest skip box (bricks)
+#ifndef SEMTSDF_BRICK_DIST_CAP
+#define SEMTSDF_BRICK_DIST_CAP 8
+#endif
+constexpr int kBrickDistCap = SEMTSDF_BRICK_DIST_CAP;  // brick distance map: radius of the largest skip box (bricks)
 constexpr int kListSegs = 64;    // segments (and counters) of the live-unit list
 constexpr int kListCountStride = 64;  // counters 256 B apart (separate memory channels)
 

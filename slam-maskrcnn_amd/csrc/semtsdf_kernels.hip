@@ -245,11 +245,6 @@ __global__ __launch_bounds__(256) void k_brick_super(VolGeom g, const float* __r
     if (lane == 0) sbmin[sb] = m;
 }
 
-__global__ __launch_bounds__(256) void k_brick_copy_u8(const uint8_t* __restrict__ a, uint8_t* __restrict__ b, unsigned n) {
-    const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) b[i] = a[i];
-}
-
 hipError_t launch_brick_min(const VolGeom& g, const VolBufs& b, bool all, hipStream_t s) {
     const unsigned nb = (unsigned)g.nbx * g.nby * g.nbz;
     if (nb == 0) return hipSuccess;
@@ -257,12 +252,11 @@ hipError_t launch_brick_min(const VolGeom& g, const VolBufs& b, bool all, hipStr
     hipLaunchKernelGGL(k_brick_plain, dim3((nq + 3) / 4), dim3(256), 0, s, g, b.sdf, b.bplain, b.bdirty, all ? 1 : 0);
     const bool dist = SEMTSDF_BRICK_DIST && b.bdist && b.bdtmp;
     hipLaunchKernelGGL(k_brick_dilate, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.bplain, b.bmin,
-                       dist ? b.bdist : nullptr);
-    if (dist) {  // bdist -> bdtmp (x) -> bdist (y) -> bdtmp (z) -> copy-free: z pass writes bdist
-        hipLaunchKernelGGL(k_brick_dist_axis, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.bdist, b.bdtmp, 0);
-        hipLaunchKernelGGL(k_brick_dist_axis, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.bdtmp, b.bdist, 1);
-        hipLaunchKernelGGL(k_brick_dist_axis, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.bdist, b.bdtmp, 2);
-        hipLaunchKernelGGL(k_brick_copy_u8, dim3((nb + 255) / 256), dim3(256), 0, s, b.bdtmp, b.bdist, nb);
+                       dist ? b.bdtmp : nullptr);
+    if (dist) {  // d0 in bdtmp -> x -> bdist -> y -> bdtmp -> z -> bdist
+        hipLaunchKernelGGL(k_brick_dist_axis, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.bdtmp, b.bdist, 0);
+        hipLaunchKernelGGL(k_brick_dist_axis, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.bdist, b.bdtmp, 1);
+        hipLaunchKernelGGL(k_brick_dist_axis, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.bdtmp, b.bdist, 2);
     } else {
         const unsigned ns = (unsigned)g.nsx * g.nsy * g.nsz;
         if (b.sbmin && ns) hipLaunchKernelGGL(k_brick_super, dim3((ns + 3) / 4), dim3(256), 0, s, g, b.bmin, b.sbmin);
