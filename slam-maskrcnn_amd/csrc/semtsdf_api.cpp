@@ -251,6 +251,7 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
     screen_map(a);
     a.pinhole = (a.K[1] == 0.0f && a.K[3] == 0.0f && a.K[6] == 0.0f && a.K[7] == 0.0f && a.K[8] == 1.0f) ? 1 : 0;
     a.rmu = 1.0f / v->g.mu;  // IEEE: the correctly rounded reciprocal
+    a.skip_thr = v->g.voxel[0] / 2.0f * (1.0f + 0x1p-16f);  // = skip_threshold (device), same IEEE ops
     a.fastdiv = (v->g.mu >= 0x1p-20f && v->g.mu <= 0x1p20f && a.debug != 8) ? 1 : 0;
     if (a.debug == 2) return SEMTSDF_OK;
     EventPair epp;

@@ -90,6 +90,7 @@ struct IntegrateArgs {
     float M[9];      // RN(K E[0:3,0:3]) (products summed in double): screen map s = M p + m
     float m[3];      // RN(K E[0:3,3])
     float ftol;      // 0.5 - B 2^-21, B = 2^ceil(log2(max(W, H) + 2)): exactness window of the pixel floor
+    float skip_thr;  // the marches' skip threshold (skip_threshold): a voxel crossing it dirties its brick
     const float* rcp_table;        // [kRcpTable] RN(1/n), n = 1.. (volume constant)
     int width, height;
     float depth_scale;

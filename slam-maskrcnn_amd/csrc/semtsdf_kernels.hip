@@ -135,8 +135,9 @@ hipError_t launch_copy_f4(const void* src, void* dst, size_t n16, hipStream_t s)
 
 // Empty-space map, in two passes.  k_brick_plain: one wave per 8^3 brick (lane = one of
 // its 64 (x, y) rows, two float4 loads) writes the min of sdf over the brick's own voxels;
-// with all == 0 only bricks the cull pass marked dirty (they overlap a live unit, the only
-// voxels an integrate can change) are recomputed.  k_brick_dilate: bmin[b] = min of the
+// with all == 0 only bricks the integrate marked dirty are recomputed (a voxel of theirs
+// crossed the skip threshold, the only change that can flip the map; the stale minima of
+// the other bricks stay on their side of it).  k_brick_dilate: bmin[b] = min of the
 // plain map over b + {0,1}^3, which covers [8b, 8b + 8] per axis: every voxel a trilinear
 // sample based in brick b reads.
 __global__ __launch_bounds__(256) void k_brick_plain(VolGeom g, const float* __restrict__ sdf, float* __restrict__ plain,
@@ -537,15 +538,6 @@ __global__ __launch_bounds__(256) void k_cull_units(IntegrateArgs a, UnitGrid ug
         const int ux = (int)(u % ug.nux), uy = (int)((u / ug.nux) % ug.nuy), uz = (int)(u / (ug.nux * ug.nuy));
         live = a.cull ? !unit_cull(a, ux * UX, uy * UY, uz * UZ) : 1;
         a.unit_flags[u] = (uint8_t)live;
-        if (live && a.b.bdirty) {  // the 8^3 bricks this unit overlaps may change (empty-space map)
-            const VolGeom& g = a.g;
-            const int bx1 = min(ux * UX + UX - 1, g.dimx - 1) >> 3, by1 = min(uy * UY + UY - 1, g.dimy - 1) >> 3;
-            const int bz1 = min(uz * UZ + UZ - 1, g.lz - 1) >> 3;
-            for (int bx = (ux * UX) >> 3; bx <= bx1; ++bx)
-                for (int by = (uy * UY) >> 3; by <= by1; ++by)
-                    for (int bz = (uz * UZ) >> 3; bz <= bz1; ++bz)
-                        a.b.bdirty[((unsigned)bx * (unsigned)g.nby + (unsigned)by) * (unsigned)g.nbz + (unsigned)bz] = 1;
-        }
     }
     const int lane = (int)(threadIdx.x & 63u), wv = (int)(threadIdx.x >> 6);
     const unsigned long long bal = __ballot(live);
@@ -663,6 +655,7 @@ struct Ld {
 struct Out {
     float4 s4;
     int4 w4;
+    bool cross;      // a voxel's sdf crossed the skip threshold (its brick's map entry may flip)
     uint4 c8;
     int4 c32[4];
     uint4 h4;
@@ -890,6 +883,10 @@ __device__ __forceinline__ void stage_compute(const IntegrateArgs& a, const floa
     }
     O.s4 = make_float4(sn[0], sn[1], sn[2], sn[3]);
     O.w4 = make_int4(wn[0], wn[1], wn[2], wn[3]);
+    bool cross = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) cross |= (so[k] < a.skip_thr) != (sn[k] < a.skip_thr);
+    O.cross = cross;
     if (CI32) {  // unchanged lines of a stored row
 #pragma unroll
         for (int k = 0; k < 4; ++k) O.c32[k] = L.c32[k];
@@ -970,6 +967,18 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
     const bool trow = tile_line_any(tmask != 0u), grow = tile_line_any(gmask != 0u);
     if (!trow) return;
     const uint64_t v = unit_tile(g, up) + coff;
+    if (a.b.bdirty) {
+        // a brick of the empty-space map changes only where a voxel crossed the threshold:
+        // z-brick j of the unit holds the lanes of z-quads 2j, 2j+1 (lane = zq + 8 y)
+        const uint64_t cb = __ballot(O.cross);
+        if (cb) {  // rare: most updates keep their side of the threshold
+            const int lane = (int)__lane_id();
+            const int bz = (up.uz * UZ >> 3) + lane;
+            if (lane < UZ / 8 && ((cb >> (2 * lane)) & 0x0303030303030303ull) && bz < g.nbz)
+                a.b.bdirty[__umul24(__umul24((unsigned)(up.x * UX >> 3), (unsigned)g.nby) + (unsigned)(up.uy * UY >> 3),
+                                    (unsigned)g.nbz) + (unsigned)bz] = 1;
+        }
+    }
     if (a.debug != 10) {  // 10: timing probe, loads but no sdf/weight stores
         st_state(a.b.sdf + v, O.s4);
         st_state(a.b.wt + v, O.w4);
