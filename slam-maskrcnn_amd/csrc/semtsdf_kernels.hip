@@ -437,8 +437,11 @@ __device__ int unit_cull(const IntegrateArgs& a, int x0, int y0, int lz0) {
     const int gz1 = min(local_to_global_z(g, min(lz0 + UZ - 1, g.lz - 1)), g.dimz - 1);
     float umin = 3.0e38f, umax = -3.0e38f, vmin = 3.0e38f, vmax = -3.0e38f;
     float zmin = 3.0e38f, zmax = -3.0e38f, wmin = 3.0e38f, wmax = -3.0e38f;
+    // a unit one voxel thick in x has 4 distinct corners
+    constexpr int kCorners = UX == 1 ? 4 : 8;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
+    for (int cc = 0; cc < kCorners; ++cc) {
+        const int c = UX == 1 ? cc << 1 : cc;  // bit 0 selects x1 == x0 when UX == 1
         const float px = fmaf((float)((c & 1) ? x1 : x0), g.voxel[0], g.start[0]);
         const float py = fmaf((float)((c & 2) ? y1 : y0), g.voxel[1], g.start[1]);
         const float pz = fmaf((float)((c & 4) ? gz1 : gz0), g.voxel[2], g.start[2]);
