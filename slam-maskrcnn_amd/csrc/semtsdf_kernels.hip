@@ -364,26 +364,29 @@ hipError_t launch_depth_pyramid(const uint16_t* depth, const uint8_t* rgb, const
 // integrate
 // ------------------------------------------------------------------------------------
 // ---- work decomposition ------------------------------------------------------------
-// Cull unit = UX(x) x UY(y) x UZ(z) = 256 voxels, tested once per frame by one lane of the
-// cull pass against the frustum and the depth pyramid.  Integrate work item = one unit,
-// handled by one wavefront: lane = (zq, y, x) owns planes 4zq..4zq+3 of row (x, y), so
-// every state access is one 16-byte vector per lane and a z-row of the unit is UZ*4 bytes
-// contiguous.  1 x 8 x 32 makes every z-row one whole 128-B line: tighter shapes visit
-// fewer voxels (2 x 8 x 16: 75 % against 63 % of the visited voxels are touched on the
-// synthetic stream) but split lines between units and measured 9 % (2x8x16), 15 %
-// (1x16x16) and 64 % (4x8x8) slower on MI355X.
+// Cull unit = UX(x) x UY(y) x UZ(z) voxels, tested once per frame by one lane of the cull
+// pass against the frustum and the depth pyramid.  A wavefront integrates kSlots units at
+// a time: lane = (slot, y, zq) owns planes 4zq..4zq+3 of row (x, y) of its slot's unit, so
+// every state access is one 16-byte vector per lane and the 8 y-lanes of one z-quad cover
+// one 128-B line of the tiled layout.  Half tiles (1 x 8 x 16, two per wave) visit 16 %
+// fewer voxels than whole tiles (the cull is near exact at unit resolution: 23.5 M against
+// 28.0 M visited voxels per 512^3 frame) and measured 14 % faster; quarter tiles visit 5 %
+// fewer again but the cull of 4x as many units costs more than that saves.
 #ifndef SEMTSDF_UNIT_X
 #define SEMTSDF_UNIT_X 1
 #define SEMTSDF_UNIT_Y 8
-#define SEMTSDF_UNIT_Z 32
+#define SEMTSDF_UNIT_Z 16
 #endif
 constexpr int UX = SEMTSDF_UNIT_X, UY = SEMTSDF_UNIT_Y, UZ = SEMTSDF_UNIT_Z;
-constexpr int LZQ = UZ / 4;  // lanes along z
-static_assert(UX * UY * UZ == 256 && UZ % 4 == 0, "a unit is 64 lanes x 4 z-voxels");
+constexpr int LZQ = UZ / 4;                 // lanes along z
+constexpr int kUnitLanes = UX * UY * UZ / 4;  // lanes of one unit (4 z-voxels each)
+constexpr int kSlots = 64 / kUnitLanes;     // units per wave
+static_assert(kUnitLanes * kSlots == 64 && UZ % 4 == 0, "a wave is kSlots units of 4 z-voxels per lane");
 static_assert(kZAlign % UZ == 0, "the stored z extent is whole tiles");
 __device__ __forceinline__ int lane_zq(int lane) { return lane % LZQ; }
 __device__ __forceinline__ int lane_y(int lane) { return (lane / LZQ) % UY; }
-__device__ __forceinline__ int lane_x(int lane) { return lane / (LZQ * UY); }
+__device__ __forceinline__ int lane_x(int lane) { return (lane / (LZQ * UY)) % UX; }
+__device__ __forceinline__ int lane_slot(int lane) { return lane / kUnitLanes; }
 
 // floor(a / b) with the IEEE quotient, through v_rcp when the result is provably the same:
 // |a*rcp(b) - RN(a/b)| < |q| 2^-20, so a q farther than |q| 2^-19 from an integer floors the
@@ -579,8 +582,8 @@ __device__ __forceinline__ unsigned avg_u8(unsigned c, unsigned x, unsigned w, f
 }
 
 // ---- the integrate of one unit in stages ---------------------------------------------------
-// A unit (UX x UY x UZ voxels) is handled by one wavefront: lane = (zq, y, x) owns planes
-// 4zq..4zq+3 of row (x, y), so every state access is one 16-byte vector per lane.  Stages:
+// kSlots units (UX x UY x UZ voxels each) share a wavefront: lane = (slot, y, zq) owns
+// planes 4zq..4zq+3 of row (x, y) of its unit, one 16-byte vector per state access.  Stages:
 //   project  — screen position, exact pixel, gather of the pixel records (depth, rgb, label)
 //   classify — tsdf.cu:46-52 tests
 //   load     — state of the touched lanes (sdf, weight; colour and histogram words of the
@@ -598,7 +601,8 @@ __device__ __forceinline__ unsigned avg_u8(unsigned c, unsigned x, unsigned w, f
 // voxel within a frame); a lane whose gated voxels carry different labels (object borders)
 // takes no-return atomics.
 struct UnitPos {
-    int x, uy, uz;  // wave-uniform
+    int x, uy, uz;  // per slot of the wave (wave-uniform with one unit per wave)
+    bool ok = true; // false: the slot has no unit this iteration (end of the list)
 };
 
 __device__ __forceinline__ UnitPos unit_pos(const UnitGrid& ug, unsigned u) {
@@ -613,8 +617,9 @@ __device__ __forceinline__ UnitPos unit_pos(const UnitGrid& ug, unsigned u) {
 
 // First voxel of the unit in the tiled layout (a unit is one tile).
 __device__ __forceinline__ uint64_t unit_tile(const VolGeom& g, const UnitPos& up) {
-    static_assert(UX == 1 && UY == 8 && UZ == 32, "a unit is one 256-voxel tile (tile_index)");
-    return tile_xterm(g, up.x) + __umul24((uint32_t)up.uy, g.ty) + (uint32_t)up.uz * 256u;
+    static_assert(UX == 1 && UY == 8 && (UZ == 32 || UZ == 16 || UZ == 8), "a unit is a whole tile or a part of one");
+    const uint32_t z0 = (uint32_t)(up.uz * UZ);  // first plane: a multiple of UZ within its tile
+    return tile_xterm(g, up.x) + __umul24((uint32_t)up.uy, g.ty) + (z0 >> 5) * 256u + ((z0 >> 2) & 7u) * 32u;
 }
 
 struct Proj {
@@ -674,7 +679,7 @@ __device__ __forceinline__ void stage_project(const IntegrateArgs& a, const Unit
     const int x = up.x * UX + lane_x(lane);
     const int y = up.uy * UY + lane_y(lane);
     const int l0 = up.uz * UZ + lane_zq(lane) * 4;
-    const bool row_ok = (x < g.dimx) & (y < g.dimy) & (l0 < g.lz);
+    const bool row_ok = up.ok & (x < g.dimx) & (y < g.dimy) & (l0 < g.lz);
     const float px = fmaf((float)x, g.voxel[0], g.start[0]);
     const float py = fmaf((float)y, g.voxel[1], g.start[1]);
     const float bsx = fmaf(a.M[1], py, fmaf(a.M[0], px, a.m[0]));
@@ -783,12 +788,19 @@ __device__ __forceinline__ void stage_classify(const IntegrateArgs& a, const Pro
 // Whole-line state traffic: a 128-B line of a per-voxel array is the 8 lanes of one
 // z-quad (lane % 8); when any of them updates, all 8 load and store it (unchanged values
 // included), so every line written back is fully dirty.
+constexpr uint64_t line_lanes() {  // lanes of one line of slot 0, z-quad 0: zq + LZQ y
+    uint64_t m = 0;
+    for (int y = 0; y < UY; ++y) m |= 1ull << (LZQ * y);
+    return m;
+}
+constexpr uint64_t kLineLanes = line_lanes();
+
 __device__ __forceinline__ bool tile_line_any(bool p) {
-    static_assert(LZQ == 8 && UY == 8 && UX == 1, "lane = zq + 8 y");
+    static_assert(UY == 8 && UX == 1, "lane = zq + LZQ y + kUnitLanes slot");
     if (!SEMTSDF_FULLROW) return p;
     const uint64_t b = __ballot(p);
     const int lane = (int)__lane_id();
-    return ((b >> (lane & 7)) & 0x0101010101010101ull) != 0ull;
+    return ((b >> (lane % LZQ + lane_slot(lane) * kUnitLanes)) & kLineLanes) != 0ull;
 }
 
 #ifndef SEMTSDF_NT_LOAD
@@ -975,9 +987,12 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
         // z-brick j of the unit holds the lanes of z-quads 2j, 2j+1 (lane = zq + 8 y)
         const uint64_t cb = __ballot(O.cross);
         if (cb) {  // rare: most updates keep their side of the threshold
-            const int lane = (int)__lane_id();
-            const int bz = (up.uz * UZ >> 3) + lane;
-            if (lane < UZ / 8 && ((cb >> (2 * lane)) & 0x0303030303030303ull) && bz < g.nbz)
+            // lane j of a slot marks z-brick j of its unit (z-quads 2j, 2j+1)
+            const int lane = (int)__lane_id(), j = lane % kUnitLanes;
+            const int bz = (up.uz * UZ >> 3) + j;
+            const uint64_t pj = ((kLineLanes << (2 * (j & 3))) | (kLineLanes << (2 * (j & 3) + 1)))
+                                << (lane_slot(lane) * kUnitLanes);
+            if (j < UZ / 8 && (cb & pj) && bz < g.nbz)
                 a.b.bdirty[__umul24(__umul24((unsigned)(up.x * UX >> 3), (unsigned)g.nby) + (unsigned)(up.uy * UY >> 3),
                                     (unsigned)g.nbz) + (unsigned)bz] = 1;
         }
@@ -1044,7 +1059,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_INT
     __syncthreads();
     const int lane = threadIdx.x & 63;
     // the lane's offset from the unit origin (a volume has < 2^31 stored voxels per x-plane pair)
-    const unsigned coff = (unsigned)lane_zq(lane) * 32u + (unsigned)lane_y(lane) * 4u;  // lane's offset in the tile
+    const unsigned coff = (unsigned)lane_zq(lane) * 32u + (unsigned)lane_y(lane) * 4u;  // lane's offset in its unit
     const unsigned wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     const unsigned nwaves = gridDim.x * (blockDim.x >> 6);
     // segment counts, one per lane; inclusive prefix over the lanes (kListSegs == 64)
@@ -1068,10 +1083,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_INT
             (const __attribute__((address_space(4))) unsigned*)a.unit_list;
         return list[seg * seg_cap + off];
     };
+    // group k of the list = entries k*kSlots .. k*kSlots+kSlots-1, one unit per slot of the wave
+    const unsigned ngroups = (total + kSlots - 1) / kSlots;
+    const int slot = lane_slot(lane);
+    auto group_entries = [&](unsigned grp, unsigned* e) {
+#pragma unroll
+        for (int k = 0; k < kSlots; ++k) {
+            const unsigned idx = grp * kSlots + k;
+            e[k] = idx < total ? entry(idx) : ~0u;
+        }
+    };
+    auto lane_pos = [&](const unsigned* e) -> UnitPos {  // the lane's unit (a group's first entry exists)
+        UnitPos p = unit_pos(ug, e[0]);
+#pragma unroll
+        for (int k = 1; k < kSlots; ++k) {
+            const bool have = e[k] != ~0u;
+            const UnitPos q = unit_pos(ug, have ? e[k] : e[0]);
+            if (slot == k) {
+                p = q;
+                p.ok = have;
+            }
+        }
+        return p;
+    };
     unsigned i = wave;
-    if (i < total) {
-        UnitPos cur = unit_pos(ug, entry(i));
-        unsigned un = (i + nwaves < total) ? entry(i + nwaves) : 0u;
+    if (i < ngroups) {
+        unsigned e[kSlots], en[kSlots];
+        group_entries(i, e);
+        UnitPos cur = lane_pos(e);
+        if (i + nwaves < ngroups) group_entries(i + nwaves, en);
         Proj P;
         Cls C;
         Ld L;
@@ -1080,11 +1120,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_INT
         stage_classify<SEM, GATE, VOTE, COUNT>(a, P, C, true, n_touch, n_gate);
         stage_load<SEM, CI32, VOTE>(a, cur, coff, C, L);
         while (true) {
-            const bool has = i + nwaves < total;
-            // the last iteration projects a copy of the current unit, so the memory
+            const bool has = i + nwaves < ngroups;
+            // the last iteration projects a copy of the current units, so the memory
             // operations issued per iteration do not depend on the branch
-            const UnitPos nxt = has ? unit_pos(ug, un) : cur;
-            un = (i + 2u * nwaves < total) ? entry(i + 2u * nwaves) : 0u;
+            const UnitPos nxt = has ? lane_pos(en) : cur;
+            if (i + 2u * nwaves < ngroups) group_entries(i + 2u * nwaves, en);
             stage_project<SHARD, PIN>(a, nxt, lane, P);
             if (SEMTSDF_FULLROW || C.tmask) stage_compute<SEM, GATE, CI32, VOTE>(a, s_rcp, C, L, O);
             const StoreMeta Mc = store_meta(C);
