@@ -187,7 +187,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--dim", type=int, default=512)
     ap.add_argument("--frames", type=int, default=16, help="distinct synthetic frames cycled through")
-    ap.add_argument("--z-chunk", type=int, default=32)
+    ap.add_argument("--z-chunk", type=int, default=63)  # 63 + 1 halo plane = 4 half-tile units per chunk
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true")
     ap.add_argument("--no-cull", action="store_true", help="debug: disable brick culling")
