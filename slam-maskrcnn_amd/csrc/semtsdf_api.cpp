@@ -85,7 +85,6 @@ struct semtsdf_vol {
     uint8_t* render_d = nullptr;
     float* render_t_d = nullptr;
     unsigned long long* counters_d = nullptr;
-    uint8_t* unit_flags_d = nullptr;
     unsigned* unit_list_d = nullptr;  // live units of the frame (cull pass)
     unsigned* list_count_d = nullptr; // [kListSegs * kListCountStride]
     float* rcp_table_d = nullptr;    // RN(1/n), n = 1..kRcpTable
@@ -125,7 +124,7 @@ void free_all(semtsdf_vol* v) {
     void* ptrs[] = {v->b.sdf, v->b.wt, v->b.bmin, v->b.bplain, v->b.sbmin, v->b.bdist, v->b.bdtmp, v->b.bdirty, v->b.color, v->b.hist, v->b.hmask, v->b.cls, v->b.cls_cnt, v->depth_d, v->rgb_d,
                     v->mask_d, v->cls_d, v->pyr.px, v->pyr.l0, v->pyr.l1, v->tables_d, v->decision_d,
                     v->num_objs_d, v->probs_d, v->box_d, v->palette_d, v->render_d, v->render_t_d,
-                    v->counters_d, v->unit_flags_d, v->ray_state_d, v->unit_list_d, v->list_count_d, v->rcp_table_d};
+                    v->counters_d, v->ray_state_d, v->unit_list_d, v->list_count_d, v->rcp_table_d};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (v->decision_h) (void)hipHostFree(v->decision_h);
@@ -244,7 +243,6 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
     a.cls = cls_d;
     a.pyr = v->pyr;
     a.counters = v->counters_d;
-    a.unit_flags = v->unit_flags_d;
     a.unit_list = v->unit_list_d;
     a.list_count = v->list_count_d;
     a.rcp_table = v->rcp_table_d;
@@ -589,7 +587,6 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     if (hipMemset(pyr.px, 0, (px + 1) * 8) != hipSuccess) return bail(fail(SEMTSDF_ERR_HIP, "memset failed"));
     if ((rc = dev_alloc(v, (void**)&pyr.l0, (size_t)pyr.w1 * 4 * pyr.h1 * 4 * 2))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&pyr.l1, (size_t)pyr.w1 * pyr.h1 * 2))) return bail(rc);
-    if ((rc = dev_alloc(v, (void**)&v->unit_flags_d, unit_count(g)))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->unit_list_d, unit_list_capacity(g) * sizeof(unsigned)))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->list_count_d, kListSegs * kListCountStride * sizeof(unsigned)))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->rcp_table_d, kRcpTable * sizeof(float)))) return bail(rc);

@@ -103,7 +103,6 @@ struct IntegrateArgs {
     const uint8_t* mask;    // semantic
     const int32_t* cls;     // vote
     DepthPyramid pyr;
-    uint8_t* unit_flags;           // per cull unit: 1 = may hold a touched voxel (k_cull_units)
     unsigned long long* counters;  // [0] touched, [1] gated, [2] bad-label flag, [3] live bricks
     int pinhole;                   // K rows are (fx 0 cx; 0 fy cy; 0 0 1)
     float rmu;                     // RN(1/mu), for the exact division by mu (k_integrate)

@@ -543,7 +543,6 @@ __global__ __launch_bounds__(256) void k_cull_units(IntegrateArgs a, UnitGrid ug
     if (u < ug.n) {
         const int ux = (int)(u % ug.nux), uy = (int)((u / ug.nux) % ug.nuy), uz = (int)(u / (ug.nux * ug.nuy));
         live = a.cull ? !unit_cull(a, ux * UX, uy * UY, uz * UZ) : 1;
-        a.unit_flags[u] = (uint8_t)live;
     }
     const int lane = (int)(threadIdx.x & 63u), wv = (int)(threadIdx.x >> 6);
     const unsigned long long bal = __ballot(live);

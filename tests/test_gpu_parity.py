@@ -472,3 +472,26 @@ def test_tiled_layout_roundtrip(S, stream, dims, flags):
         else:
             assert np.array_equal(got.reshape(-1), v.reshape(-1)), k
     vol.close()
+
+
+def test_full_size_512_semantic_integrate(S, oracle, stream):
+    """C3 at its full size (512^3, semantic, culling on, 3 frames of the bench's synthetic
+    stream): every array bit-identical to the exhaustive C oracle.  The oracle runs over
+    disjoint x-slabs in threads (ctypes releases the GIL; slabs share no voxel)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    st, frames = stream
+    p, vol, g, ost = make(S, oracle, (512, 512, 512), frames[0], 0x3)
+    slabs = [(x, x + 32) for x in range(0, 512, 32)]
+    touched = 0
+    with ThreadPoolExecutor(8) as ex:
+        for k in range(1, 4):
+            fr = frames[k]
+            E = (fr.w2c @ frames[0].c2w).astype(np.float32)
+            vol.integrate(fr.depth, fr.rgb, fr.gt_ids, E)
+            counts = list(ex.map(lambda r: oracle.integrate(g, ost, list(p.K), E, fr.depth, fr.rgb, fr.gt_ids,
+                                                            flags=0x3, x_range=r), slabs))
+            touched += sum(int(c[0]) for c in counts)
+    assert touched > 10_000_000  # the surface band and free space in front of it are exercised
+    assert_same(vol, ost, hist=True)
+    vol.close()
