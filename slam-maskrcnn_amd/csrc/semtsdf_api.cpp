@@ -208,6 +208,25 @@ void screen_map(IntegrateArgs& a) {
                            (double)a.K[i * 3 + 2] * (double)a.E[11];
         a.m[i] = (float)acc;
     }
+    // cull map: s(x, y, gz) = K (E3 (start + voxel * (x, y, gz)) + t), in double, rounded once
+    double KE[4][4];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            if (i == 3) {
+                KE[i][j] = (double)a.E[2 * 4 + j];  // qz = E row 2
+                continue;
+            }
+            KE[i][j] = (double)a.K[i * 3 + 0] * (double)a.E[0 * 4 + j] + (double)a.K[i * 3 + 1] * (double)a.E[1 * 4 + j] +
+                       (double)a.K[i * 3 + 2] * (double)a.E[2 * 4 + j];
+        }
+    for (int i = 0; i < 4; ++i) {
+        double c0 = KE[i][3];
+        for (int j = 0; j < 3; ++j) {
+            a.cullC[i * 4 + j] = (float)(KE[i][j] * (double)a.g.voxel[j]);
+            c0 += KE[i][j] * (double)a.g.start[j];
+        }
+        a.cullC[i * 4 + 3] = (float)c0;
+    }
     int b = 1;
     while (b < (a.width > a.height ? a.width : a.height) + 2) b <<= 1;
     a.ftol = 0.5f - ldexpf((float)b, -21);

@@ -89,6 +89,8 @@ struct IntegrateArgs {
     float K[9];      // rows 0..2, cols 0..2 of the intrinsic
     float M[9];      // RN(K E[0:3,0:3]) (products summed in double): screen map s = M p + m
     float m[3];      // RN(K E[0:3,3])
+    float cullC[16]; // cull only (conservative, not the contract): rows sx, sy, sz, qz as affine
+                     // functions (cx, cy, cz, c0) of the global voxel index (x, y, gz)
     float ftol;      // 0.5 - B 2^-21, B = 2^ceil(log2(max(W, H) + 2)): exactness window of the pixel floor
     float skip_thr;  // the marches' skip threshold (skip_threshold): a voxel crossing it dirties its brick
     const float* rcp_table;        // [kRcpTable] RN(1/n), n = 1.. (volume constant)

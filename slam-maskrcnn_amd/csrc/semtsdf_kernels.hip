@@ -440,19 +440,25 @@ __device__ int unit_cull(const IntegrateArgs& a, int x0, int y0, int lz0) {
     const int gz1 = min(local_to_global_z(g, min(lz0 + UZ - 1, g.lz - 1)), g.dimz - 1);
     float umin = 3.0e38f, umax = -3.0e38f, vmin = 3.0e38f, vmax = -3.0e38f;
     float zmin = 3.0e38f, zmax = -3.0e38f, wmin = 3.0e38f, wmax = -3.0e38f;
-    // a unit one voxel thick in x has 4 distinct corners
+    // Corners through the affine cull map (host-rounded, ~1e-4 px from the contract's screen
+    // position, far inside the 1-px guard band); a unit one voxel thick in x has 4 distinct
+    // corners, which share their x part.
     constexpr int kCorners = UX == 1 ? 4 : 8;
+    const float* C = a.cullC;
+    float bx[4][2];  // row r at x0 / x1
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        bx[r][0] = fmaf((float)x0, C[r * 4 + 0], C[r * 4 + 3]);
+        bx[r][1] = UX == 1 ? bx[r][0] : fmaf((float)x1, C[r * 4 + 0], C[r * 4 + 3]);
+    }
 #pragma unroll
     for (int cc = 0; cc < kCorners; ++cc) {
         const int c = UX == 1 ? cc << 1 : cc;  // bit 0 selects x1 == x0 when UX == 1
-        const float px = fmaf((float)((c & 1) ? x1 : x0), g.voxel[0], g.start[0]);
-        const float py = fmaf((float)((c & 2) ? y1 : y0), g.voxel[1], g.start[1]);
-        const float pz = fmaf((float)((c & 4) ? gz1 : gz0), g.voxel[2], g.start[2]);
-        const float qx = dot3(a.E[0], a.E[1], a.E[2], px, py, pz) + a.E[3];
-        const float qy = dot3(a.E[4], a.E[5], a.E[6], px, py, pz) + a.E[7];
-        const float qz = dot3(a.E[8], a.E[9], a.E[10], px, py, pz) + a.E[11];
-        float sx, sy, sz;
-        screen(a, qx, qy, qz, &sx, &sy, &sz);
+        const float fy = (float)((c & 2) ? y1 : y0), fz = (float)((c & 4) ? gz1 : gz0);
+        float v4[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v4[r] = fmaf(fz, C[r * 4 + 2], fmaf(fy, C[r * 4 + 1], bx[r][c & 1]));
+        const float sx = v4[0], sy = v4[1], sz = v4[2], qz = v4[3];
         // conservative test: the reciprocal's ~1e-4 px error is far inside the 1-px guard band
         const float rz = __builtin_amdgcn_rcpf(sz);
         const float u = sx * rz, v = sy * rz;
@@ -528,27 +534,27 @@ __host__ __device__ inline UnitGrid unit_grid(const VolGeom& g) {
 // per counter to 1/64 of the workgroups).  Capacity of a segment: all units of its
 // workgroups.
 __host__ __device__ inline unsigned list_seg_cap(const UnitGrid& ug) {
-    const unsigned groups = (ug.n + 255u) / 256u;
+    const unsigned groups = (ug.nux + 255u) / 256u * ug.nuy * ug.nuz;  // k_cull_units workgroups
     return (groups + kListSegs - 1u) / kListSegs * 256u;
 }
 
-// Cull pass: one lane per unit (x fastest).  flags[u] = 1 when the unit may hold a touched
-// voxel; the live units of a workgroup are appended to its segment of the live-unit list
-// (their order is irrelevant: units are independent).
+// Cull pass: one lane per unit (x fastest).  The units that may hold a touched voxel are
+// appended to the workgroup's segment of the live-unit list (their order is irrelevant:
+// units are independent).
 __global__ __launch_bounds__(256) void k_cull_units(IntegrateArgs a, UnitGrid ug, unsigned seg_cap) {
     __shared__ unsigned s_cnt[4];
     __shared__ unsigned s_base;
-    const unsigned u = blockIdx.x * blockDim.x + threadIdx.x;
+    // grid (x runs of 256 units, uy, uz): no integer division by the runtime unit counts
+    const unsigned ux = blockIdx.x * blockDim.x + threadIdx.x, uy = blockIdx.y, uz = blockIdx.z;
+    const unsigned u = (uz * ug.nuy + uy) * ug.nux + ux;
+    const unsigned bid = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
     int live = 0;
-    if (u < ug.n) {
-        const int ux = (int)(u % ug.nux), uy = (int)((u / ug.nux) % ug.nuy), uz = (int)(u / (ug.nux * ug.nuy));
-        live = a.cull ? !unit_cull(a, ux * UX, uy * UY, uz * UZ) : 1;
-    }
+    if (ux < ug.nux) live = a.cull ? !unit_cull(a, (int)ux * UX, (int)uy * UY, (int)uz * UZ) : 1;
     const int lane = (int)(threadIdx.x & 63u), wv = (int)(threadIdx.x >> 6);
     const unsigned long long bal = __ballot(live);
     if (lane == 0) s_cnt[wv] = (unsigned)__popcll(bal);
     __syncthreads();
-    const unsigned seg = blockIdx.x % (unsigned)kListSegs;
+    const unsigned seg = bid % (unsigned)kListSegs;
     if (threadIdx.x == 0) {
         const unsigned tot = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
         s_base = tot ? atomicAdd(a.list_count + seg * kListCountStride, tot) : 0u;
@@ -564,7 +570,8 @@ __global__ __launch_bounds__(256) void k_cull_units(IntegrateArgs a, UnitGrid ug
 hipError_t launch_cull(const IntegrateArgs& a, hipStream_t s) {
     const UnitGrid ug = unit_grid(a.g);
     if (ug.n == 0) return hipSuccess;  // a shard that owns no chunk
-    hipLaunchKernelGGL(k_cull_units, dim3((ug.n + 255) / 256), dim3(256), 0, s, a, ug, list_seg_cap(ug));
+    hipLaunchKernelGGL(k_cull_units, dim3((ug.nux + 255) / 256, ug.nuy, ug.nuz), dim3(256), 0, s, a, ug,
+                       list_seg_cap(ug));
     return hipGetLastError();
 }
 
