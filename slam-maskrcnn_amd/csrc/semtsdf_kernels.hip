@@ -284,7 +284,6 @@ hipError_t launch_fill_volume(const VolGeom& g, const VolBufs& b, uint32_t flags
 __global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restrict__ depth, const uint8_t* __restrict__ rgb,
                                                        const uint8_t* __restrict__ mask, int w, int h, float scale,
                                                        int vec, DepthPyramid p, unsigned* list_count) {
-    __shared__ unsigned s_m[32][8];
     const int tx = blockIdx.x, ty = blockIdx.y;
     const int t = threadIdx.x;
     if (list_count && tx == 0 && ty == 0 && t < kListSegs) list_count[t * kListCountStride] = 0u;  // this frame's list
@@ -328,27 +327,23 @@ __global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restric
             }
         }
     }
-    s_m[r][t & 7] = m;
-    __syncthreads();
-    __shared__ unsigned s_l0[4][4];
-    if (t < 16) {
-        const int a = t >> 2, bcol = t & 3;  // level-0 tile (a, bcol) inside this 32x32 tile
-        unsigned mm = 0;
-        for (int rr = 0; rr < 8; ++rr) {
-            mm = max(mm, s_m[a * 8 + rr][bcol * 2]);
-            mm = max(mm, s_m[a * 8 + rr][bcol * 2 + 1]);
-        }
-        s_l0[a][bcol] = mm;
-        const int gx0 = tx * 4 + bcol, gy0 = ty * 4 + a;
-        if (gx0 < p.w0 && gy0 < p.h0) p.l0[gy0 * p.w0 + gx0] = (uint16_t)mm;
+    // wave w holds rows 8w..8w+7: the level-0 tiles (w, 0..3), each the lanes with
+    // (t & 7) >> 1 == bcol; reduce over lane bits 0, 3, 4, 5 in registers
+    m = max(m, (unsigned)__shfl_xor((int)m, 1));
+    m = max(m, (unsigned)__shfl_xor((int)m, 8));
+    m = max(m, (unsigned)__shfl_xor((int)m, 16));
+    m = max(m, (unsigned)__shfl_xor((int)m, 32));
+    const int wv = t >> 6, ln = t & 63;
+    if (ln < 8 && (ln & 1) == 0) {
+        const int gx0 = tx * 4 + (ln >> 1), gy0 = ty * 4 + wv;
+        if (gx0 < p.w0 && gy0 < p.h0) p.l0[gy0 * p.w0 + gx0] = (uint16_t)m;
     }
+    m = max(m, (unsigned)__shfl_xor((int)m, 2));
+    m = max(m, (unsigned)__shfl_xor((int)m, 4));
+    __shared__ unsigned s_w[4];
+    if (ln == 0) s_w[wv] = m;
     __syncthreads();
-    if (t == 0) {
-        unsigned mm = 0;
-        for (int a = 0; a < 4; ++a)
-            for (int bcol = 0; bcol < 4; ++bcol) mm = max(mm, s_l0[a][bcol]);
-        p.l1[ty * p.w1 + tx] = (uint16_t)mm;
-    }
+    if (t == 0) p.l1[ty * p.w1 + tx] = (uint16_t)max(max(s_w[0], s_w[1]), max(s_w[2], s_w[3]));
 }
 
 hipError_t launch_depth_pyramid(const uint16_t* depth, const uint8_t* rgb, const uint8_t* mask, int w, int h,
