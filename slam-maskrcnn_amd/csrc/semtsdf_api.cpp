@@ -121,7 +121,7 @@ int dev_alloc(semtsdf_vol* v, void** p, size_t bytes) {
 }
 
 void free_all(semtsdf_vol* v) {
-    void* ptrs[] = {v->b.sdf, v->b.wt, v->b.bmin, v->b.bplain, v->b.sbmin, v->b.bdist, v->b.bdtmp, v->b.bdirty, v->b.color, v->b.hist, v->b.hmask, v->b.cls, v->b.cls_cnt, v->depth_d, v->rgb_d,
+    void* ptrs[] = {v->b.sdf, v->b.wt, v->b.bmin, v->b.bplain, v->b.sbmin, v->b.bdist, v->b.bdtmp, v->b.bdirty, v->b.sflag, v->b.color, v->b.hist, v->b.hmask, v->b.cls, v->b.cls_cnt, v->depth_d, v->rgb_d,
                     v->mask_d, v->cls_d, v->pyr.px, v->pyr.l0, v->pyr.l1, v->tables_d, v->decision_d,
                     v->num_objs_d, v->probs_d, v->box_d, v->palette_d, v->render_d, v->render_t_d,
                     v->counters_d, v->ray_state_d, v->unit_list_d, v->list_count_d, v->rcp_table_d};
@@ -577,6 +577,7 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     const bool ci32 = p->flags & SEMTSDF_F_COLOR_I32;
     if ((rc = dev_alloc(v, (void**)&v->b.sdf, n * 4))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->b.wt, n * 4))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&v->b.sflag, n / 32 + 1))) return bail(rc);
     const size_t nbricks = (size_t)g.nbx * g.nby * g.nbz;
     if ((rc = dev_alloc(v, (void**)&v->b.bmin, nbricks * 4))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->b.bplain, nbricks * 4))) return bail(rc);
@@ -677,6 +678,7 @@ int semtsdf_reset(semtsdf_vol* v, void* stream) {
     const size_t n = v->g.nvox;
     HIPC(launch_fill_volume(v->g, v->b, v->p.flags, s));
     HIPC(hipMemsetAsync(v->b.wt, 0, n * 4, s));
+    HIPC(hipMemsetAsync(v->b.sflag, 0, n / 32 + 1, s));  // steady flags: unknown
     HIPC(hipMemsetAsync(v->b.color, 0, v->g.nvox * 4 * ((v->p.flags & SEMTSDF_F_COLOR_I32) ? 4 : 1), s));
     if (v->b.hist) HIPC(hipMemsetAsync(v->b.hist, 0, v->g.nvox * kMaxObjects * 4, s));
     if (v->b.hmask) HIPC(hipMemsetAsync(v->b.hmask, 0, n * 4, s));
@@ -1249,6 +1251,7 @@ int semtsdf_upload(semtsdf_vol* v, const float* sdf, const int32_t* wt, const vo
     int rc;
     if (sdf && (rc = vox_xfer(v, const_cast<float*>(sdf), v->b.sdf, false, "sdf", s))) return rc;
     if (wt && (rc = vox_xfer(v, const_cast<int32_t*>(wt), v->b.wt, false, "weight", s))) return rc;
+    if (sdf || wt) HIPC(hipMemsetAsync(v->b.sflag, 0, v->g.nvox / 32 + 1, s));  // steady flags: unknown
     if (color) {
         rc = color_xfer(v, const_cast<void*>(color), false, s);
         if (rc) return rc;

@@ -69,6 +69,8 @@ struct VolBufs {
                        // brick (0: not skippable), capped at kBrickDistCap
     uint8_t* bdtmp;    // scratch of the distance passes
     uint8_t* bdirty;   // per 8^3 brick: overlaps a unit integrated since the last map update
+    uint8_t* sflag;    // per 128-B sdf line (32 voxels): 1 = every sdf is 1.0f and every weight
+                       // < 2^23 (k_integrate skips the sdf traffic of such lines); 0 = unknown
 };
 
 // Per-frame images of the integrate: depth in metres and rgb+label per pixel (row-major,

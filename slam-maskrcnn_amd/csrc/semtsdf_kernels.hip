@@ -623,10 +623,15 @@ __device__ __forceinline__ uint64_t unit_tile(const VolGeom& g, const UnitPos& u
     return tile_xterm(g, up.x) + __umul24((uint32_t)up.uy, g.ty) + (z0 >> 5) * 256u + ((z0 >> 2) & 7u) * 32u;
 }
 
+#ifndef SEMTSDF_STEADY
+#define SEMTSDF_STEADY 1  // skip the sdf traffic of steady lines (Ld::skip)
+#endif
+
 struct Proj {
     float qz[4];
     uint2 rec[4];  // gathered pixel record {metres bits, rgbl}
     int img[4];    // pixel index; W*H (the zero record) off-image or on an invalid plane
+    unsigned sflag;  // steady flag of the lane's sdf line (below)
 };
 
 struct Cls {
@@ -636,6 +641,7 @@ struct Cls {
     unsigned hmode;    // 1: the gated voxels share label hlab < 32 (one 16-B histogram RMW); 2: atomics
     unsigned hlab;
     int img[4];        // vote mode
+    unsigned sflag;    // steady flag of the lane's sdf line
 };
 
 // What stage_store needs of a classification: masks, histogram mode/label and the 4 labels.
@@ -652,6 +658,7 @@ __device__ __forceinline__ StoreMeta store_meta(const Cls& C) {
 }
 
 struct Ld {
+    bool skip;  // steady line: s4 not loaded, every value is 1.0f
     float4 s4;
     int4 w4;
     uint4 c8;
@@ -664,6 +671,8 @@ struct Ld {
 struct Out {
     float4 s4;
     int4 w4;
+    bool skip;       // the line's sdf was neither loaded nor changes (steady line)
+    unsigned oflag;  // the line's steady flag before this update
     bool cross;      // a voxel's sdf crossed the skip threshold (its brick's map entry may flip)
     uint4 c8;
     int4 c32[4];
@@ -726,6 +735,10 @@ __device__ __forceinline__ void stage_project(const IntegrateArgs& a, const Unit
             P.img[k] = in ? iy * a.width + ix : npx;
         }
     }
+    // steady flag of the lane's sdf line (one byte per 128-B line, unconditional)
+    P.sflag = SEMTSDF_STEADY ? (unsigned)a.b.sflag[(unit_tile(g, up) + (unsigned)lane_zq(lane) * 32u +
+                                                    (unsigned)lane_y(lane) * 4u) >> 5]
+                             : 0u;
     // unconditional gathers; an off-image voxel reads the zero record past the image (depth 0)
 #pragma unroll
     for (int k = 0; k < 4; ++k) P.rec[k] = a.pyr.px[(unsigned)P.img[k]];
@@ -750,6 +763,7 @@ __device__ __forceinline__ void stage_classify(const IntegrateArgs& a, const Pro
         C.pix[k] = P.rec[k].y;
         if (VOTE) C.img[k] = P.img[k];
     }
+    C.sflag = P.sflag;
     if (dslow || !a.fastdiv) {  // rare: tiny differences, or mu outside the reciprocal range
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -804,6 +818,13 @@ __device__ __forceinline__ bool tile_line_any(bool p) {
     return ((b >> (lane % LZQ + lane_slot(lane) * kUnitLanes)) & kLineLanes) != 0ull;
 }
 
+// true when p holds on all 8 lanes of the lane's line (inactive lanes count as true)
+__device__ __forceinline__ bool tile_line_all(bool p) {
+    const uint64_t b = __ballot(!p);
+    const int lane = (int)__lane_id();
+    return ((b >> (lane % LZQ + lane_slot(lane) * kUnitLanes)) & kLineLanes) == 0ull;
+}
+
 #ifndef SEMTSDF_NT_LOAD
 #define SEMTSDF_NT_LOAD 1
 #endif
@@ -851,7 +872,15 @@ __device__ __forceinline__ void stage_load(const IntegrateArgs& a, const UnitPos
     const uint4* dummy = reinterpret_cast<const uint4*>(a.rcp_table);
     const bool t = tile_line_any(C.tmask != 0u), gt = tile_line_any(C.gmask != 0u);
     const unsigned lt = t ? coff : 0u, lg = gt ? coff : 0u;
-    L.s4 = ld_state<float4>(a.b.sdf + ub + lt);
+    // Steady line: every sdf of the line is exactly 1.0f with weight < 2^23 (flag) and every
+    // touched voxel of it has f == 1.0f, so (1 w + 1) / (w + 1) == 1 exactly (w + 1 < 2^24 in
+    // both the reciprocal and the IEEE path): the line's sdf is neither read nor written.
+    bool fone = true;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) fone &= (((C.tmask >> k) & 1u) == 0u) | (C.fv[k] == 1.0f);
+    const bool skip = SEMTSDF_STEADY && tile_line_all((C.sflag != 0u) & fone);
+    L.skip = skip;
+    L.s4 = ld_state<float4>(skip ? reinterpret_cast<const float*>(dummy) : a.b.sdf + ub + lt);
     L.w4 = ld_state<int4>(a.b.wt + ub + lt);
     if (CI32) {
 #pragma unroll
@@ -875,7 +904,10 @@ __device__ __forceinline__ void stage_compute(const IntegrateArgs& a, const floa
                                               const Ld& L, Out& O) {
     const unsigned tmask = C.tmask, gmask = C.gmask;
     // ---- running mean (tsdf.cu:56, 68) through RN(1/(w+1)) from the LDS table
-    const float so[4] = {L.s4.x, L.s4.y, L.s4.z, L.s4.w};
+    const float so[4] = {L.skip ? 1.0f : L.s4.x, L.skip ? 1.0f : L.s4.y, L.skip ? 1.0f : L.s4.z,
+                         L.skip ? 1.0f : L.s4.w};
+    O.skip = L.skip;
+    O.oflag = C.sflag;
     const int wo[4] = {L.w4.x, L.w4.y, L.w4.z, L.w4.w};
     float sn[4];
     int wn[4];
@@ -999,8 +1031,14 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
         }
     }
     if (a.debug != 10) {  // 10: timing probe, loads but no sdf/weight stores
-        st_state(a.b.sdf + v, O.s4);
+        if (!O.skip) st_state(a.b.sdf + v, O.s4);
         st_state(a.b.wt + v, O.w4);
+    }
+    if (SEMTSDF_STEADY) {  // the line's steady flag after this update (one lane per line writes)
+        const bool one = (O.s4.x == 1.0f) & (O.s4.y == 1.0f) & (O.s4.z == 1.0f) & (O.s4.w == 1.0f) &
+                         (O.w4.x < (1 << 23)) & (O.w4.y < (1 << 23)) & (O.w4.z < (1 << 23)) & (O.w4.w < (1 << 23));
+        const bool nflag = tile_line_all(one);
+        if (lane_y((int)__lane_id()) == 0 && nflag != (O.oflag != 0u)) a.b.sflag[v >> 5] = nflag ? 1u : 0u;
     }
     if (grow) {
         if (CI32) {
