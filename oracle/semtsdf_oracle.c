@@ -130,7 +130,10 @@ void oracle_integrate(const int32_t* dims, const float* geo, const float* K9, co
                             col[v * 3 + c] = (col[v * 3 + c] * w + (int)rgb[img * 3 + c]) / (w + 1);
                         } else {
                             uint8_t* col = (uint8_t*)color;
-                            col[v * 3 + c] = (uint8_t)(((int)col[v * 3 + c] * w + (int)rgb[img * 3 + c]) / (w + 1));
+                            /* int arithmetic of tsdf.cu:59; c * w wraps past 2^31 (w > 8.4 M)
+                               as on the reference's hardware (explicitly, not as C UB) */
+                            const int num = (int)((uint32_t)col[v * 3 + c] * (uint32_t)w + (uint32_t)rgb[img * 3 + c]);
+                            col[v * 3 + c] = (uint8_t)(num / (w + 1));
                         }
                     }
                     if (sem) {

@@ -974,9 +974,12 @@ __device__ __forceinline__ void stage_compute(const IntegrateArgs& a, const floa
                 for (int k = 0; k < 4; ++k) {
                     if (!(cslow & (1u << k))) continue;
                     const unsigned wi = (unsigned)wo[k], o = co[k], px = C.pix[k];
-                    const unsigned n0 = ((o & 0xFFu) * wi + (px & 0xFFu)) / (wi + 1u);
-                    const unsigned n1 = (((o >> 8) & 0xFFu) * wi + ((px >> 8) & 0xFFu)) / (wi + 1u);
-                    const unsigned n2 = (((o >> 16) & 0xFFu) * wi + ((px >> 16) & 0xFFu)) / (wi + 1u);
+                    // int arithmetic of tsdf.cu:59 (c * w wraps past 2^31 at w > 8.4 M, as on the
+                    // reference's hardware), truncating signed quotient, then the u8 store
+                    const int dw = (int)(wi + 1u);
+                    const unsigned n0 = (unsigned)((int)((o & 0xFFu) * wi + (px & 0xFFu)) / dw);
+                    const unsigned n1 = (unsigned)((int)(((o >> 8) & 0xFFu) * wi + ((px >> 8) & 0xFFu)) / dw);
+                    const unsigned n2 = (unsigned)((int)(((o >> 16) & 0xFFu) * wi + ((px >> 16) & 0xFFu)) / dw);
                     cw[k] = (n0 & 0xFFu) | ((n1 & 0xFFu) << 8) | ((n2 & 0xFFu) << 16);
                 }
             }

@@ -495,3 +495,31 @@ def test_full_size_512_semantic_integrate(S, oracle, stream):
     assert touched > 10_000_000  # the surface band and free space in front of it are exercised
     assert_same(vol, ost, hist=True)
     vol.close()
+
+
+def test_steady_lines_repeated_frames_and_weight_limit(S, oracle, stream):
+    """Steady sdf lines (all 1.0f, weights < 2^23) skip their sdf traffic: repeated frames
+    make most free-space lines steady; an uploaded state of sdf 1.0 with weights around 2^23
+    and 2^24 checks the weight bound of the flag and that uploads clear the flags."""
+    st, frames = stream
+    p, vol, g, ost = make(S, oracle, (64, 64, 64), frames[0], 0x3)
+    for k in (1, 1, 1, 2, 2, 1, 3, 3, 1):
+        fr = frames[k]
+        E = (fr.w2c @ frames[0].c2w).astype(np.float32)
+        vol.integrate(fr.depth, fr.rgb, fr.gt_ids, E)
+        oracle.integrate(g, ost, list(p.K), E, fr.depth, fr.rgb, fr.gt_ids, flags=0x3)
+    assert (ost.sdf == 1.0).mean() > 0.05  # free space converged to exactly 1.0
+    assert_same(vol, ost, hist=True)
+    rng = np.random.default_rng(5)
+    n = ost.sdf.size
+    base = np.where(rng.random(n) < 0.5, (1 << 23) - 3, (1 << 24) - 3).astype(np.int64)
+    ost.sdf[:] = np.float32(1.0)
+    ost.wt[:] = (base + rng.integers(0, 6, n)).astype(np.int32)
+    vol.upload(sdf=ost.sdf, wt=ost.wt)
+    for k in (1, 1, 2, 1, 1, 3):
+        fr = frames[k]
+        E = (fr.w2c @ frames[0].c2w).astype(np.float32)
+        vol.integrate(fr.depth, fr.rgb, fr.gt_ids, E)
+        oracle.integrate(g, ost, list(p.K), E, fr.depth, fr.rgb, fr.gt_ids, flags=0x3)
+    assert_same(vol, ost, hist=True)
+    vol.close()
