@@ -296,6 +296,7 @@ def main():
     touched = tc.touched / args.steps
     gated = tc.gated / args.steps
     bricks = tc.bricks / args.steps
+    free_units = tc.free_units / args.steps
     bytes_per_launch = 16.0 * touched + 14.0 * gated + 6.0 * npx
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
 
@@ -390,7 +391,8 @@ def main():
             "prep_ms": round(prep_ms, 4),
             "touched_per_frame": int(touched),
             "gated_per_frame": int(gated),
-            "live_bricks_per_frame": int(bricks),
+            "live_units_per_frame": int(bricks),
+            "free_units_per_frame": int(free_units),
             "touched_mvox_per_s": round(touched / (kern_ms * 1e-3) / 1e6, 1),
             "roofline": {
                 "bound": "hbm",

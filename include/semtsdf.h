@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SEMTSDF_ABI_VERSION 2
+#define SEMTSDF_ABI_VERSION 3
 #define SEMTSDF_MAX_OBJECTS 32 /* tsdf.cuh:4 */
 
 /* ---- status codes ------------------------------------------------------------ */
@@ -104,9 +104,10 @@ typedef struct semtsdf_timing {
     uint64_t n_integrate, n_assoc, n_render;
     uint64_t touched;     /* voxels updated (count mode only) */
     uint64_t gated;       /* voxels whose colour/histogram were updated (count mode only) */
-    uint64_t bricks;      /* 8x8x32 bricks that survived the frustum/depth cull (count mode only) */
+    uint64_t bricks;      /* integrate units that survived the frustum/depth cull (count mode only) */
     double prep_ms;       /* sum over the per-frame depth-pyramid + brick-cull passes */
     uint64_t n_prep;
+    uint64_t free_units;  /* of those, units whose touched voxels all have f == 1 (count mode only) */
 } semtsdf_timing;
 
 /* ---- library ------------------------------------------------------------------------ */

@@ -56,6 +56,8 @@ const uint8_t kPalette[kMaxObjects * 3] = {
     210, 245, 60,  250, 190, 190, 0,   128, 128, 230, 190, 255, 170, 110, 40,  255, 250, 200,
     128, 0,   0,   170, 255, 195};
 
+constexpr int kCounters = 8;  // device counters of a volume (IntegrateArgs::counters)
+
 struct EventPair {
     hipEvent_t a, b;
 };
@@ -86,7 +88,7 @@ struct semtsdf_vol {
     float* render_t_d = nullptr;
     unsigned long long* counters_d = nullptr;
     unsigned* unit_list_d = nullptr;  // live units of the frame (cull pass)
-    unsigned* list_count_d = nullptr; // [kListSegs * kListCountStride]
+    unsigned* list_count_d = nullptr; // [2][kListSegs * kListCountStride] (general, free)
     float* rcp_table_d = nullptr;    // RN(1/n), n = 1..kRcpTable
     AssocDecision* decision_h = nullptr;  // pinned
     // Z-sharded raycast protocol (allocated on first use)
@@ -133,6 +135,8 @@ void free_all(semtsdf_vol* v) {
     if (v->stream) (void)hipStreamDestroy(v->stream);
 }
 
+int local_planes(const semtsdf_params* p, int* chunk, int* halo);
+
 int check_params(const semtsdf_params* p) {
     if (!p) return fail(SEMTSDF_ERR_INVALID, "params is NULL");
     for (int i = 0; i < 3; ++i) {
@@ -160,6 +164,13 @@ int check_params(const semtsdf_params* p) {
         return fail(SEMTSDF_ERR_INVALID, "bad shard %d of %d", p->z_shard, p->z_nshards);
     if (p->z_nshards > 1 && (p->z_chunk < 1 || p->z_chunk > p->dim[2]))
         return fail(SEMTSDF_ERR_INVALID, "bad z_chunk %d", p->z_chunk);
+    {  // integrate list entries pack a unit's (x, y/8, z/16) into 12 + 10 + 10 bits (pack_unit)
+        int chunk, halo;
+        const int lz = local_planes(p, &chunk, &halo);
+        if (p->dim[0] > 4096 || (p->dim[1] + 7) / 8 > 1024 || (lz + 15) / 16 > 1024)
+            return fail(SEMTSDF_ERR_INVALID, "volume %d x %d x %d (%d local planes) outside the unit grid limits "
+                        "(x <= 4096, y <= 8192, local z <= 16384)", p->dim[0], p->dim[1], p->dim[2], lz);
+    }
     return SEMTSDF_OK;
 }
 
@@ -270,6 +281,12 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
     a.rmu = 1.0f / v->g.mu;  // IEEE: the correctly rounded reciprocal
     a.skip_thr = v->g.voxel[0] / 2.0f * (1.0f + 0x1p-16f);  // = skip_threshold (device), same IEEE ops
     a.fastdiv = (v->g.mu >= 0x1p-20f && v->g.mu <= 0x1p20f && a.debug != 8) ? 1 : 0;
+    // free units (f == 1 everywhere they are touched) change only sdf and weight when the
+    // colour/histogram gate rejects f == 1 (tsdf.cu:57): SfM gated modes with gate <= 1
+    a.free_ok = ((v->p.flags & SEMTSDF_F_GATE_COLOR) && !(v->p.flags & SEMTSDF_F_VOTE) && !(a.gate > 1.0f) &&
+                 a.fastdiv && a.debug != 9)
+                    ? 1
+                    : 0;
     if (a.debug == 2) return SEMTSDF_OK;
     EventPair epp;
     timing_begin(v, v->ev_prep, s, &epp);
@@ -605,10 +622,10 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     pyr.w1 = (p->width + 31) / 32; pyr.h1 = (p->height + 31) / 32;
     if ((rc = dev_alloc(v, (void**)&pyr.px, (px + 1) * 8))) return bail(rc);
     if (hipMemset(pyr.px, 0, (px + 1) * 8) != hipSuccess) return bail(fail(SEMTSDF_ERR_HIP, "memset failed"));
-    if ((rc = dev_alloc(v, (void**)&pyr.l0, (size_t)pyr.w1 * 4 * pyr.h1 * 4 * 2))) return bail(rc);
-    if ((rc = dev_alloc(v, (void**)&pyr.l1, (size_t)pyr.w1 * pyr.h1 * 2))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&pyr.l0, (size_t)pyr.w1 * 4 * pyr.h1 * 4 * 4))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&pyr.l1, (size_t)pyr.w1 * pyr.h1 * 4))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->unit_list_d, unit_list_capacity(g) * sizeof(unsigned)))) return bail(rc);
-    if ((rc = dev_alloc(v, (void**)&v->list_count_d, kListSegs * kListCountStride * sizeof(unsigned)))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&v->list_count_d, 2 * kListSegs * kListCountStride * sizeof(unsigned)))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->rcp_table_d, kRcpTable * sizeof(float)))) return bail(rc);
     {
         float t[kRcpTable];
@@ -619,7 +636,7 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     if ((rc = dev_alloc(v, (void**)&v->tables_d, sizeof(AssocTables)))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->decision_d, sizeof(AssocDecision)))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->num_objs_d, 16))) return bail(rc);
-    if ((rc = dev_alloc(v, (void**)&v->counters_d, 4 * sizeof(unsigned long long)))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&v->counters_d, kCounters * sizeof(unsigned long long)))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->palette_d, sizeof(kPalette)))) return bail(rc);
     if (hipHostMalloc((void**)&v->decision_h, sizeof(AssocDecision), 0) != hipSuccess)
         return bail(fail(SEMTSDF_ERR_HIP, "hipHostMalloc failed"));
@@ -685,7 +702,7 @@ int semtsdf_reset(semtsdf_vol* v, void* stream) {
     if (v->b.cls) HIPC(hipMemsetAsync(v->b.cls, 0, n * 4, s));
     if (v->b.cls_cnt) HIPC(hipMemsetAsync(v->b.cls_cnt, 0, n * 4, s));
     HIPC(hipMemsetAsync(v->num_objs_d, 0, 16, s));
-    HIPC(hipMemsetAsync(v->counters_d, 0, 4 * sizeof(unsigned long long), s));
+    HIPC(hipMemsetAsync(v->counters_d, 0, kCounters * sizeof(unsigned long long), s));
     v->n_obs = 0;
     v->bmin_stale = true;
     return SEMTSDF_OK;
@@ -1316,7 +1333,7 @@ int semtsdf_get_timing(semtsdf_vol* v, semtsdf_timing* out) {
     v->t_assoc += drain(v->ev_assoc);
     v->t_render += drain(v->ev_render);
     v->t_prep += drain(v->ev_prep);
-    unsigned long long c[4] = {0, 0, 0, 0};
+    unsigned long long c[kCounters] = {0, 0, 0, 0, 0, 0, 0, 0};
     HIPC(hipMemcpy(c, v->counters_d, sizeof(c), hipMemcpyDeviceToHost));
     out->integrate_ms = v->t_integrate;
     out->assoc_ms = v->t_assoc;
@@ -1327,6 +1344,7 @@ int semtsdf_get_timing(semtsdf_vol* v, semtsdf_timing* out) {
     out->touched = c[0];
     out->gated = c[1];
     out->bricks = c[3];
+    out->free_units = c[4];
     out->prep_ms = v->t_prep;
     out->n_prep = v->n_prep;
     return SEMTSDF_OK;
@@ -1343,7 +1361,7 @@ int semtsdf_reset_timing(semtsdf_vol* v) {
     v->t_integrate = v->t_assoc = v->t_render = v->t_prep = 0;
     v->n_integrate = v->n_assoc = v->n_render = v->n_prep = 0;
     HIPC(hipMemset(v->counters_d, 0, 2 * sizeof(unsigned long long)));
-    HIPC(hipMemset(v->counters_d + 3, 0, sizeof(unsigned long long)));
+    HIPC(hipMemset(v->counters_d + 3, 0, (kCounters - 3) * sizeof(unsigned long long)));
     return SEMTSDF_OK;
 }
 

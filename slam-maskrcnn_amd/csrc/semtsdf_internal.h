@@ -74,13 +74,15 @@ struct VolBufs {
 };
 
 // Per-frame images of the integrate: depth in metres and rgb+label per pixel (row-major,
-// W x H), and the max raw depth over 8- and 32-pixel tiles used by the unit culler.
+// W x H), and per 8- and 32-pixel tile the max raw depth (bits 0-15) and 0xFFFF - the min
+// nonzero raw depth (bits 16-31; 0 when the tile has no nonzero pixel), used by the unit
+// culler (dead units, and free units whose touched voxels all have f == 1).
 struct DepthPyramid {
     uint2* px;      // [H][W] pixel records {bits of depth / depth_scale (IEEE, tsdf.cu:49),
                     //                       r | g << 8 | b << 16 | label << 24}: one 8-B gather per voxel;
                     // record W*H is zero (the target of off-image voxels)
-    uint16_t* l0;  // [ceil(H/8)][ceil(W/8)]
-    uint16_t* l1;  // [ceil(H/32)][ceil(W/32)]
+    uint32_t* l0;  // [ceil(H/8)][ceil(W/8)]
+    uint32_t* l1;  // [ceil(H/32)][ceil(W/32)]
     int w0, h0, w1, h1;
 };
 
@@ -107,12 +109,13 @@ struct IntegrateArgs {
     const uint8_t* mask;    // semantic
     const int32_t* cls;     // vote
     DepthPyramid pyr;
-    unsigned long long* counters;  // [0] touched, [1] gated, [2] bad-label flag, [3] live bricks
+    unsigned long long* counters;  // [0] touched, [1] gated, [2] bad-label flag, [3] live units, [4] free units
     int pinhole;                   // K rows are (fx 0 cx; 0 fy cy; 0 0 1)
     float rmu;                     // RN(1/mu), for the exact division by mu (k_integrate)
     int fastdiv;                   // mu in [2^-20, 2^20]: divisions by mu/(w+1) via RN reciprocals
-    unsigned* unit_list;           // live units, kListSegs segments (k_cull_units)
-    unsigned* list_count;          // [kListSegs * kListCountStride] entries per segment (zeroed by the frame prepass)
+    unsigned* unit_list;           // live units: two lists (general, free) of kListSegs segments (k_cull_units)
+    unsigned* list_count;          // [2][kListSegs * kListCountStride] entries per segment (zeroed by the frame prepass)
+    int free_ok;                   // free units allowed: gated colour with gate <= 1 (f == 1 updates sdf/weight only)
 };
 
 // Association accumulators (fixed point, scale 2^28, deterministic).

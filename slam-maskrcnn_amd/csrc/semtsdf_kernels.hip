@@ -286,18 +286,22 @@ __global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restric
                                                        int vec, DepthPyramid p, unsigned* list_count) {
     const int tx = blockIdx.x, ty = blockIdx.y;
     const int t = threadIdx.x;
-    if (list_count && tx == 0 && ty == 0 && t < kListSegs) list_count[t * kListCountStride] = 0u;  // this frame's list
+    if (list_count && tx == 0 && ty == 0 && t < 2 * kListSegs)  // this frame's two lists (general, free)
+        list_count[(t & (kListSegs - 1)) * kListCountStride + (t >> 6) * kListSegs * kListCountStride] = 0u;
     const int r = t >> 3;          // row in tile
     const int c4 = (t & 7) * 4;    // first column in tile
     const int yy = ty * 32 + r;
     const int x0 = tx * 32 + c4;
-    unsigned m = 0;
+    // m: max raw depth; n: 0xFFFF - min nonzero raw depth (0: no nonzero pixel); both reduce by max
+    unsigned m = 0, n = 0;
     if (yy < h && x0 < w) {
         const size_t px0 = (size_t)yy * w + x0;
         if (vec && x0 + 3 < w) {
             const ushort4 d4 = *reinterpret_cast<const ushort4*>(depth + px0);
             const unsigned d[4] = {d4.x, d4.y, d4.z, d4.w};
             m = max(max(d[0], d[1]), max(d[2], d[3]));
+#pragma unroll
+            for (int k = 0; k < 4; ++k) n = max(n, d[k] ? 0xFFFFu - d[k] : 0u);
             uint4 o = make_uint4(0, 0, 0, 0);
             if (rgb) {
                 const uint32_t* c = reinterpret_cast<const uint32_t*>(rgb + px0 * 3);
@@ -317,6 +321,7 @@ __global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restric
                 const size_t px = px0 + k;
                 const unsigned d = depth[px];
                 m = max(m, d);
+                n = max(n, d ? 0xFFFFu - d : 0u);
                 unsigned c = 0;
                 if (rgb) {
                     const unsigned lab = mask ? (unsigned)mask[px] : 0u;
@@ -329,21 +334,27 @@ __global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restric
     }
     // wave w holds rows 8w..8w+7: the level-0 tiles (w, 0..3), each the lanes with
     // (t & 7) >> 1 == bcol; reduce over lane bits 0, 3, 4, 5 in registers
-    m = max(m, (unsigned)__shfl_xor((int)m, 1));
-    m = max(m, (unsigned)__shfl_xor((int)m, 8));
-    m = max(m, (unsigned)__shfl_xor((int)m, 16));
-    m = max(m, (unsigned)__shfl_xor((int)m, 32));
+#pragma unroll
+    for (int b : {1, 8, 16, 32}) {
+        m = max(m, (unsigned)__shfl_xor((int)m, b));
+        n = max(n, (unsigned)__shfl_xor((int)n, b));
+    }
     const int wv = t >> 6, ln = t & 63;
     if (ln < 8 && (ln & 1) == 0) {
         const int gx0 = tx * 4 + (ln >> 1), gy0 = ty * 4 + wv;
-        if (gx0 < p.w0 && gy0 < p.h0) p.l0[gy0 * p.w0 + gx0] = (uint16_t)m;
+        if (gx0 < p.w0 && gy0 < p.h0) p.l0[gy0 * p.w0 + gx0] = m | (n << 16);
     }
-    m = max(m, (unsigned)__shfl_xor((int)m, 2));
-    m = max(m, (unsigned)__shfl_xor((int)m, 4));
-    __shared__ unsigned s_w[4];
-    if (ln == 0) s_w[wv] = m;
+#pragma unroll
+    for (int b : {2, 4}) {
+        m = max(m, (unsigned)__shfl_xor((int)m, b));
+        n = max(n, (unsigned)__shfl_xor((int)n, b));
+    }
+    __shared__ unsigned s_w[4], s_n[4];
+    if (ln == 0) { s_w[wv] = m; s_n[wv] = n; }
     __syncthreads();
-    if (t == 0) p.l1[ty * p.w1 + tx] = (uint16_t)max(max(s_w[0], s_w[1]), max(s_w[2], s_w[3]));
+    if (t == 0)
+        p.l1[ty * p.w1 + tx] = max(max(s_w[0], s_w[1]), max(s_w[2], s_w[3])) |
+                               (max(max(s_n[0], s_n[1]), max(s_n[2], s_n[3])) << 16);
 }
 
 hipError_t launch_depth_pyramid(const uint16_t* depth, const uint8_t* rgb, const uint8_t* mask, int w, int h,
@@ -373,6 +384,12 @@ hipError_t launch_depth_pyramid(const uint16_t* depth, const uint8_t* rgb, const
 #define SEMTSDF_UNIT_Z 16
 #endif
 constexpr int UX = SEMTSDF_UNIT_X, UY = SEMTSDF_UNIT_Y, UZ = SEMTSDF_UNIT_Z;
+// Timing probes of the integrate (SEMTSDF_DEBUG_INTEGRATE=n at run time) exist only in a
+// build with -DSEMTSDF_INTEGRATE_PROBES=1: the production kernel carries no probe branches.
+#ifndef SEMTSDF_INTEGRATE_PROBES
+#define SEMTSDF_INTEGRATE_PROBES 0
+#endif
+constexpr bool kProbes = SEMTSDF_INTEGRATE_PROBES != 0;
 constexpr int LZQ = UZ / 4;                 // lanes along z
 constexpr int kUnitLanes = UX * UY * UZ / 4;  // lanes of one unit (4 z-voxels each)
 constexpr int kSlots = 64 / kUnitLanes;     // units per wave
@@ -425,7 +442,8 @@ __device__ __forceinline__ void screen(const IntegrateArgs& a, float qx, float q
 }
 
 // Conservative unit test: returns 1 when no voxel of the unit can pass the projection /
-// depth tests of tsdf.cu:46-50, so culling never changes results.
+// depth tests of tsdf.cu:46-50 (dead), 2 when every voxel that passes them has f == 1
+// (free: tsdf.cu:46-56 with diff >= mu), else 0; culling never changes results.
 __device__ int unit_cull(const IntegrateArgs& a, int x0, int y0, int lz0) {
     const VolGeom& g = a.g;
     const int x1 = min(x0 + UX - 1, g.dimx - 1);
@@ -475,17 +493,21 @@ __device__ int unit_cull(const IntegrateArgs& a, int x0, int y0, int lz0) {
     const int v0 = (int)fmaxf(floorf(vmin) - 1.0f, 0.0f);
     const int v1 = (int)fminf(floorf(vmax) + 1.0f, H - 1.0f);
     if (u0 > u1 || v0 > v1) return 1;
-    // max depth over the footprint, on the finest pyramid level covering it with <= 4x4
-    // tiles: the 16 loads are issued together (predicated), one round trip
-    unsigned m = 0;
+    // max depth (and min nonzero depth) over the footprint, on the finest pyramid level
+    // covering it with <= 4x4 tiles: the 16 loads are issued together (predicated), one round trip
+    unsigned m = 0, nz = 0;  // nz: 0xFFFF - min nonzero raw depth (0: none)
     const bool fit0 = ((u1 >> 3) - (u0 >> 3)) < 4 && ((v1 >> 3) - (v0 >> 3)) < 4;
     const bool fit1 = ((u1 >> 5) - (u0 >> 5)) < 4 && ((v1 >> 5) - (v0 >> 5)) < 4;
     if (!fit0 && ((u1 >> 3) - (u0 >> 3) + 1) * ((v1 >> 3) - (v0 >> 3) + 1) <= 16) {  // thin footprints
         for (int ty = v0 >> 3; ty <= (v1 >> 3); ++ty)
-            for (int tx = u0 >> 3; tx <= (u1 >> 3); ++tx) m = max(m, (unsigned)a.pyr.l0[ty * a.pyr.w0 + tx]);
+            for (int tx = u0 >> 3; tx <= (u1 >> 3); ++tx) {
+                const unsigned w = a.pyr.l0[ty * a.pyr.w0 + tx];
+                m = max(m, w & 0xFFFFu);
+                nz = max(nz, w >> 16);
+            }
     } else if (fit0 || fit1) {
         const int sh = fit0 ? 3 : 5;
-        const uint16_t* lv = fit0 ? a.pyr.l0 : a.pyr.l1;
+        const uint32_t* lv = fit0 ? a.pyr.l0 : a.pyr.l1;
         const int wl = fit0 ? a.pyr.w0 : a.pyr.w1;
         const int tx0 = u0 >> sh, ty0 = v0 >> sh, nx = (u1 >> sh) - tx0, ny = (v1 >> sh) - ty0;
         unsigned t[16];
@@ -496,24 +518,47 @@ __device__ int unit_cull(const IntegrateArgs& a, int x0, int y0, int lz0) {
             t[j] = ok ? t[j] : 0u;
         }
 #pragma unroll
-        for (int j = 0; j < 16; ++j) m = max(m, t[j]);
+        for (int j = 0; j < 16; ++j) {
+            m = max(m, t[j] & 0xFFFFu);
+            nz = max(nz, t[j] >> 16);
+        }
     } else if (((u1 >> 5) - (u0 >> 5) + 1) * ((v1 >> 5) - (v0 >> 5) + 1) <= 64) {
         for (int ty = v0 >> 5; ty <= (v1 >> 5); ++ty)
-            for (int tx = u0 >> 5; tx <= (u1 >> 5); ++tx) m = max(m, (unsigned)a.pyr.l1[ty * a.pyr.w1 + tx]);
+            for (int tx = u0 >> 5; tx <= (u1 >> 5); ++tx) {
+                const unsigned w = a.pyr.l1[ty * a.pyr.w1 + tx];
+                m = max(m, w & 0xFFFFu);
+                nz = max(nz, w >> 16);
+            }
     } else {
         return 0;  // footprint wider than 256x256 px (units at the near plane): keep
     }
     if (m == 0) return 1;  // every pixel of the footprint has depth 0
     const float dmax = (float)m / a.depth_scale;
-    const float margin = 1.0e-3f + 1.0e-4f * fabsf(zmax);
+    const float margin = 1.0e-3f + 1.0e-4f * fmaxf(fabsf(zmax), fabsf(zmin));
     // every voxel has qz >= zmin, so diff <= dmax - zmin; rejected when that is <= -mu
     if (dmax - zmin < -g.mu - margin) return 1;
+    // free unit: every pixel it can touch has depth >= dmin (the zeros leave their voxels
+    // untouched), and every voxel has qz <= zmax, so a touched voxel has diff >= mu, i.e.
+    // f == 1 exactly; with the gate at or below 1 such a voxel updates only its sdf and weight
+    if (a.free_ok && nz != 0) {
+        const float dmin = (float)(0xFFFFu - nz) / a.depth_scale;
+        if (dmin - zmax > g.mu + margin) return 2;
+    }
     return 0;
 }
 
 struct UnitGrid {
     unsigned nux, nuy, nuz, n;
 };
+
+// A live-list entry is the unit's coordinates packed into one word (x | uy << 12 | uz << 22),
+// so the integrate decodes it with bit-field extracts instead of divisions by the runtime
+// unit counts; the host rejects volumes whose unit grid does not fit (check_params).
+constexpr int kEntryXBits = 12, kEntryYBits = 10, kEntryZBits = 10;
+static_assert(kEntryXBits + kEntryYBits + kEntryZBits == 32, "one word per entry");
+__device__ __forceinline__ unsigned pack_unit(unsigned ux, unsigned uy, unsigned uz) {
+    return ux | (uy << kEntryXBits) | (uz << (kEntryXBits + kEntryYBits));
+}
 
 __host__ __device__ inline UnitGrid unit_grid(const VolGeom& g) {
     UnitGrid u;
@@ -534,31 +579,37 @@ __host__ __device__ inline unsigned list_seg_cap(const UnitGrid& ug) {
 }
 
 // Cull pass: one lane per unit (x fastest).  The units that may hold a touched voxel are
-// appended to the workgroup's segment of the live-unit list (their order is irrelevant:
-// units are independent).
+// appended to the workgroup's segment of one of two live-unit lists: list 0 (general) and
+// list 1 (free units, unit_cull == 2), each kListSegs segments of seg_cap entries with its
+// own counters (their order is irrelevant: units are independent).
 __global__ __launch_bounds__(256) void k_cull_units(IntegrateArgs a, UnitGrid ug, unsigned seg_cap) {
-    __shared__ unsigned s_cnt[4];
-    __shared__ unsigned s_base;
+    __shared__ unsigned s_cnt[2][4];
+    __shared__ unsigned s_base[2];
     // grid (x runs of 256 units, uy, uz): no integer division by the runtime unit counts
     const unsigned ux = blockIdx.x * blockDim.x + threadIdx.x, uy = blockIdx.y, uz = blockIdx.z;
-    const unsigned u = (uz * ug.nuy + uy) * ug.nux + ux;
+    const unsigned u = pack_unit(ux, uy, uz);
     const unsigned bid = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-    int live = 0;
-    if (ux < ug.nux) live = a.cull ? !unit_cull(a, (int)ux * UX, (int)uy * UY, (int)uz * UZ) : 1;
+    int c = 1;  // dead
+    if (ux < ug.nux) c = a.cull ? unit_cull(a, (int)ux * UX, (int)uy * UY, (int)uz * UZ) : 0;
     const int lane = (int)(threadIdx.x & 63u), wv = (int)(threadIdx.x >> 6);
-    const unsigned long long bal = __ballot(live);
-    if (lane == 0) s_cnt[wv] = (unsigned)__popcll(bal);
-    __syncthreads();
-    const unsigned seg = bid % (unsigned)kListSegs;
-    if (threadIdx.x == 0) {
-        const unsigned tot = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
-        s_base = tot ? atomicAdd(a.list_count + seg * kListCountStride, tot) : 0u;
+    const unsigned long long bal0 = __ballot(c == 0), bal1 = __ballot(c == 2);
+    if (lane == 0) {
+        s_cnt[0][wv] = (unsigned)__popcll(bal0);
+        s_cnt[1][wv] = (unsigned)__popcll(bal1);
     }
     __syncthreads();
-    if (live) {
-        unsigned off = s_base + (unsigned)__popcll(bal & ((1ull << lane) - 1ull));
-        for (int w = 0; w < wv; ++w) off += s_cnt[w];
-        a.unit_list[seg * seg_cap + off] = u;
+    const unsigned seg = bid % (unsigned)kListSegs;
+    if (threadIdx.x < 2) {
+        const unsigned l = threadIdx.x;
+        const unsigned tot = s_cnt[l][0] + s_cnt[l][1] + s_cnt[l][2] + s_cnt[l][3];
+        s_base[l] = tot ? atomicAdd(a.list_count + (l * kListSegs + seg) * kListCountStride, tot) : 0u;
+    }
+    __syncthreads();
+    if (c != 1) {
+        const unsigned l = c == 2 ? 1u : 0u;
+        unsigned off = s_base[l] + (unsigned)__popcll((l ? bal1 : bal0) & ((1ull << lane) - 1ull));
+        for (int w = 0; w < wv; ++w) off += s_cnt[l][w];
+        a.unit_list[(size_t)l * kListSegs * seg_cap + seg * seg_cap + off] = u;
     }
 }
 
@@ -571,7 +622,7 @@ hipError_t launch_cull(const IntegrateArgs& a, hipStream_t s) {
 }
 
 uint64_t unit_count(const VolGeom& g) { return unit_grid(g).n; }
-uint64_t unit_list_capacity(const VolGeom& g) { return (uint64_t)list_seg_cap(unit_grid(g)) * kListSegs; }
+uint64_t unit_list_capacity(const VolGeom& g) { return (uint64_t)list_seg_cap(unit_grid(g)) * kListSegs * 2; }
 
 // Exact floor of the colour running mean (c*w + x) / (w + 1) for 0 <= c, x <= 255 and
 // w + 1 <= kRcpTable, from r = RN(1/(w+1)): floor(RN(num*r + 2^-12)) equals the integer
@@ -607,11 +658,11 @@ struct UnitPos {
 };
 
 __device__ __forceinline__ UnitPos unit_pos(const UnitGrid& ug, unsigned u) {
-    const unsigned uxy = u % (ug.nux * ug.nuy);
+    (void)ug;  // list entries are packed unit coordinates (pack_unit): bit-field extracts only
     UnitPos p;
-    p.x = (int)(uxy % ug.nux);
-    p.uy = (int)(uxy / ug.nux);
-    p.uz = (int)(u / (ug.nux * ug.nuy));
+    p.x = (int)(u & ((1u << kEntryXBits) - 1u));
+    p.uy = (int)((u >> kEntryXBits) & ((1u << kEntryYBits) - 1u));
+    p.uz = (int)(u >> (kEntryXBits + kEntryYBits));
     return p;
 }
 
@@ -682,7 +733,7 @@ struct Out {
 
 // Screen position s = M p + m (DESIGN.md §4 contract; per-row bases then one fma per
 // coordinate per voxel), the exact pixel through the reciprocal, and the record gather.
-template <bool SHARD, bool PIN>
+template <bool SHARD, bool PIN, bool FREE>
 __device__ __forceinline__ void stage_project(const IntegrateArgs& a, const UnitPos& up, int lane, Proj& P) {
     const VolGeom& g = a.g;
     const int npx = a.width * a.height;
@@ -739,15 +790,43 @@ __device__ __forceinline__ void stage_project(const IntegrateArgs& a, const Unit
     P.sflag = SEMTSDF_STEADY ? (unsigned)a.b.sflag[(unit_tile(g, up) + (unsigned)lane_zq(lane) * 32u +
                                                     (unsigned)lane_y(lane) * 4u) >> 5]
                              : 0u;
-    // unconditional gathers; an off-image voxel reads the zero record past the image (depth 0)
+    // unconditional gathers; an off-image voxel reads the zero record past the image (depth 0);
+    // a free unit needs only the depth word (touched <=> depth != 0, f == 1)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) P.rec[k] = a.pyr.px[(unsigned)P.img[k]];
+    for (int k = 0; k < 4; ++k) {
+        if (FREE)
+            P.rec[k] = make_uint2(reinterpret_cast<const unsigned*>(a.pyr.px)[2u * (unsigned)P.img[k]], 0u);
+        else
+            P.rec[k] = a.pyr.px[(kProbes && a.debug == 21) ? 0u : (unsigned)P.img[k]];  // 21: probe, one address
+#if SEMTSDF_PROBE_GATHER2
+        {  // timing probe: a second gather per voxel (no effect on results)
+            const uint2 extra = a.pyr.px[(unsigned)P.img[k] ^ 1u];
+            P.rec[k].y += (extra.x == 0x7fc00001u) ? 1u : 0u;
+        }
+#endif
+    }
 }
 
-template <bool SEM, bool GATE, bool VOTE, bool COUNT>
+template <bool SEM, bool GATE, bool VOTE, bool COUNT, bool FREE>
 __device__ __forceinline__ void stage_classify(const IntegrateArgs& a, const Proj& P, Cls& C, bool count,
                                                unsigned& n_touch, unsigned& n_gate) {
     const VolGeom& g = a.g;
+    if (FREE) {  // free unit (unit_cull == 2): a voxel with depth is touched with f == 1, never gated
+        unsigned tm = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            tm |= (P.rec[k].x != 0u ? 1u : 0u) << k;
+            C.fv[k] = 1.0f;
+            C.pix[k] = 0u;
+        }
+        C.sflag = P.sflag;
+        C.tmask = tm;
+        C.gmask = 0u;
+        C.hlab = 0xFFu;
+        C.hmode = 0u;
+        if (COUNT && count) n_touch += __popc(tm);
+        return;
+    }
     unsigned tmask = 0, dslow = 0;
     float dm[4];
 #pragma unroll
@@ -779,14 +858,14 @@ __device__ __forceinline__ void stage_classify(const IntegrateArgs& a, const Pro
         n_touch += __popc(tmask);
         n_gate += __popc(gmask);
     }
-    if (a.debug == 3) tmask = gmask = 0;  // timing probe: classification only, no state traffic
-    if (a.debug == 4) gmask = 0;          // timing probe: no colour/histogram traffic
+    if (kProbes && (a.debug == 3 || a.debug == 21)) tmask = gmask = 0;  // probe: classification only, no state traffic
+    if (kProbes && a.debug == 4) gmask = 0;          // timing probe: no colour/histogram traffic
     C.tmask = tmask;
     C.gmask = gmask;
     // histogram mode of the lane: the label of its first gated voxel, shared by all of them?
     C.hlab = 0xFFu;
     C.hmode = 0u;
-    if (SEM && gmask && a.debug != 6) {  // ~2/3 of the units have no gated lane: skipped
+    if (SEM && gmask && !(kProbes && a.debug == 6)) {  // ~2/3 of the units have no gated lane: skipped
         unsigned lab = 0xFFu, same = 1u;
 #pragma unroll
         for (int k = 3; k >= 0; --k) lab = ((gmask >> k) & 1u) ? (C.pix[k] >> 24) : lab;
@@ -861,7 +940,7 @@ __device__ __forceinline__ void st_state(void* p, const T& v) {
 
 // Unconditional loads: a lane with nothing to load reads the dummy line (one 16-B vector
 // shared by all such lanes), so the issue count is the same on every path.
-template <bool SEM, bool CI32, bool VOTE>
+template <bool SEM, bool CI32, bool VOTE, bool FREE>
 __device__ __forceinline__ void stage_load(const IntegrateArgs& a, const UnitPos& up, unsigned coff, const Cls& C,
                                            Ld& L) {
     const VolGeom& g = a.g;
@@ -882,6 +961,7 @@ __device__ __forceinline__ void stage_load(const IntegrateArgs& a, const UnitPos
     L.skip = skip;
     L.s4 = ld_state<float4>(skip ? reinterpret_cast<const float*>(dummy) : a.b.sdf + ub + lt);
     L.w4 = ld_state<int4>(a.b.wt + ub + lt);
+    if (FREE) return;  // sdf and weight only
     if (CI32) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) L.c32[k] = reinterpret_cast<const int4*>(a.b.color)[ub + lg + (gt ? k : 0)];
@@ -899,7 +979,7 @@ __device__ __forceinline__ void stage_load(const IntegrateArgs& a, const UnitPos
     }
 }
 
-template <bool SEM, bool GATE, bool CI32, bool VOTE>
+template <bool SEM, bool GATE, bool CI32, bool VOTE, bool FREE>
 __device__ __forceinline__ void stage_compute(const IntegrateArgs& a, const float* __restrict__ s_rcp, const Cls& C,
                                               const Ld& L, Out& O) {
     const unsigned tmask = C.tmask, gmask = C.gmask;
@@ -935,6 +1015,7 @@ __device__ __forceinline__ void stage_compute(const IntegrateArgs& a, const floa
 #pragma unroll
     for (int k = 0; k < 4; ++k) cross |= (so[k] < a.skip_thr) != (sn[k] < a.skip_thr);
     O.cross = cross;
+    if (FREE) return;  // no colour, histogram or vote state
     if (CI32) {  // unchanged lines of a stored row
 #pragma unroll
         for (int k = 0; k < 4; ++k) O.c32[k] = L.c32[k];
@@ -1009,7 +1090,7 @@ __device__ __forceinline__ void stage_compute(const IntegrateArgs& a, const floa
     }
 }
 
-template <bool SEM, bool CI32, bool VOTE>
+template <bool SEM, bool CI32, bool VOTE, bool FREE>
 __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPos& up, unsigned coff,
                                             const StoreMeta& M, const Out& O) {
     const VolGeom& g = a.g;
@@ -1033,7 +1114,7 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
                                     (unsigned)g.nbz) + (unsigned)bz] = 1;
         }
     }
-    if (a.debug != 10) {  // 10: timing probe, loads but no sdf/weight stores
+    if (!(kProbes && a.debug == 10)) {  // 10: timing probe, loads but no sdf/weight stores
         if (!O.skip) st_state(a.b.sdf + v, O.s4);
         st_state(a.b.wt + v, O.w4);
     }
@@ -1043,7 +1124,7 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
         const bool nflag = tile_line_all(one);
         if (lane_y((int)__lane_id()) == 0 && nflag != (O.oflag != 0u)) a.b.sflag[v >> 5] = nflag ? 1u : 0u;
     }
-    if (grow) {
+    if (!FREE && grow) {
         if (CI32) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) reinterpret_cast<int4*>(a.b.color)[v + k] = O.c32[k];
@@ -1081,32 +1162,26 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
             }
         }
     }
-    if (VOTE && tmask) {
+    if (!FREE && VOTE && tmask) {
         *reinterpret_cast<int4*>(a.b.cls + v) = O.vc4;
         *reinterpret_cast<int4*>(a.b.cls_cnt + v) = O.vn4;
     }
 }
 
-// Persistent wavefronts over the live-unit list: wave w takes entries w, w + nwaves, ...
-// (every wave gets the same number of units +-1), read with scalar loads one unit ahead.
-#ifndef SEMTSDF_INTEGRATE_WPE
-#define SEMTSDF_INTEGRATE_WPE 4  // waves per SIMD the register allocation targets (5 spills; measured equal)
-#endif
-template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT, bool SHARD, bool PIN>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_INTEGRATE_WPE))) void k_integrate(
-    IntegrateArgs a, UnitGrid ug,
-                                                                                          unsigned seg_cap) {
-    __shared__ float s_rcp[kRcpTable];
-    for (int i = (int)threadIdx.x; i < kRcpTable; i += (int)blockDim.x) s_rcp[i] = a.rcp_table[i];
-    __syncthreads();
+// One list of the frame (general or free units) by the persistent waves: wave w takes the
+// groups w', w' + nwaves, ... with w' = (w - rot) mod nwaves (rot balances the extra groups of
+// the two lists), a group being kSlots consecutive entries, one unit per slot.
+template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT, bool SHARD, bool PIN, bool FREE>
+__device__ __forceinline__ unsigned integrate_list(const IntegrateArgs& a, const UnitGrid& ug, unsigned seg_cap,
+                                                   const float* __restrict__ s_rcp, const unsigned* list,
+                                                   const unsigned* list_count, unsigned wave, unsigned nwaves,
+                                                   unsigned rot, unsigned& n_touch, unsigned& n_gate) {
     const int lane = threadIdx.x & 63;
     // the lane's offset from the unit origin (a volume has < 2^31 stored voxels per x-plane pair)
     const unsigned coff = (unsigned)lane_zq(lane) * 32u + (unsigned)lane_y(lane) * 4u;  // lane's offset in its unit
-    const unsigned wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
-    const unsigned nwaves = gridDim.x * (blockDim.x >> 6);
     // segment counts, one per lane; inclusive prefix over the lanes (kListSegs == 64)
     static_assert(kListSegs == 64, "one list segment per lane");
-    const unsigned cnt_l = a.list_count[lane * kListCountStride];
+    const unsigned cnt_l = list_count[lane * kListCountStride];
     unsigned incl = cnt_l;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -1114,16 +1189,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_INT
         if (lane >= off) incl += o;
     }
     const unsigned total = __builtin_amdgcn_readfirstlane((unsigned)__shfl((int)incl, 63, 64));
-    unsigned n_touch = 0, n_gate = 0;
     auto entry = [&](unsigned i) -> unsigned {  // i < total: segment = number of segments ending at or before i
         const unsigned seg = (unsigned)__popcll(__ballot(incl <= i));
         const unsigned before = seg ? __builtin_amdgcn_readfirstlane((unsigned)__shfl((int)incl, (int)seg - 1, 64)) : 0u;
         const unsigned off = i - before;
         // constant address space: the list is read-only here, so this is a scalar load
         // (s_load, lgkmcnt) and never waits behind the wave's vector memory operations
-        const __attribute__((address_space(4))) unsigned* list =
-            (const __attribute__((address_space(4))) unsigned*)a.unit_list;
-        return list[seg * seg_cap + off];
+        const __attribute__((address_space(4))) unsigned* l4 = (const __attribute__((address_space(4))) unsigned*)list;
+        return l4[seg * seg_cap + off];
     };
     // group k of the list = entries k*kSlots .. k*kSlots+kSlots-1, one unit per slot of the wave
     const unsigned ngroups = (total + kSlots - 1) / kSlots;
@@ -1148,7 +1221,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_INT
         }
         return p;
     };
-    unsigned i = wave;
+    unsigned i = (wave + nwaves - rot % nwaves) % nwaves;
     if (i < ngroups) {
         unsigned e[kSlots], en[kSlots];
         group_entries(i, e);
@@ -1158,27 +1231,57 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_INT
         Cls C;
         Ld L;
         Out O;
-        stage_project<SHARD, PIN>(a, cur, lane, P);
-        stage_classify<SEM, GATE, VOTE, COUNT>(a, P, C, true, n_touch, n_gate);
-        stage_load<SEM, CI32, VOTE>(a, cur, coff, C, L);
+        stage_project<SHARD, PIN, FREE>(a, cur, lane, P);
+        stage_classify<SEM, GATE, VOTE, COUNT, FREE>(a, P, C, true, n_touch, n_gate);
+        stage_load<SEM, CI32, VOTE, FREE>(a, cur, coff, C, L);
         while (true) {
             const bool has = i + nwaves < ngroups;
             // the last iteration projects a copy of the current units, so the memory
             // operations issued per iteration do not depend on the branch
             const UnitPos nxt = has ? lane_pos(en) : cur;
             if (i + 2u * nwaves < ngroups) group_entries(i + 2u * nwaves, en);
-            stage_project<SHARD, PIN>(a, nxt, lane, P);
-            if (SEMTSDF_FULLROW || C.tmask) stage_compute<SEM, GATE, CI32, VOTE>(a, s_rcp, C, L, O);
+            stage_project<SHARD, PIN, FREE>(a, nxt, lane, P);
+            if (SEMTSDF_FULLROW || C.tmask) stage_compute<SEM, GATE, CI32, VOTE, FREE>(a, s_rcp, C, L, O);
             const StoreMeta Mc = store_meta(C);
-            stage_classify<SEM, GATE, VOTE, COUNT>(a, P, C, has, n_touch, n_gate);
-            stage_store<SEM, CI32, VOTE>(a, cur, coff, Mc, O);
+            stage_classify<SEM, GATE, VOTE, COUNT, FREE>(a, P, C, has, n_touch, n_gate);
+            stage_store<SEM, CI32, VOTE, FREE>(a, cur, coff, Mc, O);
             if (!has) break;
-            stage_load<SEM, CI32, VOTE>(a, nxt, coff, C, L);
+            stage_load<SEM, CI32, VOTE, FREE>(a, nxt, coff, C, L);
             cur = nxt;
             i += nwaves;
         }
     }
+    return total;
+}
+
+// Persistent wavefronts over the two live-unit lists of the frame: the free units first
+// (sdf/weight only, when the mode allows them), then the general units.
+#ifndef SEMTSDF_INTEGRATE_WPE
+#define SEMTSDF_INTEGRATE_WPE 4  // waves per SIMD the register allocation targets (5 spills; measured equal)
+#endif
+template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT, bool SHARD, bool PIN>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_INTEGRATE_WPE))) void k_integrate(
+    IntegrateArgs a, UnitGrid ug, unsigned seg_cap) {
+    __shared__ float s_rcp[kRcpTable];
+    for (int i = (int)threadIdx.x; i < kRcpTable; i += (int)blockDim.x) s_rcp[i] = a.rcp_table[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const unsigned wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+    const unsigned nwaves = gridDim.x * (blockDim.x >> 6);
+    unsigned n_touch = 0, n_gate = 0;
+    unsigned rot = 0, nlive = 0;
+    if (GATE && !VOTE) {  // free units exist only in gated modes (free_ok)
+        const unsigned n1 = integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, true>(
+            a, ug, seg_cap, s_rcp, a.unit_list + (size_t)kListSegs * seg_cap, a.list_count + kListSegs * kListCountStride,
+            wave, nwaves, 0u, n_touch, n_gate);
+        rot = (n1 + kSlots - 1) / kSlots % nwaves;
+        if (COUNT && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.counters + 4, (unsigned long long)n1);
+        if (COUNT) nlive += n1;
+    }
+    const unsigned n0 = integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, false>(
+        a, ug, seg_cap, s_rcp, a.unit_list, a.list_count, wave, nwaves, rot, n_touch, n_gate);
     if (COUNT) {
+        nlive += n0;
         unsigned long long t = n_touch, gg = n_gate;
         for (int off = 32; off > 0; off >>= 1) {
             t += __shfl_xor(t, off, 64);
@@ -1188,7 +1291,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_INT
             if (t) atomicAdd(a.counters + 0, t);
             if (gg) atomicAdd(a.counters + 1, gg);
         }
-        if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.counters + 3, (unsigned long long)total);
+        // live units of both lists
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.counters + 3, (unsigned long long)nlive);
     }
 }
 
@@ -1220,7 +1324,7 @@ static hipError_t launch_integrate_k(const IntegrateArgs& a, hipStream_t s, hipE
     static const unsigned grid0 = resident_grid(k_integrate<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>);
     const unsigned ncu = resident_grid_cus();
     unsigned grid = grid0;
-    if (a.debug >= 100) grid = grid0 * (unsigned)(a.debug - 100) / 8u;  // probe: fraction of residency
+    if (kProbes && a.debug >= 100) grid = grid0 * (unsigned)(a.debug - 100) / 8u;  // probe: fraction of residency
     static const char* gpc = getenv("SEMTSDF_GRID_PER_CU");              // probe: blocks per CU
     if (gpc && atoi(gpc) > 0) grid = ncu * (unsigned)atoi(gpc);
     if (e0) {  // timing: events recorded by the dispatch itself (kernel start / end)

@@ -105,6 +105,7 @@ class Timing(C.Structure):
         ("bricks", C.c_uint64),
         ("prep_ms", C.c_double),
         ("n_prep", C.c_uint64),
+        ("free_units", C.c_uint64),
     ]
 
 

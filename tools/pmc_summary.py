@@ -7,7 +7,7 @@ import sys
 
 d = sys.argv[1]
 pat = sys.argv[2] if len(sys.argv) > 2 else "k_integrate<true, true, false, false, false, false, true>"
-for f in sorted(glob.glob(f"{d}/p*/run_counter_collection.csv")):
+for f in sorted(glob.glob(f"{d}/[pe]*/run_counter_collection.csv")):
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
         if pat in r["Kernel_Name"]:
