@@ -66,6 +66,8 @@ def lib():
         _lib.oracle_place.restype = C.c_int
         _lib.oracle_orbit_camera.argtypes = [P, C.c_float, C.c_float, P, P]
         _lib.oracle_orbit_camera.restype = None
+        _lib.oracle_project.argtypes = [P, P, P, P, C.c_int, C.c_int, P, C.c_int, C.c_int]
+        _lib.oracle_project.restype = None
     return _lib
 
 
@@ -130,6 +132,36 @@ def integrate(g: OGeom, st: OState, K16, E16, depth, rgb, mask=None, cls=None, f
                            _p(None if cls is None else np.ascontiguousarray(cls, np.int32)), x0, x1, _p(counts),
                            _p(zm), 0 if zm is None else int(zm.size))
     return counts
+
+
+def project(g: OGeom, K16, E16, W, H, x_range=None):
+    """Pixel index (y*W + x, -1 off-image) of every voxel under the f32 contract."""
+    x0, x1 = (0, int(g.dims[0])) if x_range is None else x_range
+    out = np.full(int(np.prod(g.dims)), -1, np.int32)
+    lib().oracle_project(_p(g.dims), _p(g.geo), _p(k9(K16)), _p(np.ascontiguousarray(E16, np.float32).reshape(16)),
+                         int(W), int(H), _p(out), x0, x1)
+    return out
+
+
+def numpy_pixels(vol_dim, vol_start, voxel, K, E, W, H, n_flat=None):
+    """Pixel index (-1 where rejected) of every flat voxel under the float64 reference block
+    (tsdf.py:86-97: f64 pose, f32 K, truncation toward zero, bounds on the truncated value)."""
+    D = int(vol_dim)
+    n = D ** 3 if n_flat is None else int(n_flat)
+    flat = np.arange(n, dtype=np.int64)
+    xi = flat // (D * D)
+    yi = flat // D - xi * D
+    zi = flat % D
+    vs = np.asarray(vol_start, np.float64)
+    vx = np.asarray(voxel, np.float64) * np.ones(3)
+    pos = np.stack([vs[0] + xi * vx[0], vs[1] + yi * vx[1], vs[2] + zi * vx[2], np.ones(n)], axis=0)
+    proj = np.dot(np.asarray(E, np.float64), pos)
+    pixel = np.dot(np.asarray(K, np.float32), proj)
+    pixel /= pixel[2, :]
+    px = pixel[0].astype(np.int64)
+    py = pixel[1].astype(np.int64)
+    ok = (px >= 0) & (px <= W - 1) & (py >= 0) & (py <= H - 1)
+    return np.where(ok, py * W + px, -1)
 
 
 def march_probs(g: OGeom, Kinv16, E16, W, H, sdf, hist, box_thresh=0.3):

@@ -12,6 +12,7 @@
  * Followed reference locations:
  *   oracle_integrate         src/SfM_CUDA/tsdf.cu:18-70 (histogram, gate) and
  *                            src/TSDF_Python/tsdf.cu:10-58 (i32 colour ungated, label vote)
+ *   oracle_project           the pixel choice of oracle_integrate (tsdf.cu:30-44)
  *   oracle_march_probs       src/SfM_CUDA/tsdf.cu:72-135, utils.cu:93-119,144-170
  *   oracle_filter_overlaps   src/SfM_CUDA/tsdf.cu:304-416 (+ configuration.h:8)
  *   oracle_render            src/SfM_CUDA/viewer.cu:17-86, palette viewer.cu:93-126
@@ -158,6 +159,38 @@ void oracle_integrate(const int32_t* dims, const float* geo, const float* K9, co
         }
     }
     if (counts) { counts[0] += n_touch; counts[1] += n_gate; counts[2] += n_bad; }
+}
+
+/* Pixel each voxel of x-planes [x_begin, x_end) projects to under the same f32 contract as
+ * oracle_integrate (y*width + x, or -1 off-image), flat x-major: tests use it to find the
+ * voxels whose f32 pixel choice differs from the float64 reference block (tsdf.py:86-97). */
+void oracle_project(const int32_t* dims, const float* geo, const float* K9, const float* E16, int width, int height,
+                    int32_t* img_out, int x_begin, int x_end) {
+    const ogeom g = mk_geom(dims, geo);
+    float M[9], m[3];
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j)
+            M[i * 3 + j] = (float)((double)K9[i * 3 + 0] * (double)E16[0 * 4 + j] +
+                                   (double)K9[i * 3 + 1] * (double)E16[1 * 4 + j] +
+                                   (double)K9[i * 3 + 2] * (double)E16[2 * 4 + j]);
+        m[i] = (float)((double)K9[i * 3 + 0] * (double)E16[3] + (double)K9[i * 3 + 1] * (double)E16[7] +
+                       (double)K9[i * 3 + 2] * (double)E16[11]);
+    }
+    for (int x = x_begin; x < x_end; ++x) {
+        const float px = fmaf((float)x, g.voxel[0], g.start[0]);
+        for (int y = 0; y < g.dy; ++y) {
+            const float py = fmaf((float)y, g.voxel[1], g.start[1]);
+            for (int z = 0; z < g.dz; ++z) {
+                const float pz = fmaf((float)z, g.voxel[2], g.start[2]);
+                const float sx = fmaf(M[2], pz, fmaf(M[1], py, fmaf(M[0], px, m[0])));
+                const float sy = fmaf(M[5], pz, fmaf(M[4], py, fmaf(M[3], px, m[1])));
+                const float sz = fmaf(M[8], pz, fmaf(M[7], py, fmaf(M[6], px, m[2])));
+                const int ix = o_f2i_rd(sx / sz), iy = o_f2i_rd(sy / sz);
+                const size_t v = ((size_t)x * g.dy + y) * g.dz + z;
+                img_out[v] = (ix < 0 || ix >= width || iy < 0 || iy >= height) ? -1 : iy * width + ix;
+            }
+        }
+    }
 }
 
 /* ---------------------------------------------------------------- trilinear samplers */

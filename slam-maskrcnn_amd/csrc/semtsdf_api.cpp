@@ -405,6 +405,35 @@ int check_bad_label(semtsdf_vol* v, hipStream_t s) {
 
 }  // namespace
 
+namespace {
+// Contiguous runs of the flat x-major D^3 array whose voxels have a coordinate >= d8.
+template <class F>
+void for_tail_runs(int D, int d8, F&& f) {
+    const size_t D2 = (size_t)D * D;
+    for (int x = 0; x < D; ++x) {
+        if (x >= d8) { f((size_t)x * D2, D2); continue; }
+        for (int y = 0; y < D; ++y) {
+            const size_t row = (size_t)x * D2 + (size_t)y * D;
+            if (y >= d8) f(row, (size_t)D);
+            else if (D > d8) f(row + d8, (size_t)(D - d8));
+        }
+    }
+}
+template <class T>
+void tail_save(const T* a, int comps, int D, int d8, std::vector<T>& buf) {
+    buf.clear();
+    for_tail_runs(D, d8, [&](size_t off, size_t n) { buf.insert(buf.end(), a + off * comps, a + (off + n) * comps); });
+}
+template <class T>
+void tail_restore(T* a, int comps, int D, int d8, const std::vector<T>& buf) {
+    size_t k = 0;
+    for_tail_runs(D, d8, [&](size_t off, size_t n) {
+        std::copy(buf.begin() + k, buf.begin() + k + n * comps, a + off * comps);
+        k += n * comps;
+    });
+}
+}  // namespace
+
 // =====================================================================================
 extern "C" {
 
@@ -1266,9 +1295,12 @@ int semtsdf_upload(semtsdf_vol* v, const float* sdf, const int32_t* wt, const vo
     HIPC(hipSetDevice(v->device));
     hipStream_t s = v->stream;
     int rc;
+    // derived maps first: a transfer that fails half-way must not leave steady flags or an
+    // empty-space map that describe the old contents (0 = unknown is always safe)
+    v->bmin_stale = true;
+    if (sdf || wt) HIPC(hipMemsetAsync(v->b.sflag, 0, v->g.nvox / 32 + 1, s));  // steady flags: unknown
     if (sdf && (rc = vox_xfer(v, const_cast<float*>(sdf), v->b.sdf, false, "sdf", s))) return rc;
     if (wt && (rc = vox_xfer(v, const_cast<int32_t*>(wt), v->b.wt, false, "weight", s))) return rc;
-    if (sdf || wt) HIPC(hipMemsetAsync(v->b.sflag, 0, v->g.nvox / 32 + 1, s));  // steady flags: unknown
     if (color) {
         rc = color_xfer(v, const_cast<void*>(color), false, s);
         if (rc) return rc;
@@ -1283,6 +1315,8 @@ int semtsdf_upload(semtsdf_vol* v, const float* sdf, const int32_t* wt, const vo
     }
     if (hist) {
         if (!(v->p.flags & SEMTSDF_F_SEMANTIC)) return fail(SEMTSDF_ERR_STATE, "not a SEMANTIC volume");
+        // bin mask "every bin may be present" until it is rebuilt from the new histogram
+        HIPC(hipMemsetAsync(v->b.hmask, 0xFF, v->g.nvox * 4, s));
         const uint64_t n = (uint64_t)v->g.dimx * v->g.dimy * v->g.lz;
         const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(n, 1ull << 22));
         uint32_t* stage = nullptr;
@@ -1366,8 +1400,12 @@ int semtsdf_reset_timing(semtsdf_vol* v) {
 }
 
 // Drop-in for tsdf_cuda.tsdf_update: whole-volume in, kernel, whole-volume out, like the
-// reference (TSDF_Python/tsdf.cu:78-112), but with a cached device volume instead of a
-// fresh thrust allocation per call.
+// reference (TSDF_Python/tsdf.cu:78-112), but with a device volume cached across calls
+// (recreated, and re-validated by semtsdf_create, whenever an argument that shapes it
+// changes: vol_dim, vol_start, voxel, miu, intrinsic, frame size or the current device).
+// The reference launches (vol_dim/8)^3 blocks of 8^3 threads with no bounds check
+// (TSDF_Python/tsdf.cu:90), so voxels with a coordinate >= 8*(vol_dim/8) are never updated;
+// they are kept unchanged here as well.
 int semtsdf_tsdf_update(float* tsdf_diff, int32_t* tsdf_color, int32_t* tsdf_wt, int32_t* tsdf_cls,
                         int32_t* tsdf_cls_cnt, int vol_dim, const float* vol_start, float voxel, float miu,
                         const float* intrinsic, const uint16_t* depth, const uint8_t* color, const int32_t* cls,
@@ -1375,9 +1413,14 @@ int semtsdf_tsdf_update(float* tsdf_diff, int32_t* tsdf_color, int32_t* tsdf_wt,
     if (!tsdf_diff || !tsdf_color || !tsdf_wt || !tsdf_cls || !tsdf_cls_cnt || !vol_start || !intrinsic || !depth ||
         !color || !cls || !extrinsic2init)
         return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    if (vol_dim < 2) return fail(SEMTSDF_ERR_INVALID, "vol_dim=%d", vol_dim);
+    const int d8 = vol_dim / 8 * 8;  // (vol_dim/8)^3 blocks of 8^3 voxels
+    if (d8 == 0) return SEMTSDF_OK;  // the reference launches no block
     static std::mutex mu_cache;
     static semtsdf_vol* cache = nullptr;
     std::lock_guard<std::mutex> lock(mu_cache);
+    int device = 0;
+    HIPC(hipGetDevice(&device));
     semtsdf_params p{};
     const float intr[4] = {intrinsic[0], intrinsic[5], intrinsic[2], intrinsic[6]};
     int rc = semtsdf_params_default(&p, vol_dim, intr, width, height);
@@ -1390,18 +1433,24 @@ int semtsdf_tsdf_update(float* tsdf_diff, int32_t* tsdf_color, int32_t* tsdf_wt,
     }
     p.mu = miu;
     p.flags = SEMTSDF_F_VOTE | SEMTSDF_F_COLOR_I32;
-    if (cache && (cache->p.dim[0] != vol_dim || cache->p.width != width || cache->p.height != height)) {
+    if (cache && (memcmp(&cache->p, &p, sizeof(p)) != 0 || cache->device != device)) {
         semtsdf_destroy(cache);
         cache = nullptr;
     }
     if (!cache) {
-        rc = semtsdf_create(&p, 0, &cache);
+        rc = semtsdf_create(&p, device, &cache);  // check_params validates the new arguments
         if (rc) return rc;
     }
     semtsdf_vol* v = cache;
-    v->p = p;
-    for (int i = 0; i < 3; ++i) { v->g.start[i] = p.vol_start[i]; v->g.voxel[i] = p.voxel[i]; v->g.end[i] = p.vol_end[i]; }
-    v->g.mu = p.mu;
+    std::vector<float> t_sdf;
+    std::vector<int32_t> t_col, t_wt, t_cls, t_cnt;
+    if (d8 < vol_dim) {
+        tail_save(tsdf_diff, 1, vol_dim, d8, t_sdf);
+        tail_save(tsdf_color, 3, vol_dim, d8, t_col);
+        tail_save(tsdf_wt, 1, vol_dim, d8, t_wt);
+        tail_save(tsdf_cls, 1, vol_dim, d8, t_cls);
+        tail_save(tsdf_cls_cnt, 1, vol_dim, d8, t_cnt);
+    }
     rc = semtsdf_upload(v, tsdf_diff, tsdf_wt, tsdf_color, nullptr, tsdf_cls, tsdf_cls_cnt);
     if (rc) return rc;
     const size_t n = npx(v);
@@ -1411,7 +1460,16 @@ int semtsdf_tsdf_update(float* tsdf_diff, int32_t* tsdf_color, int32_t* tsdf_wt,
     HIPC(hipMemcpyAsync(v->cls_d, cls, n * 4, hipMemcpyHostToDevice, s));
     rc = integrate_impl(v, v->depth_d, v->rgb_d, nullptr, v->cls_d, extrinsic2init, s);
     if (rc) return rc;
-    return semtsdf_download(v, tsdf_diff, tsdf_wt, tsdf_color, nullptr, tsdf_cls, tsdf_cls_cnt);
+    rc = semtsdf_download(v, tsdf_diff, tsdf_wt, tsdf_color, nullptr, tsdf_cls, tsdf_cls_cnt);
+    if (rc) return rc;
+    if (d8 < vol_dim) {
+        tail_restore(tsdf_diff, 1, vol_dim, d8, t_sdf);
+        tail_restore(tsdf_color, 3, vol_dim, d8, t_col);
+        tail_restore(tsdf_wt, 1, vol_dim, d8, t_wt);
+        tail_restore(tsdf_cls, 1, vol_dim, d8, t_cls);
+        tail_restore(tsdf_cls_cnt, 1, vol_dim, d8, t_cnt);
+    }
+    return SEMTSDF_OK;
 }
 
 }  // extern "C"

@@ -53,7 +53,9 @@ def parse_extrinsic(pos) -> np.ndarray:
 
 
 def transform44(l) -> np.ndarray:
-    """tsdf_utils.py:32-61 (TUM benchmark formula), returning the inverse (W2C)."""
+    """tsdf_utils.py:32-61 (TUM benchmark formula), returning the inverse (W2C) -- except
+    for a near-zero quaternion, where the reference returns the translation matrix itself,
+    un-inverted (tsdf_utils.py:46-52), and so does this."""
     l = np.asarray(l, dtype=np.float64)
     t = l[:3]
     q = np.array(l[3:7], dtype=np.float64, copy=True)
@@ -61,7 +63,7 @@ def transform44(l) -> np.ndarray:
     if nq < 1e-7:
         m = np.eye(4)
         m[:3, 3] = t
-        return np.linalg.inv(m)
+        return m
     q *= math.sqrt(2.0 / nq)
     q = np.outer(q, q)
     m = np.array(
@@ -98,12 +100,12 @@ def slerp(q1, q2, t: float) -> np.ndarray:
 
 def interpolate_pose(traj: np.ndarray, ts: float) -> np.ndarray:
     """TSDF_Python/main.py:127-140: lerp translation + slerp rotation between the bracketing
-    trajectory rows (first row with time >= ts and its predecessor)."""
+    trajectory rows (first row with time >= ts and its predecessor).  As in the reference,
+    a first row at or after ts pairs with row -1 (Python's last row), which passes the
+    main.py:134 assertion only when ts equals the first time stamp."""
     for k in range(traj.shape[0]):
         if traj[k, 0] < ts:
             continue
-        if k == 0:
-            return traj[0, 1:].copy()
         t = (ts - traj[k - 1, 0]) / (traj[k, 0] - traj[k - 1, 0])
         assert 0 <= t <= 1  # main.py:134
         return np.concatenate(

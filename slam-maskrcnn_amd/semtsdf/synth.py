@@ -116,7 +116,15 @@ class SyntheticStream:
         for lab, n in enumerate(order, start=1):
             mask[gt == n] = lab
         w2c = np.linalg.inv(c2w)
-        return Frame(depth, np.ascontiguousarray(rgb), mask, gt, c2w, w2c, float(k) * 0.033)
+        return Frame(depth, np.ascontiguousarray(rgb), mask, gt, c2w, w2c, self.stamp(k))
+
+    # TUM stamps of the fr2 sequences (1311868164.xxxx); the reference drivers drop the first
+    # five characters (kernel.cpp:53, tsdf_utils.py:27), leaving 68164.xxxx
+    STAMP0 = 1311868164.0
+
+    def stamp(self, k: int) -> float:
+        return self.STAMP0 + 0.033 * k
 
     def tum_lines(self, n: int) -> list[str]:
-        return [P.c2w_to_tum(68164.0 + 0.033 * k, self.c2w(k)) for k in range(n)]
+        """groundtruth.txt lines (camera-to-world) of frames 0..n-1, '# ...' header first."""
+        return ["# timestamp tx ty tz qx qy qz qw"] + [P.c2w_to_tum(self.stamp(k), self.c2w(k)) for k in range(n)]

@@ -14,6 +14,8 @@ Differences from the reference, by design:
 """
 from __future__ import annotations
 
+import dataclasses
+import json
 import math
 
 import numpy as np
@@ -227,17 +229,30 @@ class TSDF:
         vote = bool(v.params.flags & L.F_VOTE)
         data = v.download(hist=sem, cls=vote)
         st = v.state()
+        # every field of the volume's semtsdf_params (placement, intrinsics and their inverse,
+        # frame size, thresholds, knobs, flags, shard), so a reloaded volume integrates,
+        # associates and renders exactly like the saved one
+        params = {f"p_{name}": np.array(getattr(v.params, name)[:] if hasattr(getattr(v.params, name), "__len__")
+                                        else getattr(v.params, name)) for name, _ in L.Params._fields_}
         np.savez_compressed(
             path, vol_start=np.asarray(self.vol_start, np.float64), vol_end=np.asarray(self.vol_end, np.float64),
             voxel=np.asarray(self.voxel, np.float64), mu=np.float64(self.mu), vol_dim=np.int64(self.vol_dim),
             n_obs=np.int64(st.n_obs), num_objs=np.int64(st.num_objs), N=np.int64(self.N),
             mean_depth=np.float64(self.mean_depth), init_extrinsic_inv=self.init_extrinsic_inv,
-            intrinsic=self.intrinsic, flags=np.int64(v.params.flags), **data)
+            intrinsic=self.intrinsic, intrinsic_inv=np.asarray(self.intrinsic_inv), flags=np.int64(v.params.flags),
+            config=np.str_(json.dumps(dataclasses.asdict(self.config))), **params, **data)
 
     @classmethod
     def load(cls, path: str, config: FusionConfig | None = None, device: int = 0) -> "TSDF":
+        """Restores a checkpoint written by save(): the volume's full parameter block (not the
+        defaults), the host attributes and the configuration it was saved with (`config`, if
+        given, overrides the saved one for future host-side choices only)."""
         z = np.load(path, allow_pickle=False)
         K = z["intrinsic"]
+        if config is None and "config" in z:
+            d = json.loads(str(z["config"]))
+            d["intrinsics"] = tuple(d["intrinsics"])
+            config = FusionConfig(**d)
         t = cls((float(K[0, 0]), float(K[1, 1]), float(K[0, 2]), float(K[1, 2])), int(z["vol_dim"]), config, device)
         t.init = True
         t.vol_start, t.vol_end, t.voxel = z["vol_start"], z["vol_end"], z["voxel"]
@@ -245,13 +260,22 @@ class TSDF:
         t.mean_depth = float(z["mean_depth"])
         t.init_extrinsic_inv = z["init_extrinsic_inv"]
         t.N = int(z["N"])
-        W = t.config.width
-        H = t.config.height
-        p = default_params(t.vol_dim, t.config.intrinsics, W, H)
-        for i in range(3):
-            p.vol_start[i], p.vol_end[i], p.voxel[i] = t.vol_start[i], t.vol_end[i], t.voxel[i]
-        p.mu = t.mu
-        p.flags = int(z["flags"])
+        if "intrinsic_inv" in z:
+            t.intrinsic_inv = z["intrinsic_inv"]
+        p = L.Params()
+        if "p_flags" in z:
+            for name, ctype in L.Params._fields_:
+                val = z[f"p_{name}"]
+                if hasattr(getattr(p, name), "__len__"):
+                    getattr(p, name)[:] = [x.item() for x in val.reshape(-1)]
+                else:
+                    setattr(p, name, val.item())
+        else:  # checkpoints of ABI 2: geometry and flags only, defaults for the rest
+            p = default_params(t.vol_dim, t.config.intrinsics, t.config.width, t.config.height)
+            for i in range(3):
+                p.vol_start[i], p.vol_end[i], p.voxel[i] = t.vol_start[i], t.vol_end[i], t.voxel[i]
+            p.mu = t.mu
+            p.flags = int(z["flags"])
         t.vol = Volume(p, device)
         t.vol.upload(sdf=z["sdf"], wt=z["wt"], color=z["color"], hist=z["hist"] if "hist" in z else None,
                      cls=z["cls"] if "cls" in z else None, cls_cnt=z["cls_cnt"] if "cls_cnt" in z else None)

@@ -68,9 +68,15 @@ def stamp_of(fn: str, as_float32: bool) -> float:
 
 
 def mean_depth_m(depth: np.ndarray, depth_scale: float = 5000.0) -> float:
-    """utils.cu:77-91: mean of d/5000 over d > 0, accumulated in float64, returned float32."""
-    d = depth[depth > 0].astype(np.float64)
-    return float(np.float32((d / depth_scale).sum() / d.size))
+    """utils.cu:77-91: `sum += ptr[i] / 5000.` over the nonzero pixels in pixel order (double,
+    left to right), divided by their count, returned as float32 (NaN for an all-zero frame,
+    the reference's 0/0)."""
+    d = np.asarray(depth).reshape(-1)
+    d = d[d > 0].astype(np.float64) / depth_scale
+    if d.size == 0:
+        return float("nan")
+    s = float(np.cumsum(d)[-1])  # sequential accumulation, as the C loop (not pairwise)
+    return float(np.float32(s / d.size))
 
 
 def mean_depth_raw(depth: np.ndarray) -> float:
@@ -85,26 +91,20 @@ class FrameRef:
     mask_fn: str | None
     ts: float
     pose: np.ndarray  # [tx ty tz qx qy qz qw]
+    i: int = -1       # depth index
+    j: int = -1       # mask (sfm) / rgb (python) index
 
 
-def associate(root: str, mode: str = "sfm", begin: float = 68164.0, end: float = 68170.0,
-              max_frames: int = 100) -> list[FrameRef]:
-    """Frame list of a TUM directory `root` with rgb/, depth/, mask/ and groundtruth.txt."""
-    rgb_fn = sorted(glob.glob(os.path.join(root, "rgb", "*.png")))
-    depth_fn = sorted(glob.glob(os.path.join(root, "depth", "*.png")))
-    mask_fn = sorted(glob.glob(os.path.join(root, "mask", "*.png")))
-    gt = os.path.join(root, "groundtruth.txt")
-    f32 = mode == "sfm"
-    dts = [stamp_of(f, f32) for f in depth_fn]
-    pair_fn = mask_fn if mode == "sfm" else rgb_fn
-    pts = [stamp_of(f, f32) for f in pair_fn]
-    out: list[FrameRef] = []
-    if mode == "sfm":
-        traj_map = read_trajactory(gt)
-    else:
-        traj = read_traj(gt)
-    i, j = 0, 0
-    while i < len(dts):
+def _pairs_sfm(dts, pts, begin, end, max_frames):
+    """kernel.cpp:64-74: one index i that the inner loops advance (the for-loop's i++ keeps
+    them), frames counted before the cap `cnt > 100`."""
+    out = []
+    j = 0
+    i = 0
+    cnt = 0
+    while i < 10000:
+        if i >= len(dts):
+            break
         if dts[i] < begin or dts[i] > end:
             i += 1
             continue
@@ -113,17 +113,71 @@ def associate(root: str, mode: str = "sfm", begin: float = 68164.0, end: float =
         while i < len(dts) and j < len(pts) and pts[j] < dts[i]:
             j += 1
         if i >= len(dts) or j >= len(pts):
+            break  # the reference reads past the end here
+        cnt += 1
+        if cnt > max_frames:
             break
-        ts = dts[i]
-        if mode == "sfm":
-            pose = np.array(lower_bound_pose(traj_map, ts), dtype=np.float64)
-            out.append(FrameRef(depth_fn[i], rgb_fn[j] if j < len(rgb_fn) else "", mask_fn[j], ts, pose))
-        else:
-            pose = P.interpolate_pose(traj, ts)
-            out.append(FrameRef(depth_fn[i], rgb_fn[j], mask_fn[j] if j < len(mask_fn) else None, ts, pose))
-        if len(out) >= max_frames:
-            break
+        out.append((i, j))
         i += 1
+    return out
+
+
+def _pairs_python(dts, pts, begin, end, max_frames):
+    """main.py:83-91: `for i in range(3000)` rebinds i every iteration, so the inner loops'
+    advances do not carry over and a depth frame can be processed more than once."""
+    out = []
+    j = 0
+    for i0 in range(3000):
+        i = i0
+        if i >= len(dts):
+            break
+        if dts[i] < begin or dts[i] > end:
+            continue
+        while i < len(dts) and j < len(pts) and dts[i] < pts[j]:
+            i += 1
+        while i < len(dts) and j < len(pts) and pts[j] < dts[i]:
+            j += 1
+        if i >= len(dts) or j >= len(pts):
+            break  # the reference raises IndexError here
+        out.append((i, j))
+        if max_frames is not None and len(out) >= max_frames:
+            break
+    return out
+
+
+def associate(root: str, mode: str = "sfm", begin: float | None = None, end: float | None = None,
+              max_frames: int | None = None) -> list[FrameRef]:
+    """Frame list of a TUM directory `root` with rgb/, depth/, mask/ and groundtruth.txt.
+
+    mode "sfm"    (kernel.cpp:44-99): float32 time stamps, depth i paired with the first
+                  mask j whose stamp is >= the depth stamp, rgb by the mask index, pose =
+                  lower_bound of fmod(ts, 1e5) (no interpolation); window [68164, 68170],
+                  at most 100 frames.
+    mode "python" (main.py:59-142): float64 stamps, depth paired with rgb, mask by the rgb
+                  index, pose lerp/slerp-interpolated; window [68164, 68164.37], no cap."""
+    if mode not in ("sfm", "python"):
+        raise ValueError(f"mode must be 'sfm' or 'python', got {mode!r}")
+    sfm = mode == "sfm"
+    begin = (68164.0 if begin is None else begin)
+    end = (68170.0 if sfm else 68164.37) if end is None else end
+    rgb_fn = sorted(glob.glob(os.path.join(root, "rgb", "*.png")))
+    depth_fn = sorted(glob.glob(os.path.join(root, "depth", "*.png")))
+    mask_fn = sorted(glob.glob(os.path.join(root, "mask", "*.png")))
+    gt = os.path.join(root, "groundtruth.txt")
+    dts = [stamp_of(f, sfm) for f in depth_fn]
+    pair_fn = mask_fn if sfm else rgb_fn
+    pts = [stamp_of(f, sfm) for f in pair_fn]
+    out: list[FrameRef] = []
+    if sfm:
+        traj_map = read_trajactory(gt)
+        for i, j in _pairs_sfm(dts, pts, begin, end, 100 if max_frames is None else max_frames):
+            pose = np.array(lower_bound_pose(traj_map, dts[i]), dtype=np.float64)
+            out.append(FrameRef(depth_fn[i], rgb_fn[j] if j < len(rgb_fn) else "", mask_fn[j], dts[i], pose, i, j))
+    else:
+        traj = read_traj(gt)
+        for i, j in _pairs_python(dts, pts, begin, end, max_frames):
+            pose = P.interpolate_pose(traj, dts[i])
+            out.append(FrameRef(depth_fn[i], rgb_fn[j], mask_fn[j] if j < len(mask_fn) else None, dts[i], pose, i, j))
     return out
 
 

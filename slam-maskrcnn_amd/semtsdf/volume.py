@@ -112,6 +112,11 @@ class Volume:
     def reset(self):
         L.check(L.load().semtsdf_reset(self._h, None))
 
+    def get_params(self) -> L.Params:
+        p = L.Params()
+        L.check(L.load().semtsdf_get_params(self._h, C.byref(p)))
+        return p
+
     def state(self) -> L.State:
         st = L.State()
         L.check(L.load().semtsdf_get_state(self._h, C.byref(st)))

@@ -159,10 +159,13 @@ def main():
     ]
     poses = [np.array(p[:3] + list(np.array(p[3:]) / np.linalg.norm(p[3:]))) for p in poses]
     extr = [tsdf_utils.parse_pos(p) for p in poses]
+    degenerate = np.array([0.1, -0.2, 0.3, 0.0, 0.0, 1e-5, 0.0])  # |q|^2 < 1e-7: tsdf_utils.py:46-52
     pose_fix = dict(
         poses=np.array(poses),
         parse_pos=np.array(extr),
         transform44=np.array([tsdf_utils.transform44(p) for p in poses]),
+        degenerate_pose=degenerate,
+        transform44_degenerate=tsdf_utils.transform44(degenerate),
         slerp=np.array([tsdf_utils.slerp(poses[0][3:], poses[1][3:], t) for t in (0.0, 0.25, 0.5, 1.0)] +
                        [tsdf_utils.slerp(poses[0][3:], -poses[2][3:], 0.3)]),
     )
@@ -190,6 +193,71 @@ def main():
         print(name, D, [int(np.count_nonzero(o["wt"])) for o in outs], place["sdf_dtype"])
     # the frames themselves (data files of the reference, stored as arrays)
     np.savez_compressed(os.path.join(OUT, "frames_tum_fr2.npz"), depth_a=dA, rgb_a=cA, depth_b=dB, rgb_b=cB)
+
+    # placement (tsdf.py:32-52, init_vars) on both real frames at several volume sizes
+    place = {}
+    for fname, (d, c) in (("a", (dA, cA)), ("b", (dB, cB))):
+        for D in (64, 128, 256):
+            t = make_tsdf(TSDF, (520.9, 521.0, 325.1, 249.7), D)
+            mean_depth = np.mean(d[d > 0])
+            t.init_vars(d, c, np.eye(4), mean_depth)
+            for k, val in (("vol_start", t.vol_start), ("vol_end", t.vol_end), ("voxel", t.voxel), ("mu", t.mu),
+                           ("mean_depth", mean_depth), ("intrinsic_inv", t.intrinsic_inv)):
+                place[f"{fname}{D}_{k}"] = np.asarray(val)
+    np.savez_compressed(os.path.join(OUT, "placement_golden.npz"), **place)
+    print("placement", sorted({k.split('_')[0] for k in place}))
+
+    c1_case(TSDF, tsdf_utils, block)
+
+
+def c1_case(TSDF, tsdf_utils, block, n_frames=20, D=128):
+    """C1 (BASELINE.json configs[0]): the NumPy integrate at 128^3 over 20 frames, no masks.
+    fr2_desk is not in the container, so the frames are the seeded synthetic stream (seed 0,
+    regenerated by the tests) and its poses go through the reference's own pose path:
+    groundtruth lines -> tsdf_utils.read_traj -> parse_pos.  Frame 0 places the volume and is
+    integrated with E = extrinsic * inv(extrinsic) (tsdf.py:55-57); the final state is stored."""
+    import tempfile
+
+    sys.path.insert(0, os.path.join(os.path.dirname(OUT), "..", "slam-maskrcnn_amd"))
+    from semtsdf.synth import SyntheticStream
+
+    from semtsdf import pose as P
+
+    st = SyntheticStream(seed=0)
+    # the stream's frame 0 is the identity pose, whose zero rotation axis parse_pos divides by
+    # (tsdf_utils.py:67-68 -> NaN); a fixed world offset B keeps every relative pose
+    # E = inv(B c2w_k) B c2w_0 = inv(c2w_k) c2w_0 and avoids it
+    B = np.eye(4)
+    B[:3, :3] = P.rodrigues([0.02, -0.03, 0.01])
+    B[:3, 3] = (0.3, -0.1, 0.2)
+    lines = [P.c2w_to_tum(st.stamp(k), B @ st.c2w(k)) for k in range(n_frames)]
+    with tempfile.NamedTemporaryFile("w", suffix=".txt", delete=False) as f:
+        f.write("# timestamp tx ty tz qx qy qz qw\n" + "\n".join(lines) + "\n")
+        gt = f.name
+    traj = tsdf_utils.read_traj(gt)  # reference code
+    os.unlink(gt)
+    t = make_tsdf(TSDF, (520.9, 521.0, 325.1, 249.7), D)
+    np.int = int
+    Es, sums = [], []
+    for k in range(n_frames):
+        fr = st.frame(k)
+        extrinsic = tsdf_utils.parse_pos(traj[k, 1:])  # reference code (cv2.Rodrigues stubbed)
+        if not t.init:
+            t.init_vars(fr.depth, fr.rgb, extrinsic, np.mean(fr.depth[fr.depth > 0]))
+        exec(block, {"self": t, "depth": fr.depth, "color": fr.rgb, "extrinsic": extrinsic, "np": np})
+        Es.append(np.matmul(extrinsic, t.init_extrinsic_inv))
+        sums.append(int(fr.depth.astype(np.int64).sum()) ^ (int(fr.rgb.astype(np.int64).sum()) << 1))
+    wt = t.tsdf_wt.reshape(-1)
+    idx = np.nonzero(wt)[0]
+    col = t.tsdf_color.reshape(-1, 3)[idx]
+    assert wt.max() <= 255 and col.min() >= 0 and col.max() <= 255
+    np.savez_compressed(
+        os.path.join(OUT, "integrate_c1_d128.npz"), vol_dim=np.int64(D), n_frames=np.int64(n_frames),
+        n_flat=np.int64(wt.size), place_vol_start=np.array(t.vol_start), place_voxel=np.array(t.voxel),
+        place_mu=np.float64(t.mu), place_intrinsic_inv=t.intrinsic_inv, E=np.array(Es), frame_sums=np.array(sums),
+        world_offset=B, idx=idx.astype(np.uint32), sdf=t.tsdf_diff.reshape(-1)[idx].astype(np.float32), wt=wt[idx].astype(np.uint8),
+        color=col.astype(np.uint8), sdf_dtype=np.str_(str(t.tsdf_diff.dtype)))
+    print("c1", D, n_frames, "touched", idx.size)
 
 
 if __name__ == "__main__":
