@@ -188,10 +188,10 @@ int semtsdf_raycast_dev(semtsdf_vol* v, const float s2w[16], const float c[3], i
 
 /* ---- Z-sharded raycast (replaces the single-GPU back_proj_kernel
  * tsdf.cu:72-135 and show_tsdf_kernel viewer.cu:17-86 when the volume is split across GPUs)
- * Every shard of a group runs the same call sequence.  Between calls the host all-gathers
- * the per-pixel `send` records (record_bytes each) of all shards, in shard order, into
- * `gathered` (z_nshards * record_bytes, device memory):
- *   begin(kind, cam, c, &rec, &nsteps)
+ * Every shard of a group runs the same call sequence.  Between calls the host exchanges
+ * the per-pixel `send` records (record_bytes each) of all shards into `gathered` (device
+ * memory) as `exchange` says (SEMTSDF_EXCHANGE_*):
+ *   begin(kind, cam, c, exchange, &rec, &nsteps)
  *   for s in 0..nsteps-1:  step(s, s ? gathered : NULL, send);  all-gather send -> gathered
  *   kind RENDER_*:  render_finish(gathered, out_bgr, out_t)   -- all-gathered composite
  *   kind RAY_ASSOC: assoc_partial(gathered, mask, partial);    all-reduce(SUM) partial;
@@ -199,7 +199,12 @@ int semtsdf_raycast_dev(semtsdf_vol* v, const float s2w[16], const float c[3], i
  * The result is bit-identical to the single-volume raycast / association. */
 #define SEMTSDF_RAY_ASSOC 2
 #define SEMTSDF_ASSOC_PARTIAL_LEN 3168 /* int64 words: 32x32 t1, t3; 32 t2, c1, c2; 32x32 c3 */
-int semtsdf_shard_ray_begin(semtsdf_vol* v, int kind, const float cam[16], const float c[3],
+/* exchange between protocol steps: every shard's records concatenated in shard order
+ * (all-gather; gathered = z_nshards * record_bytes), or their element-wise minimum as
+ * little-endian int64 (all-reduce MIN; gathered = record_bytes), 1/z_nshards of the bytes. */
+#define SEMTSDF_EXCHANGE_ALLGATHER 0
+#define SEMTSDF_EXCHANGE_MIN 1
+int semtsdf_shard_ray_begin(semtsdf_vol* v, int kind, const float cam[16], const float c[3], int exchange,
                             size_t* record_bytes, int* nsteps);
 int semtsdf_shard_ray_step(semtsdf_vol* v, int step, const void* gathered_d, void* send_d, void* stream);
 int semtsdf_shard_render_finish(semtsdf_vol* v, const void* gathered_d, uint8_t* out_bgr_d, float* out_t_d,
@@ -208,6 +213,9 @@ int semtsdf_shard_assoc_partial(semtsdf_vol* v, const void* gathered_d, const ui
                                 int64_t* partial_d, void* stream);
 int semtsdf_shard_assoc_apply(semtsdf_vol* v, const int64_t* reduced_d, uint8_t* mask_d,
                               semtsdf_assoc_stats* stats, void* stream);
+/* dst[i] = min(dst[i], src[i]) over n int64 (device, async on stream): the exchange
+ * SEMTSDF_EXCHANGE_MIN for shards driven from one process. */
+int semtsdf_min_i64(int64_t* dst_d, const int64_t* src_d, size_t n, void* stream);
 /* parse_frame for a sharded handle: the host runs the association protocol above (when
  * n_obs > 0), then integrate_dev, then note_integrated (n_obs++, first-frame object count). */
 int semtsdf_shard_note_integrated(semtsdf_vol* v, const uint8_t* mask_d, void* stream);
@@ -222,6 +230,10 @@ int semtsdf_copy_bandwidth(int device, size_t bytes, int reps, double* gbs);
  * voxel-major u32 [N*32] (tsdf.cu:249); cls/cls_cnt i32 [N] (vote mode). */
 int semtsdf_download(semtsdf_vol* v, float* sdf, int32_t* wt, void* color, uint32_t* hist,
                      int32_t* cls, int32_t* cls_cnt);
+/* The x-planes [x0, x1) only, same layouts (arrays sized (x1-x0) * Dy * local Dz [* 3 | * 32]):
+ * checks of volumes too large to download whole (a 1024^3 histogram is 128 GiB). */
+int semtsdf_download_slab(semtsdf_vol* v, int x0, int x1, float* sdf, int32_t* wt, void* color,
+                          uint32_t* hist, int32_t* cls, int32_t* cls_cnt);
 int semtsdf_upload(semtsdf_vol* v, const float* sdf, const int32_t* wt, const void* color,
                    const uint32_t* hist, const int32_t* cls, const int32_t* cls_cnt);
 

@@ -50,6 +50,9 @@ def lib():
         _lib.oracle_integrate.argtypes = [P, P, P, P, C.c_int, C.c_int, C.c_uint32, P, P, P, P, P, P, P, P, P, P,
                                           C.c_int, C.c_int, P, P, C.c_int]
         _lib.oracle_integrate.restype = None
+        _lib.oracle_integrate_slab.argtypes = [P, P, P, P, C.c_int, C.c_int, C.c_uint32, P, P, P, P, P, P, P, P, P,
+                                               P, C.c_int, C.c_int, P]
+        _lib.oracle_integrate_slab.restype = None
         _lib.oracle_march_probs.argtypes = [P, P, P, P, C.c_int, C.c_int, P, P, C.c_float, P, P, C.c_int, C.c_int]
         _lib.oracle_march_probs.restype = None
         _lib.oracle_filter_overlaps.argtypes = [P, P, P, C.c_int, C.c_int, C.c_uint32, C.c_float, C.c_int, P, P, P]
@@ -162,6 +165,20 @@ def numpy_pixels(vol_dim, vol_start, voxel, K, E, W, H, n_flat=None):
     py = pixel[1].astype(np.int64)
     ok = (px >= 0) & (px <= W - 1) & (py >= 0) & (py <= H - 1)
     return np.where(ok, py * W + px, -1)
+
+
+def integrate_slab(g: OGeom, st: OState, K16, E16, depth, rgb, x_range, mask=None, flags=0x3):
+    """Integrate x-planes [x0, x1) into a state holding only those planes (OState with
+    dims (x1 - x0, Dy, Dz)), with the global voxel coordinates."""
+    H, W = depth.shape[:2]
+    counts = np.zeros(3, np.uint64)
+    lib().oracle_integrate_slab(_p(g.dims), _p(g.geo), _p(k9(K16)),
+                                _p(np.ascontiguousarray(E16, np.float32).reshape(16)), W, H, flags, _p(st.sdf),
+                                _p(st.wt), _p(st.color), _p(st.hist), _p(st.cls), _p(st.cls_cnt),
+                                _p(np.ascontiguousarray(depth, np.uint16)), _p(np.ascontiguousarray(rgb, np.uint8)),
+                                _p(None if mask is None else np.ascontiguousarray(mask, np.uint8)), None,
+                                int(x_range[0]), int(x_range[1]), _p(counts))
+    return counts
 
 
 def march_probs(g: OGeom, Kinv16, E16, W, H, sdf, hist, box_thresh=0.3):

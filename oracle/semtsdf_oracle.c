@@ -70,13 +70,40 @@ static ogeom mk_geom(const int32_t* dims, const float* geo) {
  * State arrays in reference layouts: sdf/wt/cls/cls_cnt [N], colour [N*3], hist
  * voxel-major [N*32].  Processes x in [x_begin, x_end).  counts[0] += touched,
  * counts[1] += gated, counts[2] += labels >= 32 seen (skipped). */
+static void integrate_core(const int32_t* dims, const float* geo, const float* K9, const float* E16, int width,
+                           int height, uint32_t flags, float* sdf, int32_t* wt, void* color, uint32_t* hist,
+                           int32_t* cls, int32_t* cls_cnt, const uint16_t* depth, const uint8_t* rgb,
+                           const uint8_t* mask, const int32_t* cls_in, int x_begin, int x_end, uint64_t* counts,
+                           const int32_t* zmap, int lz, int x_state0);
+
 void oracle_integrate(const int32_t* dims, const float* geo, const float* K9, const float* E16, int width,
                       int height, uint32_t flags, float* sdf, int32_t* wt, void* color, uint32_t* hist,
                       int32_t* cls, int32_t* cls_cnt, const uint16_t* depth, const uint8_t* rgb,
                       const uint8_t* mask, const int32_t* cls_in, int x_begin, int x_end, uint64_t* counts,
                       const int32_t* zmap, int lz) {
+    integrate_core(dims, geo, K9, E16, width, height, flags, sdf, wt, color, hist, cls, cls_cnt, depth, rgb, mask,
+                   cls_in, x_begin, x_end, counts, zmap, lz, 0);
+}
+
+/* The same over x-planes [x_begin, x_end) with state arrays that hold only those planes
+ * ([x_end - x_begin][dims[1]][dims[2]]): slabs of volumes too large for a whole host copy
+ * (1024^3), computed with the global voxel coordinates, so bit-identical to the full run. */
+void oracle_integrate_slab(const int32_t* dims, const float* geo, const float* K9, const float* E16, int width,
+                           int height, uint32_t flags, float* sdf, int32_t* wt, void* color, uint32_t* hist,
+                           int32_t* cls, int32_t* cls_cnt, const uint16_t* depth, const uint8_t* rgb,
+                           const uint8_t* mask, const int32_t* cls_in, int x_begin, int x_end, uint64_t* counts) {
+    integrate_core(dims, geo, K9, E16, width, height, flags, sdf, wt, color, hist, cls, cls_cnt, depth, rgb, mask,
+                   cls_in, x_begin, x_end, counts, NULL, 0, x_begin);
+}
+
+static void integrate_core(const int32_t* dims, const float* geo, const float* K9, const float* E16, int width,
+                           int height, uint32_t flags, float* sdf, int32_t* wt, void* color, uint32_t* hist,
+                           int32_t* cls, int32_t* cls_cnt, const uint16_t* depth, const uint8_t* rgb,
+                           const uint8_t* mask, const int32_t* cls_in, int x_begin, int x_end, uint64_t* counts,
+                           const int32_t* zmap, int lz, int x_state0) {
     /* zmap: global z of each of the lz local planes (a Z-slab shard); NULL =
-       the whole volume.  State arrays are [dims[0]][dims[1]][lz]. */
+       the whole volume.  State arrays are [dims[0]][dims[1]][lz], their plane 0 being
+       x = x_state0. */
     const ogeom g = mk_geom(dims, geo);
     if (!zmap) lz = g.dz;
     const int sem = flags & 1, gate = flags & 2, ci32 = flags & 4, vote = flags & 8;
@@ -118,7 +145,7 @@ void oracle_integrate(const int32_t* dims, const float* geo, const float* K9, co
                 if (diff <= -g.mu) continue;
                 if (diff > g.mu) diff = g.mu;
                 diff = diff / g.mu;
-                const size_t v = ((size_t)x * g.dy + y) * lz + z;
+                const size_t v = ((size_t)(x - x_state0) * g.dy + y) * lz + z;
                 const int w = wt[v];
                 /* running mean with unit weight (tsdf.cu:56) */
                 sdf[v] = fmaf(sdf[v], (float)w, diff) / (float)(w + 1);

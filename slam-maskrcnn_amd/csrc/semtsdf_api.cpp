@@ -95,6 +95,7 @@ struct semtsdf_vol {
     void* ray_state_d = nullptr;   // ShardRayState arrays, 6 x npx x 4 B
     MarchCamera ray_cam{};
     int ray_kind = -1;
+    int ray_nrec = 1;              // records per pixel of the exchange (nshards: all-gather; 1: all-reduce MIN)
     int ray_next = 0;              // next expected step
     uint32_t n_obs = 0;
     bool bmin_dirty = false;       // integrated since the last map update: update marked bricks
@@ -921,6 +922,7 @@ static ShardRayArgs shard_args(semtsdf_vol* v) {
     a.width = v->p.width;
     a.height = v->p.height;
     a.kind = v->ray_kind;
+    a.nrec = v->ray_nrec;
     const size_t n = npx(v);
     char* base = (char*)v->ray_state_d;
     a.st.k = (int*)(base);
@@ -937,9 +939,11 @@ static ShardRayArgs shard_args(semtsdf_vol* v) {
     return a;
 }
 
-int semtsdf_shard_ray_begin(semtsdf_vol* v, int kind, const float cam[16], const float c[3], size_t* record_bytes,
-                            int* nsteps) {
+int semtsdf_shard_ray_begin(semtsdf_vol* v, int kind, const float cam[16], const float c[3], int exchange,
+                            size_t* record_bytes, int* nsteps) {
     if (!v || !cam) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    if (exchange != SEMTSDF_EXCHANGE_ALLGATHER && exchange != SEMTSDF_EXCHANGE_MIN)
+        return fail(SEMTSDF_ERR_INVALID, "bad exchange %d", exchange);
     if (kind != SEMTSDF_RENDER_LABEL && kind != SEMTSDF_RENDER_COLOR && kind != SEMTSDF_RAY_ASSOC)
         return fail(SEMTSDF_ERR_INVALID, "bad ray kind %d", kind);
     if (kind != SEMTSDF_RAY_ASSOC && !c) return fail(SEMTSDF_ERR_INVALID, "render needs the camera centre");
@@ -964,6 +968,7 @@ int semtsdf_shard_ray_begin(semtsdf_vol* v, int kind, const float cam[16], const
     if (int rc = ensure_bmin(v, v->stream)) return rc;
     HIPC(hipStreamSynchronize(v->stream));  // the protocol's steps may run on another stream
     v->ray_kind = kind;
+    v->ray_nrec = exchange == SEMTSDF_EXCHANGE_MIN ? 1 : v->p.z_nshards;
     v->ray_next = 0;
     if (record_bytes) *record_bytes = 8 * npx(v);
     if (nsteps) *nsteps = kind == SEMTSDF_RAY_ASSOC ? 3 : 4;
@@ -1065,6 +1070,12 @@ int semtsdf_shard_note_integrated(semtsdf_vol* v, const uint8_t* mask_d, void* s
         HIPC(launch_first_frame_objs(v->tables_d, v->num_objs_d, s));
     }
     v->n_obs++;
+    return SEMTSDF_OK;
+}
+
+int semtsdf_min_i64(int64_t* dst_d, const int64_t* src_d, size_t n, void* stream) {
+    if (!dst_d || !src_d) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    HIPC(launch_min_i64((long long*)dst_d, (const long long*)src_d, n, (hipStream_t)stream));
     return SEMTSDF_OK;
 }
 
@@ -1189,15 +1200,19 @@ int semtsdf_raycast_dev(semtsdf_vol* v, const float s2w[16], const float c[3], i
 
 // A 4-byte per-voxel array between the reference layout (rows of lz planes, dense) and the
 // tiled device storage, chunked through a device staging buffer.
-static int vox_xfer(semtsdf_vol* v, void* host, void* dev, bool to_host, const char* what, hipStream_t s) {
-    const uint64_t n = (uint64_t)v->g.dimx * v->g.dimy * v->g.lz;
-    if (n == 0) return SEMTSDF_OK;
-    const uint64_t chunk = std::min<uint64_t>(n, 1ull << 26);  // <= 256 MiB staging
+// Voxels of the reference layout (rows of lz planes) held by the handle.
+static uint64_t nref(const semtsdf_vol* v) { return (uint64_t)v->g.dimx * v->g.dimy * v->g.lz; }
+
+// Voxels [vb, ve) of the reference layout (host[0] is voxel vb).
+static int vox_xfer(semtsdf_vol* v, void* host, void* dev, bool to_host, const char* what, hipStream_t s, uint64_t vb,
+                    uint64_t ve) {
+    if (ve <= vb) return SEMTSDF_OK;
+    const uint64_t chunk = std::min<uint64_t>(ve - vb, 1ull << 26);  // <= 256 MiB staging
     void* stage = nullptr;
     HIPC(hipMalloc(&stage, chunk * 4));
-    for (uint64_t v0 = 0; v0 < n; v0 += chunk) {
-        const uint64_t nv = std::min<uint64_t>(chunk, n - v0);
-        char* h = static_cast<char*>(host) + v0 * 4;
+    for (uint64_t v0 = vb; v0 < ve; v0 += chunk) {
+        const uint64_t nv = std::min<uint64_t>(chunk, ve - v0);
+        char* h = static_cast<char*>(host) + (v0 - vb) * 4;
         hipError_t e;
         if (to_host) {
             e = launch_vox_chunk(dev, stage, true, v->g, v0, nv, s);
@@ -1217,17 +1232,16 @@ static int vox_xfer(semtsdf_vol* v, void* host, void* dev, bool to_host, const c
 }
 
 // colour between the padded device layout and the reference [N][3] layout, chunked
-static int color_xfer(semtsdf_vol* v, void* host, bool to_host, hipStream_t s) {
+static int color_xfer(semtsdf_vol* v, void* host, bool to_host, hipStream_t s, uint64_t vb, uint64_t ve) {
     const bool i32 = v->p.flags & SEMTSDF_F_COLOR_I32;
     const size_t es = i32 ? 4 : 1;
-    const uint64_t n = (uint64_t)v->g.dimx * v->g.dimy * v->g.lz;
-    if (n == 0) return SEMTSDF_OK;
-    const uint64_t chunk = std::min<uint64_t>(n, 1ull << 24);
+    if (ve <= vb) return SEMTSDF_OK;
+    const uint64_t chunk = std::min<uint64_t>(ve - vb, 1ull << 24);
     void* stage = nullptr;
     HIPC(hipMalloc(&stage, chunk * 3 * es));
-    for (uint64_t v0 = 0; v0 < n; v0 += chunk) {
-        const uint64_t nv = std::min<uint64_t>(chunk, n - v0);
-        char* h = static_cast<char*>(host) + v0 * 3 * es;
+    for (uint64_t v0 = vb; v0 < ve; v0 += chunk) {
+        const uint64_t nv = std::min<uint64_t>(chunk, ve - v0);
+        char* h = static_cast<char*>(host) + (v0 - vb) * 3 * es;
         hipError_t e;
         if (to_host) {
             e = launch_color_chunk(v->b.color, stage, true, i32, v->g, v0, nv, s);
@@ -1246,37 +1260,39 @@ static int color_xfer(semtsdf_vol* v, void* host, bool to_host, hipStream_t s) {
     return SEMTSDF_OK;
 }
 
-int semtsdf_download(semtsdf_vol* v, float* sdf, int32_t* wt, void* color, uint32_t* hist, int32_t* cls,
-                     int32_t* cls_cnt) {
+int semtsdf_download_slab(semtsdf_vol* v, int x0, int x1, float* sdf, int32_t* wt, void* color, uint32_t* hist,
+                          int32_t* cls, int32_t* cls_cnt) {
     if (!v) return fail(SEMTSDF_ERR_INVALID, "NULL handle");
+    if (x0 < 0 || x1 > v->g.dimx || x0 > x1) return fail(SEMTSDF_ERR_INVALID, "bad x range [%d, %d)", x0, x1);
     HIPC(hipSetDevice(v->device));
     hipStream_t s = v->stream;
+    const uint64_t plane = (uint64_t)v->g.dimy * v->g.lz;  // reference layout: x-major, z fastest
+    const uint64_t vb = (uint64_t)x0 * plane, ve = (uint64_t)x1 * plane;
     int rc;
-    if (sdf && (rc = vox_xfer(v, sdf, v->b.sdf, true, "sdf", s))) return rc;
-    if (wt && (rc = vox_xfer(v, wt, v->b.wt, true, "weight", s))) return rc;
+    if (sdf && (rc = vox_xfer(v, sdf, v->b.sdf, true, "sdf", s, vb, ve))) return rc;
+    if (wt && (rc = vox_xfer(v, wt, v->b.wt, true, "weight", s, vb, ve))) return rc;
     if (color) {
-        rc = color_xfer(v, color, true, s);
+        rc = color_xfer(v, color, true, s, vb, ve);
         if (rc) return rc;
     }
     if (cls) {
         if (!(v->p.flags & SEMTSDF_F_VOTE)) return fail(SEMTSDF_ERR_STATE, "not a VOTE volume");
-        if ((rc = vox_xfer(v, cls, v->b.cls, true, "cls", s))) return rc;
+        if ((rc = vox_xfer(v, cls, v->b.cls, true, "cls", s, vb, ve))) return rc;
     }
     if (cls_cnt) {
         if (!(v->p.flags & SEMTSDF_F_VOTE)) return fail(SEMTSDF_ERR_STATE, "not a VOTE volume");
-        if ((rc = vox_xfer(v, cls_cnt, v->b.cls_cnt, true, "cls_cnt", s))) return rc;
+        if ((rc = vox_xfer(v, cls_cnt, v->b.cls_cnt, true, "cls_cnt", s, vb, ve))) return rc;
     }
     if (hist) {
         if (!(v->p.flags & SEMTSDF_F_SEMANTIC)) return fail(SEMTSDF_ERR_STATE, "not a SEMANTIC volume");
-        const uint64_t n = (uint64_t)v->g.dimx * v->g.dimy * v->g.lz;
-        const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(n, 1ull << 22));  // <= 512 MiB staging
+        const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(ve - vb, 1ull << 22));  // <= 512 MiB staging
         uint32_t* stage = nullptr;
         HIPC(hipMalloc(&stage, chunk * kMaxObjects * 4));
-        for (uint64_t v0 = 0; v0 < n; v0 += chunk) {
-            const uint64_t nv = std::min<uint64_t>(chunk, n - v0);
+        for (uint64_t v0 = vb; v0 < ve; v0 += chunk) {
+            const uint64_t nv = std::min<uint64_t>(chunk, ve - v0);
             hipError_t e = launch_hist_chunk_to_vm(v->b.hist, stage, v->g, v0, nv, s);
             if (e == hipSuccess)
-                e = hipMemcpyAsync(hist + v0 * kMaxObjects, stage, nv * kMaxObjects * 4, hipMemcpyDeviceToHost, s);
+                e = hipMemcpyAsync(hist + (v0 - vb) * kMaxObjects, stage, nv * kMaxObjects * 4, hipMemcpyDeviceToHost, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e != hipSuccess) {
                 (void)hipFree(stage);
@@ -1289,6 +1305,12 @@ int semtsdf_download(semtsdf_vol* v, float* sdf, int32_t* wt, void* color, uint3
     return SEMTSDF_OK;
 }
 
+int semtsdf_download(semtsdf_vol* v, float* sdf, int32_t* wt, void* color, uint32_t* hist, int32_t* cls,
+                     int32_t* cls_cnt) {
+    if (!v) return fail(SEMTSDF_ERR_INVALID, "NULL handle");
+    return semtsdf_download_slab(v, 0, v->g.dimx, sdf, wt, color, hist, cls, cls_cnt);
+}
+
 int semtsdf_upload(semtsdf_vol* v, const float* sdf, const int32_t* wt, const void* color, const uint32_t* hist,
                    const int32_t* cls, const int32_t* cls_cnt) {
     if (!v) return fail(SEMTSDF_ERR_INVALID, "NULL handle");
@@ -1299,19 +1321,19 @@ int semtsdf_upload(semtsdf_vol* v, const float* sdf, const int32_t* wt, const vo
     // empty-space map that describe the old contents (0 = unknown is always safe)
     v->bmin_stale = true;
     if (sdf || wt) HIPC(hipMemsetAsync(v->b.sflag, 0, v->g.nvox / 32 + 1, s));  // steady flags: unknown
-    if (sdf && (rc = vox_xfer(v, const_cast<float*>(sdf), v->b.sdf, false, "sdf", s))) return rc;
-    if (wt && (rc = vox_xfer(v, const_cast<int32_t*>(wt), v->b.wt, false, "weight", s))) return rc;
+    if (sdf && (rc = vox_xfer(v, const_cast<float*>(sdf), v->b.sdf, false, "sdf", s, 0, nref(v)))) return rc;
+    if (wt && (rc = vox_xfer(v, const_cast<int32_t*>(wt), v->b.wt, false, "weight", s, 0, nref(v)))) return rc;
     if (color) {
-        rc = color_xfer(v, const_cast<void*>(color), false, s);
+        rc = color_xfer(v, const_cast<void*>(color), false, s, 0, nref(v));
         if (rc) return rc;
     }
     if (cls) {
         if (!(v->p.flags & SEMTSDF_F_VOTE)) return fail(SEMTSDF_ERR_STATE, "not a VOTE volume");
-        if ((rc = vox_xfer(v, const_cast<int32_t*>(cls), v->b.cls, false, "cls", s))) return rc;
+        if ((rc = vox_xfer(v, const_cast<int32_t*>(cls), v->b.cls, false, "cls", s, 0, nref(v)))) return rc;
     }
     if (cls_cnt) {
         if (!(v->p.flags & SEMTSDF_F_VOTE)) return fail(SEMTSDF_ERR_STATE, "not a VOTE volume");
-        if ((rc = vox_xfer(v, const_cast<int32_t*>(cls_cnt), v->b.cls_cnt, false, "cls_cnt", s))) return rc;
+        if ((rc = vox_xfer(v, const_cast<int32_t*>(cls_cnt), v->b.cls_cnt, false, "cls_cnt", s, 0, nref(v)))) return rc;
     }
     if (hist) {
         if (!(v->p.flags & SEMTSDF_F_SEMANTIC)) return fail(SEMTSDF_ERR_STATE, "not a SEMANTIC volume");

@@ -200,7 +200,8 @@ struct ShardRayArgs {
     int width, height;
     int kind;                 // 0 label render, 1 colour render, 2 association
     int step;                 // 0..2 (k_shard_ray_step)
-    const int2* gathered;     // [nshards][npx] records of the previous step
+    const int2* gathered;     // [nrec][npx] records of the previous step ({value, key} each)
+    int nrec;                 // records per pixel in gathered: nshards (all-gather) or 1 (all-reduce MIN)
     int2* send;               // [npx] this shard's records
     ShardRayState st;
     int color_i32;
@@ -219,6 +220,7 @@ hipError_t launch_shard_render_finish(const ShardRayArgs& a, hipStream_t s);
 hipError_t launch_shard_assoc_partial(const ShardRayArgs& a, hipStream_t s);
 hipError_t launch_tables_from_partial(const long long* reduced, AssocTables* t, hipStream_t s);
 hipError_t launch_copy_f4(const void* src, void* dst, size_t n16, hipStream_t s);
+hipError_t launch_min_i64(long long* dst, const long long* src, size_t n, hipStream_t s);
 hipError_t launch_brick_min(const VolGeom& g, const VolBufs& b, bool all, hipStream_t s);
 hipError_t launch_fill_volume(const VolGeom& g, const VolBufs& b, uint32_t flags, hipStream_t s);
 hipError_t launch_depth_pyramid(const uint16_t* depth, const uint8_t* rgb, const uint8_t* mask, int w, int h,

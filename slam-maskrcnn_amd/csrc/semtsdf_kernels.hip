@@ -123,13 +123,51 @@ __global__ __launch_bounds__(256) void k_fill_f32(float* __restrict__ p, uint64_
     }
 }
 
-__global__ __launch_bounds__(256) void k_copy_f4(const float4* __restrict__ a, float4* __restrict__ b, size_t n) {
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-        b[i] = a[i];
+// Achievable-bandwidth probe: a float4 copy with kCopyUnroll independent 16-B loads in flight
+// per lane before their stores (one load per lane per grid step left too few bytes in flight
+// per CU to cover the HBM latency), over a grid of whole residency.
+#ifndef SEMTSDF_COPY_UNROLL
+#define SEMTSDF_COPY_UNROLL 4
+#endif
+#ifndef SEMTSDF_COPY_BLOCKS_PER_CU
+#define SEMTSDF_COPY_BLOCKS_PER_CU 8
+#endif
+constexpr int kCopyUnroll = SEMTSDF_COPY_UNROLL;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_copy_f4(const f32x4* __restrict__ a, f32x4* __restrict__ b, size_t n) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + (kCopyUnroll - 1) * stride < n; i += kCopyUnroll * stride) {
+        f32x4 v[kCopyUnroll];
+#pragma unroll
+        for (int k = 0; k < kCopyUnroll; ++k) v[k] = __builtin_nontemporal_load(a + i + k * stride);
+#pragma unroll
+        for (int k = 0; k < kCopyUnroll; ++k) __builtin_nontemporal_store(v[k], b + i + k * stride);
+    }
+    for (; i < n; i += stride) b[i] = a[i];
 }
 
 hipError_t launch_copy_f4(const void* src, void* dst, size_t n16, hipStream_t s) {
-    hipLaunchKernelGGL(k_copy_f4, dim3(8192), dim3(256), 0, s, (const float4*)src, (float4*)dst, n16);
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    hipLaunchKernelGGL(k_copy_f4, dim3((unsigned)cus * SEMTSDF_COPY_BLOCKS_PER_CU), dim3(256), 0, s, (const f32x4*)src,
+                       (f32x4*)dst, n16);
+    return hipGetLastError();
+}
+
+// dst[i] = min(dst[i], src[i]) over int64: the in-process stand-in of an all-reduce MIN
+// (shards driven from one process, semtsdf_min_i64)
+__global__ __launch_bounds__(256) void k_min_i64(long long* __restrict__ dst, const long long* __restrict__ src, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        dst[i] = min(dst[i], src[i]);
+}
+
+hipError_t launch_min_i64(long long* dst, const long long* src, size_t n, hipStream_t s) {
+    size_t blocks = (n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_min_i64, dim3((unsigned)blocks), dim3(256), 0, s, dst, src, n);
     return hipGetLastError();
 }
 
@@ -2193,11 +2231,20 @@ hipError_t launch_render(const RenderArgs& a, hipStream_t s) {
 // every value is computed with the same arithmetic as the single volume, so the
 // composite is bit-identical to the single-volume raycast.
 // ------------------------------------------------------------------------------------
+// A per-pixel record is 8 bytes {value (low word), key (high word)}: as a little-endian
+// int64 it orders by the signed key first, so the exchange between steps can be an
+// all-gather of every shard's records (n = nshards; the minimum is taken here) or an
+// all-reduce MIN over int64 (n = 1), which moves 1/nshards of the bytes.  Keys are unique
+// per pixel except -1 and INT_MAX, whose values agree on every shard.
+__device__ __forceinline__ int2 mk_rec(int key, int val) { return make_int2(val, key); }
+__device__ __forceinline__ int rkey(int2 r) { return r.y; }
+__device__ __forceinline__ int rval(int2 r) { return r.x; }
+
 __device__ __forceinline__ int2 gather_min(const int2* __restrict__ g, int n, int npx, int px) {
-    int2 best = make_int2(INT_MAX, 0);
+    int2 best = mk_rec(INT_MAX, 0);
     for (int r = 0; r < n; ++r) {
         const int2 v = g[(size_t)r * npx + px];
-        if (v.x < best.x) best = v;
+        if (rkey(v) < rkey(best)) best = v;
     }
     return best;
 }
@@ -2244,10 +2291,10 @@ __global__ __launch_bounds__(256) void k_shard_ray_step(ShardRayArgs a) {
     const int px = y * a.width + x;
     const RayGeo r = shard_ray(a, x, y);
     const float vx = a.g.voxel[0];
-    int2 rec = make_int2(INT_MAX, 0);
+    int2 rec = mk_rec(INT_MAX, 0);
     if (a.step == 0) {
         if (!r.in) {
-            rec.x = -1;
+            rec = mk_rec(-1, 0);
         } else {
             float t = r.t0;
             bool dead = false;
@@ -2255,34 +2302,34 @@ __global__ __launch_bounds__(256) void k_shard_ray_step(ShardRayArgs a) {
             SkipCursor cur;
             float f0;
             if (owns_at(a, r, t) && sample_at_skip(a, r, t, thr, cur, &f0)) {
-                if (!(f0 > 0.0f)) { rec.x = -1; dead = true; }
+                if (!(f0 > 0.0f)) { rec = mk_rec(-1, 0); dead = true; }
             }
             if (!dead) {
                 if (!(t < r.t1)) {
-                    rec.x = -1;
+                    rec = mk_rec(-1, 0);
                 } else {
                     for (int k = 0; t < r.t1; ++k, t += vx) {
                         if (!owns_at(a, r, t)) continue;
                         float f;
                         if (!sample_at_skip(a, r, t, thr, cur, &f)) continue;
-                        if (f < vx / 2.0f) { rec = make_int2(k, __float_as_int(f)); break; }
+                        if (f < vx / 2.0f) { rec = mk_rec(k, __float_as_int(f)); break; }
                     }
                 }
             }
         }
     } else if (a.step == 1) {
-        const int2 c = gather_min(a.gathered, a.g.nshards, npx, px);
-        if (c.x < 0 || c.x == INT_MAX) {
+        const int2 c = gather_min(a.gathered, a.nrec, npx, px);
+        if (rkey(c) < 0 || rkey(c) == INT_MAX) {
             a.st.k[px] = -1;
         } else {
-            const int k = c.x;
-            const float fk = __int_as_float(c.y);
+            const int k = rkey(c);
+            const float fk = __int_as_float(rval(c));
             a.st.k[px] = k;
             a.st.fk[px] = fk;
             if (fk < 0.0f) {
                 a.st.j[px] = 0;
                 const float t = replay_t(r.t0, k - 1, 0, vx);
-                if (owns_at(a, r, t)) rec = make_int2(0, __float_as_int(sample_at(a, r, t)));
+                if (owns_at(a, r, t)) rec = mk_rec(0, __float_as_int(sample_at(a, r, t)));
             } else {
                 float t = replay_t(r.t0, k, 0, vx);
                 const float q = vx / 4.0f;
@@ -2294,27 +2341,27 @@ __global__ __launch_bounds__(256) void k_shard_ray_step(ShardRayArgs a) {
                     if (!owns_at(a, r, t)) continue;
                     float f;
                     if (!sample_at_skip(a, r, t, thr, cur, &f)) continue;
-                    if (f < 0.0f) { rec = make_int2(j, __float_as_int(f)); break; }
+                    if (f < 0.0f) { rec = mk_rec(j, __float_as_int(f)); break; }
                 }
             }
         }
     } else {  // step 2
         const int k = a.st.k[px];
         if (k >= 0) {
-            const int2 c = gather_min(a.gathered, a.g.nshards, npx, px);
+            const int2 c = gather_min(a.gathered, a.nrec, npx, px);
             if (a.st.fk[px] < 0.0f) {
-                a.st.fp[px] = __int_as_float(c.y);
-            } else if (c.x == INT_MAX) {
+                a.st.fp[px] = __int_as_float(rval(c));
+            } else if (rkey(c) == INT_MAX) {
                 a.st.k[px] = -1;  // the quarter-step march ran out: miss
             } else {
-                const int j = c.x;
+                const int j = rkey(c);
                 a.st.j[px] = j;
-                a.st.fj[px] = __int_as_float(c.y);
+                a.st.fj[px] = __int_as_float(rval(c));
                 if (j == 1) {
                     a.st.fp[px] = a.st.fk[px];
                 } else {
                     const float t = replay_t(r.t0, k, j - 1, vx);
-                    if (owns_at(a, r, t)) rec = make_int2(0, __float_as_int(sample_at(a, r, t)));
+                    if (owns_at(a, r, t)) rec = mk_rec(0, __float_as_int(sample_at(a, r, t)));
                 }
             }
         }
@@ -2335,7 +2382,7 @@ __device__ __forceinline__ bool shard_resolve(const ShardRayArgs& a, const RayGe
         fp = a.st.fp[px];
     } else {
         const int j = a.st.j[px];
-        if (j >= 2) a.st.fp[px] = __int_as_float(gather_min(a.gathered, a.g.nshards, npx, px).y);
+        if (j >= 2) a.st.fp[px] = __int_as_float(rval(gather_min(a.gathered, a.nrec, npx, px)));
         ts = replay_t(r.t0, k, j, vx);
         step = vx / 4.0f;
         f = a.st.fj[px];
@@ -2353,18 +2400,18 @@ __global__ __launch_bounds__(256) void k_shard_render_final(ShardRayArgs a) {
     const int px = y * a.width + x;
     const RayGeo r = shard_ray(a, x, y);
     float t;
-    int2 rec = make_int2(INT_MAX, 0);
+    int2 rec = mk_rec(INT_MAX, 0);
     if (shard_resolve(a, r, px, npx, &t)) {
         a.st.t[px] = t;
         const float hx = fmaf(t, r.dx, r.ox), hy = fmaf(t, r.dy, r.oy), hz = fmaf(t, r.dz, r.oz);
         if (sample_owner(a.g, hz) == a.g.shard) {
             uint8_t b = 0, gch = 0, rr = 0;
             shade_hit(a.g, a.b, tri_setup(a.g, hx, hy, hz), a.kind, a.color_i32, a.palette, &b, &gch, &rr);
-            rec = make_int2(0, (int)((unsigned)b | ((unsigned)gch << 8) | ((unsigned)rr << 16)));
+            rec = mk_rec(0, (int)((unsigned)b | ((unsigned)gch << 8) | ((unsigned)rr << 16)));
         }
     } else {
         a.st.t[px] = -1.0f;
-        if (a.g.shard == 0) rec = make_int2(0, 0);
+        if (a.g.shard == 0) rec = mk_rec(0, 0);
     }
     a.send[px] = rec;
 }
@@ -2372,7 +2419,7 @@ __global__ __launch_bounds__(256) void k_shard_render_final(ShardRayArgs a) {
 __global__ __launch_bounds__(256) void k_shard_render_finish(ShardRayArgs a) {
     const int npx = a.width * a.height;
     for (int px = blockIdx.x * blockDim.x + threadIdx.x; px < npx; px += gridDim.x * blockDim.x) {
-        const unsigned v = (unsigned)gather_min(a.gathered, a.g.nshards, npx, px).y;
+        const unsigned v = (unsigned)rval(gather_min(a.gathered, a.nrec, npx, px));
         a.out_bgr[(size_t)px * 3 + 0] = (uint8_t)(v & 0xFF);
         a.out_bgr[(size_t)px * 3 + 1] = (uint8_t)((v >> 8) & 0xFF);
         a.out_bgr[(size_t)px * 3 + 2] = (uint8_t)((v >> 16) & 0xFF);

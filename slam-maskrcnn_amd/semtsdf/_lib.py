@@ -38,6 +38,8 @@ RENDER_LABEL = 0
 RENDER_COLOR = 1
 RAY_ASSOC = 2
 ASSOC_PARTIAL_LEN = 3168
+EXCHANGE_ALLGATHER = 0
+EXCHANGE_MIN = 1
 
 
 class SemTSDFError(RuntimeError):
@@ -147,14 +149,16 @@ SIGNATURES = {
     "semtsdf_orbit_camera": (_I, [_P, _F, _F, _P, _P]),
     "semtsdf_raycast": (_I, [_P, _P, _P, _I, _P, _P, _P]),
     "semtsdf_raycast_dev": (_I, [_P, _P, _P, _I, _P, _P, _P]),
-    "semtsdf_shard_ray_begin": (_I, [_P, _I, _P, _P, C.POINTER(C.c_size_t), C.POINTER(C.c_int)]),
+    "semtsdf_shard_ray_begin": (_I, [_P, _I, _P, _P, _I, C.POINTER(C.c_size_t), C.POINTER(C.c_int)]),
     "semtsdf_shard_ray_step": (_I, [_P, _I, _P, _P, _P]),
     "semtsdf_shard_render_finish": (_I, [_P, _P, _P, _P, _P]),
     "semtsdf_shard_assoc_partial": (_I, [_P, _P, _P, _P, _P]),
     "semtsdf_shard_assoc_apply": (_I, [_P, _P, _P, C.POINTER(AssocStats), _P]),
     "semtsdf_shard_note_integrated": (_I, [_P, _P, _P]),
+    "semtsdf_min_i64": (_I, [_P, _P, C.c_size_t, _P]),
     "semtsdf_copy_bandwidth": (_I, [_I, C.c_size_t, _I, C.POINTER(C.c_double)]),
     "semtsdf_download": (_I, [_P, _P, _P, _P, _P, _P, _P]),
+    "semtsdf_download_slab": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P]),
     "semtsdf_upload": (_I, [_P, _P, _P, _P, _P, _P, _P]),
     "semtsdf_set_instrumentation": (_I, [_P, _I]),
     "semtsdf_get_timing": (_I, [_P, C.POINTER(Timing)]),

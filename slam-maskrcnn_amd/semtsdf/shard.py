@@ -97,10 +97,20 @@ class ShardLayout:
 # ---------------------------------------------------------------------------------------
 # Z-sharded raycast / association protocol (include/semtsdf.h "Z-sharded raycast").
 # ---------------------------------------------------------------------------------------
-def _run_ray_protocol(members, gathered_ptr, allgather, kind, cam, c, stream):
-    """members: [(Volume, send_ptr)] of the shards driven by this process (one per rank in
-    a distributed group; all of them for an in-process group).  allgather() fills the
-    gathered buffer [nshards][record] from every shard's send buffer, in shard order."""
+def _exchange_code(exchange: str) -> int:
+    from . import _lib as L
+
+    if exchange not in ("allgather", "min"):
+        raise ValueError(f"exchange must be 'allgather' or 'min', got {exchange!r}")
+    return L.EXCHANGE_MIN if exchange == "min" else L.EXCHANGE_ALLGATHER
+
+
+def _run_ray_protocol(members, exchange_step, kind, cam, c, stream, exchange: int):
+    """members: [Volume] of the shards driven by this process (one per rank in a distributed
+    group; all of them for an in-process group).  exchange_step(step) -> (send_ptrs, fn):
+    the send buffer of every member for this step and the function that exchanges them
+    and returns the device pointer of the exchanged records.  Returns that pointer after
+    the last step (the input of render_finish / assoc_partial)."""
     import ctypes as C
 
     from . import _lib as L
@@ -110,33 +120,37 @@ def _run_ray_protocol(members, gathered_ptr, allgather, kind, cam, c, stream):
     cv = L.f32(c, 3) if c is not None else None
     nsteps = C.c_int()
     rec = C.c_size_t()
-    for vol, _ in members:
-        L.check(lib.semtsdf_shard_ray_begin(vol.handle, int(kind), L.ptr(camv), L.ptr(cv), C.byref(rec),
+    for vol in members:
+        L.check(lib.semtsdf_shard_ray_begin(vol.handle, int(kind), L.ptr(camv), L.ptr(cv), int(exchange), C.byref(rec),
                                             C.byref(nsteps)))
+    gathered = None
     for step in range(nsteps.value):
-        for vol, send in members:
-            L.check(lib.semtsdf_shard_ray_step(vol.handle, step, C.c_void_p(gathered_ptr) if step else None,
+        sends, fn = exchange_step(step)
+        for vol, send in zip(members, sends):
+            L.check(lib.semtsdf_shard_ray_step(vol.handle, step, C.c_void_p(gathered) if step else None,
                                                C.c_void_p(send), stream))
-        allgather()
-    return rec.value
+        gathered = fn()
+    return gathered
 
 
 class LocalShardGroup:
     """All shards of a Z-sharded volume driven from one process (tests, or several shards
-    per GPU): the all-gather is a device-to-device copy on one stream."""
+    per GPU): the exchange is device-to-device copies (all-gather) or an element-wise int64
+    minimum (the all-reduce MIN) on one stream."""
 
-    def __init__(self, vols):
+    def __init__(self, vols, exchange: str = "allgather"):
         from . import _lib as L
         from .volume import DeviceBuffer
 
         self.vols = list(vols)
         self.n = len(self.vols)
+        self.exchange = _exchange_code(exchange)
         v0 = self.vols[0]
         self.W, self.H = v0.W, v0.H
         npx = self.W * self.H
         self.rec = 8 * npx
         self.send = [DeviceBuffer(self.rec) for _ in self.vols]
-        self.gathered = DeviceBuffer(self.n * self.rec)
+        self.gathered = DeviceBuffer((self.n if self.exchange == L.EXCHANGE_ALLGATHER else 1) * self.rec)
         self.partial = [DeviceBuffer(8 * L.ASSOC_PARTIAL_LEN) for _ in self.vols]
         self.reduced = DeviceBuffer(8 * L.ASSOC_PARTIAL_LEN)
         self.stream = v0.stream  # every call goes on shard 0's stream: one order for all
@@ -146,27 +160,38 @@ class LocalShardGroup:
 
         return C.c_void_p(self.stream)
 
-    def _allgather(self):
+    def _exchange(self):
         import ctypes as C
 
         from . import _lib as L
 
         lib = L.load()
-        for r, sb in enumerate(self.send):
-            L.check(lib.semtsdf_memcpy(C.c_void_p(self.gathered.ptr + r * self.rec), C.c_void_p(sb.ptr), self.rec,
-                                       3, self._s()))
+        if self.exchange == L.EXCHANGE_ALLGATHER:
+            for r, sb in enumerate(self.send):
+                L.check(lib.semtsdf_memcpy(C.c_void_p(self.gathered.ptr + r * self.rec), C.c_void_p(sb.ptr), self.rec, 3,
+                                           self._s()))
+        else:
+            L.check(lib.semtsdf_memcpy(C.c_void_p(self.gathered.ptr), C.c_void_p(self.send[0].ptr), self.rec, 3,
+                                       self._s()))
+            for sb in self.send[1:]:
+                L.check(lib.semtsdf_min_i64(C.c_void_p(self.gathered.ptr), C.c_void_p(sb.ptr), self.rec // 8,
+                                            self._s()))
+        return self.gathered.ptr
+
+    def _protocol(self, kind, cam, c):
+        sends = [b.ptr for b in self.send]
+        return _run_ray_protocol(self.vols, lambda step: (sends, self._exchange), kind, cam, c, self._s(),
+                                 self.exchange)
 
     def raycast_dev(self, s2w, c, mode, out_ptr: int, t_ptr: int | None = None):
         import ctypes as C
 
         from . import _lib as L
 
-        members = list(zip(self.vols, [b.ptr for b in self.send]))
-        _run_ray_protocol(members, self.gathered.ptr, self._allgather, mode, s2w, c, self._s())
-        # every shard can composite the gathered records; shard 0 writes the image
-        L.check(L.load().semtsdf_shard_render_finish(self.vols[0].handle, C.c_void_p(self.gathered.ptr),
-                                                     C.c_void_p(out_ptr), C.c_void_p(t_ptr) if t_ptr else None,
-                                                     self._s()))
+        g = self._protocol(mode, s2w, c)
+        # every shard can composite the exchanged records; shard 0 writes the image
+        L.check(L.load().semtsdf_shard_render_finish(self.vols[0].handle, C.c_void_p(g), C.c_void_p(out_ptr),
+                                                     C.c_void_p(t_ptr) if t_ptr else None, self._s()))
 
     def raycast(self, s2w, c, mode, want_t=False):
         import numpy as np
@@ -193,11 +218,10 @@ class LocalShardGroup:
         from . import _lib as L
 
         lib = L.load()
-        members = list(zip(self.vols, [b.ptr for b in self.send]))
-        _run_ray_protocol(members, self.gathered.ptr, self._allgather, L.RAY_ASSOC, E, None, self._s())
+        g = self._protocol(L.RAY_ASSOC, E, None)
         for v, m, pb in zip(self.vols, mask_ptrs, self.partial):
-            L.check(lib.semtsdf_shard_assoc_partial(v.handle, C.c_void_p(self.gathered.ptr), C.c_void_p(m),
-                                                    C.c_void_p(pb.ptr), self._s()))
+            L.check(lib.semtsdf_shard_assoc_partial(v.handle, C.c_void_p(g), C.c_void_p(m), C.c_void_p(pb.ptr),
+                                                    self._s()))
         _sum_int64_dev([pb.ptr for pb in self.partial], self.reduced.ptr, L.ASSOC_PARTIAL_LEN, self.stream)
         stats = []
         for v, m in zip(self.vols, mask_ptrs):
@@ -240,10 +264,18 @@ def _sum_int64_dev(ptrs, out_ptr, n, stream):
 
 class DistShardGroup:
     """One shard per rank of a torch.distributed process group (RCCL on MI355X; gloo for
-    CPU-side rehearsal).  Buffers are torch CUDA tensors; every library call goes on the
-    current torch stream so collectives and kernels are stream-ordered."""
+    CPU-side rehearsal).  Buffers are torch CUDA tensors.  The volume's own HIP stream is
+    made torch's current stream (an ExternalStream) around every call, so the library's
+    kernels and the collectives (which order themselves after the current stream) share
+    one order; torch's default stream would be the NULL stream, which the non-blocking
+    volume stream does not synchronise with.
 
-    def __init__(self, vol, group=None):
+    exchange "min" (default): between protocol steps one all_reduce(MIN) of the 8-byte
+    int64 records (2.46 MB per rank at 640x480, whatever the group size; the step buffers
+    alternate so a step reads the previous step's reduced records while writing its own);
+    "allgather": all_gather_into_tensor of every rank's records (N x 2.46 MB)."""
+
+    def __init__(self, vol, group=None, exchange: str = "min"):
         import torch
         import torch.distributed as dist
 
@@ -256,46 +288,63 @@ class DistShardGroup:
         self.rank = dist.get_rank(group)
         if vol.params.z_nshards != self.n or vol.params.z_shard != self.rank:
             raise ValueError("volume shard does not match the process group rank")
+        self.exchange = _exchange_code(exchange)
         self.W, self.H = vol.W, vol.H
         npx = self.W * self.H
         dev = torch.device("cuda", torch.cuda.current_device())
         self.device = dev
-        self.send = torch.empty(2 * npx, dtype=torch.int32, device=dev)
-        self.gathered = torch.empty(self.n * 2 * npx, dtype=torch.int32, device=dev)
+        self.tstream = torch.cuda.ExternalStream(vol.stream, device=dev)
+        self.bufs = [torch.empty(npx, dtype=torch.int64, device=dev) for _ in range(2)]
+        self.gathered = torch.empty(self.n * npx, dtype=torch.int64, device=dev) \
+            if self.exchange == L.EXCHANGE_ALLGATHER else None
         self.partial = torch.empty(L.ASSOC_PARTIAL_LEN, dtype=torch.int64, device=dev)
         self.nccl = dist.get_backend(group) == "nccl"
-        self._parts = None if self.nccl else list(self.gathered.view(self.n, 2 * npx).unbind(0))
+        self._parts = None if (self.nccl or self.gathered is None) else list(self.gathered.view(self.n, npx).unbind(0))
 
     def _stream(self):
         import ctypes as C
 
+        return C.c_void_p(self.vol.stream)
+
+    def _on_stream(self):
         import torch
 
-        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        return torch.cuda.stream(self.tstream)
 
-    def _allgather(self):
-        if self.nccl:
-            self.dist.all_gather_into_tensor(self.gathered, self.send, group=self.group)
-        else:
-            self.dist.all_gather(self._parts, self.send, group=self.group)
+    def _exchange_step(self, step):
+        from . import _lib as L
+
+        send = self.bufs[step % 2] if self.exchange == L.EXCHANGE_MIN else self.bufs[0]
+
+        def fn():
+            if self.exchange == L.EXCHANGE_MIN:
+                self.dist.all_reduce(send, op=self.dist.ReduceOp.MIN, group=self.group)
+                return send.data_ptr()
+            if self.nccl:
+                self.dist.all_gather_into_tensor(self.gathered, send, group=self.group)
+            else:
+                self.dist.all_gather(self._parts, send, group=self.group)
+            return self.gathered.data_ptr()
+
+        return [send.data_ptr()], fn
 
     def raycast_dev(self, s2w, c, mode, out_ptr: int, t_ptr: int | None = None):
         import ctypes as C
 
         from . import _lib as L
 
-        _run_ray_protocol([(self.vol, self.send.data_ptr())], self.gathered.data_ptr(), self._allgather, mode, s2w,
-                          c, self._stream())
-        L.check(L.load().semtsdf_shard_render_finish(self.vol.handle, C.c_void_p(self.gathered.data_ptr()),
-                                                     C.c_void_p(out_ptr), C.c_void_p(t_ptr) if t_ptr else None,
-                                                     self._stream()))
+        with self._on_stream():
+            g = _run_ray_protocol([self.vol], self._exchange_step, mode, s2w, c, self._stream(), self.exchange)
+            L.check(L.load().semtsdf_shard_render_finish(self.vol.handle, C.c_void_p(g), C.c_void_p(out_ptr),
+                                                         C.c_void_p(t_ptr) if t_ptr else None, self._stream()))
 
     def raycast(self, s2w, c, mode, want_t=False):
         import torch
 
-        out = torch.empty((self.H, self.W, 3), dtype=torch.uint8, device=self.device)
-        t = torch.empty((self.H, self.W), dtype=torch.float32, device=self.device) if want_t else None
-        self.raycast_dev(s2w, c, mode, out.data_ptr(), t.data_ptr() if t is not None else None)
+        with self._on_stream():
+            out = torch.empty((self.H, self.W, 3), dtype=torch.uint8, device=self.device)
+            t = torch.empty((self.H, self.W), dtype=torch.float32, device=self.device) if want_t else None
+            self.raycast_dev(s2w, c, mode, out.data_ptr(), t.data_ptr() if t is not None else None)
         return (out, t) if want_t else out
 
     def associate_dev(self, mask_ptr: int, E, want_stats=False):
@@ -304,16 +353,16 @@ class DistShardGroup:
         from . import _lib as L
 
         lib = L.load()
-        _run_ray_protocol([(self.vol, self.send.data_ptr())], self.gathered.data_ptr(), self._allgather,
-                          L.RAY_ASSOC, E, None, self._stream())
-        L.check(lib.semtsdf_shard_assoc_partial(self.vol.handle, C.c_void_p(self.gathered.data_ptr()),
-                                                C.c_void_p(mask_ptr), C.c_void_p(self.partial.data_ptr()),
-                                                self._stream()))
-        self.dist.all_reduce(self.partial, op=self.dist.ReduceOp.SUM, group=self.group)
-        st = L.AssocStats() if want_stats else None
-        L.check(lib.semtsdf_shard_assoc_apply(self.vol.handle, C.c_void_p(self.partial.data_ptr()),
-                                              C.c_void_p(mask_ptr), C.byref(st) if st is not None else None,
-                                              self._stream()))
+        with self._on_stream():
+            g = _run_ray_protocol([self.vol], self._exchange_step, L.RAY_ASSOC, E, None, self._stream(),
+                                  self.exchange)
+            L.check(lib.semtsdf_shard_assoc_partial(self.vol.handle, C.c_void_p(g), C.c_void_p(mask_ptr),
+                                                    C.c_void_p(self.partial.data_ptr()), self._stream()))
+            self.dist.all_reduce(self.partial, op=self.dist.ReduceOp.SUM, group=self.group)
+            st = L.AssocStats() if want_stats else None
+            L.check(lib.semtsdf_shard_assoc_apply(self.vol.handle, C.c_void_p(self.partial.data_ptr()),
+                                                  C.c_void_p(mask_ptr), C.byref(st) if st is not None else None,
+                                                  self._stream()))
         return st
 
     def parse_frame_dev(self, depth_ptr: int, rgb_ptr: int, mask_ptr: int, E):

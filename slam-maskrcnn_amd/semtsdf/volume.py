@@ -228,6 +228,19 @@ class Volume:
                 out[k] = v
         return out
 
+    def download_slab(self, x0: int, x1: int, sdf=True, wt=True, color=True, hist=False, cls=False):
+        """The x-planes [x0, x1) of download() (semtsdf_download_slab)."""
+        n = (int(x1) - int(x0)) * int(self.local_dim[1]) * int(self.local_dim[2])
+        ci32 = bool(self.params.flags & L.F_COLOR_I32)
+        arrs = {"sdf": np.zeros(n, np.float32) if sdf else None, "wt": np.zeros(n, np.int32) if wt else None,
+                "color": np.zeros(n * 3, np.int32 if ci32 else np.uint8) if color else None,
+                "hist": np.zeros(n * L.MAX_OBJECTS, np.uint32) if hist else None,
+                "cls": np.zeros(n, np.int32) if cls else None, "cls_cnt": np.zeros(n, np.int32) if cls else None}
+        L.check(L.load().semtsdf_download_slab(self._h, int(x0), int(x1), *[L.ptr(arrs[k]) for k in
+                                                                             ("sdf", "wt", "color", "hist", "cls",
+                                                                              "cls_cnt")]))
+        return {k: v for k, v in arrs.items() if v is not None}
+
     def upload(self, sdf=None, wt=None, color=None, hist=None, cls=None, cls_cnt=None):
         ci32 = bool(self.params.flags & L.F_COLOR_I32)
 

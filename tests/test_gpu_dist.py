@@ -1,0 +1,183 @@
+"""C4 rows on the GPU: the distributed Z-slab shard group and the full
+1024^3 volume.
+
+* DistShardGroup (semtsdf/shard.py; torch.distributed, RCCL on a multi-GPU node): two ranks
+  spawned as separate processes on the one GPU of the test box, gloo carrying the
+  collectives (RCCL refuses two ranks on one device).  Every rank runs the sharded
+  per-frame pipeline (association protocol + all-reduce of the partial tables, integrate)
+  and the sharded raycast; rank 0 also runs the single-volume pipeline.  Relabelled masks,
+  association decisions, the gathered volume and the rendered images and hit distances
+  must equal the single volume bit for bit, with either exchange (all-reduce MIN of the
+  int64 records, or all-gather).
+* A 1024^3 semantic volume (144 GiB of state on one GPU) integrated through the HIP path,
+  x-slabs checked bit for bit against the C oracle run on those planes only.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+KI = (520.9, 521.0, 325.1, 249.7)
+DIMS = (48, 40, 64)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _params(semtsdf, L, f0, shard=None, nshards=1, chunk=8):
+    p = semtsdf.default_params(64, KI, 640, 480)
+    p.dim[0], p.dim[1], p.dim[2] = DIMS
+    semtsdf.place_from_frame(p, f0.depth, float(np.mean(f0.depth[f0.depth > 0])) / 5000.0, L.PLACE_SFM)
+    p.flags = L.F_SEMANTIC | L.F_GATE_COLOR
+    if shard is not None:
+        p.z_nshards, p.z_shard, p.z_chunk = nshards, shard, chunk
+    return p
+
+
+def _rank(rank, world, port, exchange, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import semtsdf
+        from semtsdf import _lib as L
+        from semtsdf.shard import DistShardGroup
+        from semtsdf.synth import SyntheticStream
+
+        semtsdf.load()
+        st = SyntheticStream(seed=0)
+        frames = [st.frame(k) for k in range(6)]
+        vol = semtsdf.Volume(_params(semtsdf, L, frames[0], rank, world), 0)
+        grp = DistShardGroup(vol, exchange=exchange)
+        single = semtsdf.Volume(_params(semtsdf, L, frames[0]), 0) if rank == 0 else None
+        out = {"masks": [], "luts": [], "single_masks": [], "single_luts": []}
+        for k in range(1, 6):
+            fr = frames[k]
+            E = (fr.w2c @ frames[0].c2w).astype(np.float32)
+            d = torch.from_numpy(fr.depth.view(np.int16)).cuda()
+            r = torch.from_numpy(fr.rgb).cuda()
+            m = torch.from_numpy(fr.mask.copy()).cuda()
+            torch.cuda.synchronize()  # inputs copied by torch's stream before the volume's stream reads them
+            if vol.state().n_obs > 0:
+                stt = grp.associate_dev(m.data_ptr(), E, want_stats=True)
+                out["luts"].append(bytes(stt.lut))
+            vol.integrate_dev(d.data_ptr(), r.data_ptr(), m.data_ptr(), E, grp._stream())
+            L.check(L.load().semtsdf_shard_note_integrated(vol.handle, L.ptr(m.data_ptr()), grp._stream()))
+            torch.cuda.synchronize()
+            out["masks"].append(m.cpu().numpy())
+            if single is not None:
+                ms = np.ascontiguousarray(fr.mask.copy())
+                s1 = single.parse_frame(fr.depth, fr.rgb, ms, E)
+                out["single_masks"].append(ms)
+                if k >= 2:
+                    out["single_luts"].append(bytes(s1.lut))
+        dist_c = float(np.mean(frames[0].depth[frames[0].depth > 0]) / 5000.0)
+        out["images"], out["single_images"] = [], []
+        p = vol.params
+        for mode in (L.RENDER_LABEL, L.RENDER_COLOR):
+            for angle in (0.0, 0.3):
+                s2w, c = semtsdf.orbit_camera(list(p.Kinv), angle, dist_c)
+                img, t = grp.raycast(s2w, c, mode, want_t=True)
+                torch.cuda.synchronize()
+                out["images"].append((img.cpu().numpy(), t.cpu().numpy()))
+                if single is not None:
+                    out["single_images"].append(single.raycast(s2w, c, mode, want_t=True))
+        torch.cuda.synchronize()
+        out["local"] = vol.download(hist=True)
+        out["state"] = (int(vol.state().n_obs), int(vol.state().num_objs))
+        if single is not None:
+            out["single"] = single.download(hist=True)
+            out["single_state"] = (int(single.state().n_obs), int(single.state().num_objs))
+            single.close()
+        vol.close()
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("exchange", ["min", "allgather"])
+def test_dist_shard_group_two_ranks_equals_single_volume(exchange):
+    import torch.multiprocessing as mp
+
+    from semtsdf.shard import ShardLayout
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, exchange, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        rank, out = q.get(timeout=240)
+        res[rank] = out
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0, f"rank exit code {p.exitcode}"
+    r0 = res[0]
+    for rank in (0, 1):
+        o = res[rank]
+        for k, (m, ms) in enumerate(zip(o["masks"], r0["single_masks"])):
+            assert np.array_equal(m.reshape(-1), ms.reshape(-1)), (rank, k)
+        assert o["luts"] == r0["single_luts"], rank
+        assert o["state"] == r0["single_state"], rank
+        for i, ((img, t), (simg, st)) in enumerate(zip(o["images"], r0["single_images"])):
+            assert (st >= 0).mean() > 0.2
+            dt = (t.view(np.uint32) != st.view(np.uint32))
+            di = (img != simg).any(axis=-1)
+            assert not dt.any() and not di.any(), (rank, i, int(dt.sum()), int(di.sum()), t[dt][:5], st[dt][:5])
+    lay = ShardLayout(DIMS[2], 2, 8)
+    for key, extra in (("sdf", ()), ("wt", ()), ("color", (3,)), ("hist", (32,))):
+        parts = [res[r]["local"][key].reshape((DIMS[0], DIMS[1], -1) + extra) for r in (0, 1)]
+        got = lay.gather(parts, DIMS[0], DIMS[1])
+        ref = r0["single"][key].reshape(DIMS + extra)
+        assert np.array_equal(got.view(np.uint8), ref.view(np.uint8)), key
+
+
+def test_full_size_1024_semantic_slabs(oracle):
+    """C4's volume size on one GPU: 1024^3 semantic (sdf, weight, colour, 32-bin histogram =
+    144 GiB), 3 frames of the synthetic stream with culling on; x-slabs through the middle
+    and the edges of the frustum equal the C oracle's run on the same planes bit for bit."""
+    import semtsdf
+    from semtsdf import _lib as L
+    from semtsdf.synth import SyntheticStream
+
+    st = SyntheticStream(seed=0)
+    frames = [st.frame(k) for k in range(4)]
+    p = semtsdf.default_params(1024, KI, 640, 480)
+    semtsdf.place_from_frame(p, frames[0].depth, float(np.mean(frames[0].depth[frames[0].depth > 0])) / 5000.0,
+                             L.PLACE_SFM)
+    p.flags = L.F_SEMANTIC | L.F_GATE_COLOR
+    vol = semtsdf.Volume(p, 0)
+    assert vol.state().device_bytes > 140 * 2 ** 30
+    Es = []
+    for fr in frames[1:]:
+        E = (fr.w2c @ frames[0].c2w).astype(np.float32)
+        Es.append(E)
+        vol.integrate(fr.depth, fr.rgb, fr.gt_ids, E)
+    g = oracle.OGeom.from_params(p)
+    K = list(p.K)
+    touched = 0
+    for x0 in (96, 508, 900):
+        x1 = x0 + 8
+        ost = oracle.OState([8, 1024, 1024], p.mu, semantic=True)
+        for fr, E in zip(frames[1:], Es):
+            touched += int(oracle.integrate_slab(g, ost, K, E, fr.depth, fr.rgb, (x0, x1), mask=fr.gt_ids)[0])
+        got = vol.download_slab(x0, x1, hist=True)
+        assert np.array_equal(got["sdf"].view(np.uint32), ost.sdf.view(np.uint32)), x0
+        assert np.array_equal(got["wt"], ost.wt) and np.array_equal(got["color"], ost.color), x0
+        assert np.array_equal(got["hist"], ost.hist), x0
+    assert touched > 1_000_000
+    vol.close()

@@ -507,20 +507,24 @@ def _shard_handles(S, p, nshards, chunk):
     return shards
 
 
-@pytest.mark.parametrize("nshards,chunk", [(2, 8), (3, 5), (4, 16), (1, 64)])
-def test_sharded_pipeline_equals_single_volume(S, oracle, stream, nshards, chunk):
+@pytest.mark.parametrize("nshards,chunk,dimz,exchange", [(2, 8, 64, "allgather"), (3, 5, 64, "min"),
+                                                         (4, 16, 64, "allgather"), (1, 64, 64, "min"),
+                                                         (8, 63, 512, "min")])
+def test_sharded_pipeline_equals_single_volume(S, oracle, stream, nshards, chunk, dimz, exchange):
     """The Z-sharded association + integrate + raycast protocol (k_shard_*, host
     LocalShardGroup) reproduces the single-volume pipeline bit for bit: relabelled masks,
-    decisions, the gathered volume, rendered images and hit distances."""
+    decisions, the gathered volume, rendered images and hit distances; with the exchange
+    between steps as an all-gather or as an int64 minimum (the all-reduce MIN of the
+    distributed group); (8, 63) is the bench's chunking of a 512-plane z axis over 8 shards."""
     from semtsdf.shard import LocalShardGroup, ShardLayout
     from semtsdf.volume import DeviceBuffer
 
     st, frames = stream
     semtsdf, L = S
-    dims = (48, 40, 64)
+    dims = (48, 40, dimz)
     p, vol, g, ost = make(S, oracle, dims, frames[0], 0x3)
     shards = _shard_handles(S, p, nshards, chunk)
-    grp = LocalShardGroup(shards)
+    grp = LocalShardGroup(shards, exchange=exchange)
     npx = 640 * 480
     dbuf, rbuf = DeviceBuffer(npx * 2), DeviceBuffer(npx * 3)
     mbufs = [DeviceBuffer(npx) for _ in shards]
