@@ -1,26 +1,41 @@
 """Benchmark of the semantic TSDF hot path on MI355X (BASELINE.json metric:
 "Mvoxel-updates/s + frames/s, 512^3 semantic TSDF @ 640x480").
 
-One step = one frame of the per-frame integrate (src/SfM_CUDA/tsdf.cu:18-70 semantics:
-SDF + gated colour + 32-bin instance histogram) over the whole volume, inputs resident
-in HBM.  N=1 runs configuration C3 (512^3 semantic, synthetic 640x480 stream with masks).
-N>1 ranks (torchrun, one process per GPU) each own an interleaved Z-slab shard of a
-512 x 512 x (512 N) volume covering the same physical box (the SfM placement divides
-each axis by its own dim, so z resolution grows N-fold) -- every GPU owns 512^3 voxels
-and sees the same share of the surface band per frame (weak scaling; Z-slab sharding
-needs no collective for integrate).
-
-value = voxels integrated by all ranks / max-over-ranks wall time of the K timed steps.
-Extra fields: frames/s of the full per-frame pipeline (association raycast + relabel +
-integrate, N=1), render time, the integrate kernel's HBM roofline and the CPU baseline
-(NumPy restatement of tsdf.py:78-120 + SfM gate, bounded sample, 1 core).
+N = 1 (default): configuration C3.  One step = one frame of the integrate
+(src/SfM_CUDA/tsdf.cu:18-70 semantics: SDF + gated colour + 32-bin instance histogram; the
+frame prepass + unit cull + integrate kernel) over the whole 512^3 volume, inputs resident
+in HBM; value = voxels of the volume x frames / wall time of the K timed steps (the
+KinectFusion "voxel updates" convention: every voxel is visited per frame, dead units by
+the culler).  Extra objects of the same line:
+  roofline      the integrate kernel: algorithmic bytes (the reference's types, §8d) per
+                launch / its HIP-event duration, against 8 TB/s; traffic = PMC bytes of the
+                same kernel binary (stamped by library hash, tools/traffic.py), else null;
+  pipeline      §8d frames/s of C3: per frame the host TUM pose path (groundtruth lines ->
+                read_traj -> parse_pos), async H2D of depth + RGB + mask from pinned memory
+                on a copy stream, association raycast + relabel, integrate and one live
+                raycast view, 100 frames after 5 warm-up frames;
+  orbit         the live orbit raycast of kernel.cpp:101-107 (angle += 0.01 at the mean
+                depth), views/s;
+  c2            C2: 256^3 TSDF + colour (NumPy rule: i32 colour, ungated), frames resident,
+                Mvoxel-updates/s and upload + integrate frames/s, roofline on 22 N_touch + 5 W H;
+  c4_single_gpu C4's 1024^3 semantic volume on one GPU, one step = integrate + one raycast
+                view: the base of the N > 1 strong-scaling lines;
+  cpu_baseline  the NumPy restatement of tsdf.py:78-120 (+ SfM gate/histogram) on the host.
+N > 1 (torch.distributed.run, one process per GPU, RCCL): configuration C4, strong scaling
+of the fixed 1024^3 semantic volume: rank r integrates its interleaved Z-slab shard
+(no collective) and every step composites one raycast view across the shards (the
+DistShardGroup protocol: an RCCL all-reduce MIN of 8-byte per-pixel records between
+its steps); value = 1024^3 x K / max-over-ranks wall time, so value_N / c4_single_gpu.value
+is the speed-up.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -31,17 +46,18 @@ sys.path.insert(0, os.path.join(ROOT, "slam-maskrcnn_amd"))
 METRIC = "Mvoxel-updates/s + frames/s, 512^3 semantic TSDF @ 640x480"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 KI = (520.9, 521.0, 325.1, 249.7)
+W, H = 640, 480
+NPX = W * H
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# ----------------------------------------------------------------------------- process group
 def dist_setup(n_gpus):
-    """One process per GPU (torch.distributed.run).  The data path has no collective (each
-    rank integrates its own Z-slab shard); the process group only carries the barrier and
-    the max/sum of the timings.  Backend: RCCL ("nccl") by default; BENCH_DIST_BACKEND=gloo
-    rehearses N ranks on fewer GPUs (device = LOCAL_RANK % device count)."""
+    """One process per GPU (torch.distributed.run).  Backend RCCL ("nccl") by default;
+    BENCH_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (device = LOCAL_RANK % count)."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -92,6 +108,7 @@ def sum_over_ranks(pg, device, x: float) -> float:
     return x if pg is None else _reduce(pg, device, x, pg.ReduceOp.SUM)
 
 
+# ----------------------------------------------------------------------------- CPU baseline
 def _cpu_slab_worker(job):
     """Integrate one x-slab of the volume with the NumPy restatement (1 BLAS thread).
     Returns (voxel-updates, seconds)."""
@@ -168,6 +185,7 @@ def host_cores() -> int:
     return max(1, n)
 
 
+# ----------------------------------------------------------------------------- helpers
 def copy_bandwidth(device: int, nbytes: int = 1 << 30) -> float:
     """Achievable HBM bandwidth (GB/s, read + write) of a float4 device copy (library kernel),
     for context beside the 8 TB/s spec peak."""
@@ -180,6 +198,325 @@ def copy_bandwidth(device: int, nbytes: int = 1 << 30) -> float:
     return out.value
 
 
+def loaded_lib_sha256() -> str:
+    from semtsdf import _lib as L
+
+    path = os.environ.get("SEMTSDF_LIB", L.LIB_PATH)
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def read_traffic(path, dim, world):
+    """PMC bytes per launch of the integrate kernel, only if measured on this very library
+    binary (tools/traffic.py stamps its SHA-256) and configuration."""
+    if not path or not os.path.exists(path):
+        return None, "no traffic record"
+    try:
+        with open(path) as f:
+            tj = json.load(f)
+    except Exception as e:  # pragma: no cover
+        return None, f"unreadable traffic record: {e}"
+    if tj.get("dim") != dim or tj.get("n_gpus", 1) != world:
+        return None, "traffic record is for another configuration"
+    if tj.get("lib_sha256") != loaded_lib_sha256():
+        return None, "traffic record was measured on another library build"
+    return tj.get("bytes_per_launch"), f"PMC FETCH_SIZE x2 + WRITE_SIZE of lib {tj['lib_sha256'][:12]}"
+
+
+def place(semtsdf, L, D, f0, dimz=None):
+    p = semtsdf.default_params(D, KI, W, H)
+    if dimz is not None:
+        p.dim[2] = dimz
+    semtsdf.place_from_frame(p, f0.depth, float(np.mean(f0.depth[f0.depth > 0])) / 5000.0, L.PLACE_SFM)
+    return p
+
+
+def resident_frames(frames, with_mask=True, ids=False):
+    """Depth, RGB and masks of `frames` in HBM (library allocations)."""
+    from semtsdf.volume import DeviceBuffer
+
+    n = len(frames)
+    dbuf, rbuf = DeviceBuffer(n * NPX * 2), DeviceBuffer(n * NPX * 3)
+    mbuf = DeviceBuffer(n * NPX) if with_mask else None
+    for i, fr in enumerate(frames):
+        dbuf.upload(fr.depth, None, i * NPX * 2)
+        rbuf.upload(fr.rgb, None, i * NPX * 3)
+        if with_mask:
+            mbuf.upload(fr.gt_ids if ids else fr.mask, None, i * NPX)
+    return dbuf, rbuf, mbuf
+
+
+def timed_integrate(vol, step, K, warmup, pg=None, device=0):
+    """Wall time of K steps (barrier + sync on both sides), then the same K steps again
+    with kernel events (integrate kernel, prepass) and once more counting voxels."""
+    for k in range(warmup):
+        step(k)
+    vol.sync()
+    barrier(pg, device)
+    vol.sync()
+    t0 = time.perf_counter()
+    for k in range(K):
+        step(warmup + k)
+    vol.sync()
+    barrier(pg, device)
+    elapsed = time.perf_counter() - t0
+    vol.reset_timing()
+    vol.set_instrumentation(events=True, count=False)
+    for k in range(K):
+        step(warmup + k)
+    vol.sync()
+    tm = vol.timing()
+    vol.reset_timing()
+    vol.set_instrumentation(events=False, count=True)
+    for k in range(K):
+        step(warmup + k)
+    tc = vol.timing()
+    vol.set_instrumentation(events=False, count=False)
+    return elapsed, tm, tc
+
+
+# ----------------------------------------------------------------------------- C3 pipeline
+def run_pipeline(semtsdf, L, p, local, n_frames=100, n_warm=5):
+    """§8d frames/s of C3: host pose path + async H2D (pinned, copy stream) + association
+    raycast + relabel + integrate + one live raycast view per frame."""
+    import torch
+
+    from semtsdf import pose as P
+    from semtsdf import tum
+    from semtsdf.synth import SyntheticStream
+
+    st = SyntheticStream(seed=1, noise=True)
+    n_all = n_frames + n_warm + 1
+    t_gen = time.perf_counter()
+    frames = [st.frame(k) for k in range(n_all)]
+    log(f"[bench] pipeline: generated {n_all} frames in {time.perf_counter() - t_gen:.1f}s")
+    with tempfile.TemporaryDirectory() as d:
+        gt = os.path.join(d, "groundtruth.txt")
+        with open(gt, "w") as f:
+            f.write("\n".join(st.tum_lines(n_all)) + "\n")
+        traj = tum.read_traj(gt)  # tsdf_utils.py:23-29
+    vol = semtsdf.Volume(p, local)
+    dev = torch.device("cuda", local)
+    vstream = torch.cuda.ExternalStream(vol.stream, device=dev)
+    cstream = torch.cuda.Stream(device=dev)
+    # pinned host frames (a capture pipeline's DMA buffers) and a device ring of 2 slots
+    h_d = torch.empty((n_all, NPX), dtype=torch.int16).pin_memory()
+    h_r = torch.empty((n_all, NPX * 3), dtype=torch.uint8).pin_memory()
+    h_m = torch.empty((n_all, NPX), dtype=torch.uint8).pin_memory()
+    for k, fr in enumerate(frames):
+        h_d[k].copy_(torch.from_numpy(fr.depth.reshape(-1).view(np.int16)))
+        h_r[k].copy_(torch.from_numpy(fr.rgb.reshape(-1)))
+        h_m[k].copy_(torch.from_numpy(fr.mask.reshape(-1)))
+    ring = 2
+    d_d = torch.empty((ring, NPX), dtype=torch.int16, device=dev)
+    d_r = torch.empty((ring, NPX * 3), dtype=torch.uint8, device=dev)
+    d_m = torch.empty((ring, NPX), dtype=torch.uint8, device=dev)
+    out = torch.empty(NPX * 3, dtype=torch.uint8, device=dev)
+    copied = [torch.cuda.Event() for _ in range(ring)]
+    used = [torch.cuda.Event() for _ in range(ring)]
+    mean_m = tum.mean_depth_m(frames[0].depth)
+    ext0_inv = np.linalg.inv(P.parse_pos(traj[0, 1:]))  # frame 0 places the volume (tsdf.cu:173-214)
+    torch.cuda.synchronize()
+
+    def upload(k):
+        s = k % ring
+        with torch.cuda.stream(cstream):
+            cstream.wait_event(used[s])
+            d_d[s].copy_(h_d[k], non_blocking=True)
+            d_r[s].copy_(h_r[k], non_blocking=True)
+            d_m[s].copy_(h_m[k], non_blocking=True)
+            copied[s].record(cstream)
+
+    def frame(k):
+        s = k % ring
+        E = P.relative_pose(P.parse_pos(traj[k, 1:]), ext0_inv)  # host pose path (tsdf.cu:217)
+        vstream.wait_event(copied[s])
+        vol.parse_frame_dev(d_d[s].data_ptr(), d_r[s].data_ptr(), d_m[s].data_ptr(), E)
+        s2w, c = semtsdf.orbit_camera(list(p.Kinv), 0.01 * k, mean_m)
+        vol.raycast_dev(s2w, c, L.RENDER_LABEL, out.data_ptr())
+        used[s].record(vstream)
+        if k + ring < n_all:
+            upload(k + ring)
+
+    for k in range(ring):
+        upload(1 + k)
+    for k in range(1, 1 + n_warm):
+        frame(k)
+    vol.sync()
+    torch.cuda.synchronize()
+    vol.reset_timing()
+    vol.set_instrumentation(events=True, count=False)
+    t0 = time.perf_counter()
+    for k in range(1 + n_warm, n_all):
+        frame(k)
+    vol.sync()
+    t1 = time.perf_counter()
+    tm = vol.timing()
+    vol.set_instrumentation(events=False, count=False)
+    st_ = vol.state()
+    # live orbit (kernel.cpp:101-107): angle += 0.01 per view, distance = mean depth
+    n_views = 60
+    vol.reset_timing()
+    vol.set_instrumentation(events=True, count=False)
+    tv0 = time.perf_counter()
+    for v in range(n_views):
+        s2w, c = semtsdf.orbit_camera(list(p.Kinv), 0.01 * (v + 1), mean_m)
+        vol.raycast_dev(s2w, c, L.RENDER_LABEL, out.data_ptr())
+    vol.sync()
+    tv1 = time.perf_counter()
+    tr = vol.timing()
+    vol.set_instrumentation(events=False, count=False)
+    vol.close()
+    return {
+        "frames_per_s": n_frames / (t1 - t0),
+        "ms_per_frame": (t1 - t0) * 1e3 / n_frames,
+        "frames": n_frames, "warmup_frames": n_warm,
+        "per_frame": "host TUM pose (read_traj -> parse_pos) + async pinned H2D of depth/RGB/mask on a copy stream "
+                     "+ association raycast + relabel + integrate + 1 label raycast view",
+        "assoc_ms_per_frame": tm.assoc_ms / max(tm.n_assoc, 1),
+        "integrate_ms_per_frame": tm.integrate_ms / max(tm.n_integrate, 1),
+        "prep_ms_per_frame": tm.prep_ms / max(tm.n_prep, 1),
+        "render_ms_per_view": tm.render_ms / max(tm.n_render, 1),
+        "num_objs": int(st_.num_objs),
+    }, {
+        "views_per_s": n_views / (tv1 - tv0),
+        "render_ms_per_view": tr.render_ms / max(tr.n_render, 1),
+        "views": n_views,
+        "camera": "viewer.cu:137-146 orbit, angle += 0.01 per view (kernel.cpp:104), dist = mean depth of frame 0",
+    }
+
+
+# ----------------------------------------------------------------------------- C2
+def run_c2(semtsdf, L, local, frames, f0, K=30, warmup=3):
+    """C2: 256^3 TSDF + colour (NumPy rule: int32 colour, no gate), synthetic stream."""
+    D = 256
+    p = place(semtsdf, L, D, f0)
+    p.flags = L.F_COLOR_I32
+    vol = semtsdf.Volume(p, local)
+    dbuf, rbuf, _ = resident_frames(frames, with_mask=False)
+    Es = [(fr.w2c @ f0.c2w).astype(np.float32) for fr in frames]
+
+    def step(k):
+        i = k % len(frames)
+        vol.integrate_dev(dbuf.ptr + i * NPX * 2, rbuf.ptr + i * NPX * 3, None, Es[i])
+
+    elapsed, tm, tc = timed_integrate(vol, step, K, warmup)
+    kern_ms = tm.integrate_ms / max(tm.n_integrate, 1)
+    touched = tc.touched / K
+    b = 22.0 * touched + 5.0 * NPX
+    # upload + integrate (§8d C2 frames/s): host frames through the library's H2D path
+    vol.reset()
+    t0 = time.perf_counter()
+    for k in range(K):
+        fr = frames[k % len(frames)]
+        vol.integrate(fr.depth, fr.rgb, None, Es[k % len(frames)])
+    vol.sync()
+    t_up = time.perf_counter() - t0
+    vol.close()
+    dbuf.free()
+    rbuf.free()
+    return {
+        "workload": "C2: 256^3 TSDF + colour (sdf f32, weight i32, colour i32x3, NumPy rule: colour ungated), "
+                    "synthetic 640x480 stream, ground-truth poses",
+        "value": round(D ** 3 * K / elapsed / 1e6, 2), "unit": "Mvoxel-updates/s",
+        "ms_per_step": round(elapsed * 1e3 / K, 4),
+        "integrate_kernel_ms": round(kern_ms, 4),
+        "frames_per_s_upload_integrate": round(K / t_up, 1),
+        "touched_per_frame": int(touched),
+        "roofline": {"bound": "hbm", "achieved": round(b / (kern_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(b / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "algorithmic_bytes_per_launch": int(b), "bytes_rule": "22 N_touch + 5 W H (SURVEY §8d)"},
+    }
+
+
+# ----------------------------------------------------------------------------- C4
+def c4_params(semtsdf, L, f0, world=1, rank=0, chunk=64):
+    p = place(semtsdf, L, 1024, f0)
+    p.flags = L.F_SEMANTIC | L.F_GATE_COLOR
+    if world > 1:
+        p.z_nshards, p.z_shard, p.z_chunk = world, rank, chunk
+    return p
+
+
+def run_c4_single(semtsdf, L, local, frames, f0, K, warmup):
+    """C4's 1024^3 semantic volume whole on one GPU: integrate + one label raycast view per
+    step (the single-GPU base of the strong-scaling lines)."""
+    from semtsdf.volume import DeviceBuffer
+
+    p = c4_params(semtsdf, L, f0)
+    vol = semtsdf.Volume(p, local)
+    dbuf, rbuf, mbuf = resident_frames(frames, ids=True)
+    Es = [(fr.w2c @ f0.c2w).astype(np.float32) for fr in frames]
+    mean_m = float(np.mean(f0.depth[f0.depth > 0]) / 5000.0)
+    out = DeviceBuffer(NPX * 3)
+
+    def step(k):
+        i = k % len(frames)
+        vol.integrate_dev(dbuf.ptr + i * NPX * 2, rbuf.ptr + i * NPX * 3, mbuf.ptr + i * NPX, Es[i])
+        s2w, c = semtsdf.orbit_camera(list(p.Kinv), 0.01 * k, mean_m)
+        vol.raycast_dev(s2w, c, L.RENDER_LABEL, out.ptr)
+
+    elapsed, tm, tc = timed_integrate(vol, step, K, warmup)
+    res = {
+        "workload": "C4 on one GPU: 1024^3 semantic TSDF (144 GiB), integrate + 1 label raycast view per step",
+        "value": round(1024 ** 3 * K / elapsed / 1e6, 2), "unit": "Mvoxel-updates/s",
+        "ms_per_step": round(elapsed * 1e3 / K, 4),
+        "integrate_kernel_ms": round(tm.integrate_ms / max(tm.n_integrate, 1), 4),
+        "prep_ms": round(tm.prep_ms / max(tm.n_prep, 1), 4),
+        "render_ms_per_view": round(tm.render_ms / max(tm.n_render, 1), 4),
+        "touched_per_frame": int(tc.touched / K),
+        "device_gib": round(vol.state().device_bytes / 2 ** 30, 1),
+    }
+    out.free()
+    for b in (dbuf, rbuf, mbuf):
+        b.free()
+    vol.close()
+    return res
+
+
+def run_c4_dist(semtsdf, L, rank, world, local, pg, frames, f0, K, warmup, chunk):
+    """C4 strong scaling: rank r integrates shard r of the 1024^3 volume and every step
+    composites one label raycast view across the shards (DistShardGroup, RCCL all-reduce
+    MIN between protocol steps)."""
+    import torch
+
+    from semtsdf.shard import DistShardGroup
+
+    p = c4_params(semtsdf, L, f0, world, rank, chunk)
+    vol = semtsdf.Volume(p, local)
+    grp = DistShardGroup(vol, exchange=os.environ.get("BENCH_C4_EXCHANGE", "min"))
+    dbuf, rbuf, mbuf = resident_frames(frames, ids=True)
+    Es = [(fr.w2c @ f0.c2w).astype(np.float32) for fr in frames]
+    mean_m = float(np.mean(f0.depth[f0.depth > 0]) / 5000.0)
+    out = torch.empty(NPX * 3, dtype=torch.uint8, device=torch.device("cuda", local))
+    torch.cuda.synchronize()
+
+    def step(k):
+        i = k % len(frames)
+        vol.integrate_dev(dbuf.ptr + i * NPX * 2, rbuf.ptr + i * NPX * 3, mbuf.ptr + i * NPX, Es[i])
+        s2w, c = semtsdf.orbit_camera(list(p.Kinv), 0.01 * k, mean_m)
+        grp.raycast_dev(s2w, c, L.RENDER_LABEL, out.data_ptr())
+
+    elapsed, tm, tc = timed_integrate(vol, step, K, warmup, pg, local)
+    t_max = max_over_ranks(pg, local, elapsed)
+    kern = tm.integrate_ms / max(tm.n_integrate, 1)
+    prep = tm.prep_ms / max(tm.n_prep, 1)
+    res = {
+        "elapsed": t_max,
+        "integrate_kernel_ms_max": max_over_ranks(pg, local, kern),
+        "prep_ms_max": max_over_ranks(pg, local, prep),
+        "composite_ms_per_view": (tm.render_ms / max(tm.n_render, 1)),
+        "touched_per_frame": sum_over_ranks(pg, local, tc.touched / K),
+        "local_planes": int(vol.state().local_dim[2]),
+        "device_gib": round(vol.state().device_bytes / 2 ** 30, 1),
+    }
+    for b in (dbuf, rbuf, mbuf):
+        b.free()
+    vol.close()
+    return res
+
+
+# ----------------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -187,49 +524,69 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--dim", type=int, default=512)
     ap.add_argument("--frames", type=int, default=16, help="distinct synthetic frames cycled through")
-    ap.add_argument("--z-chunk", type=int, default=63)  # 63 + 1 halo plane = 4 half-tile units per chunk
+    ap.add_argument("--c4-chunk", type=int, default=64, help="Z-slab chunk of the C4 shards (planes)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-pipeline", action="store_true")
-    ap.add_argument("--no-cull", action="store_true", help="debug: disable brick culling")
+    ap.add_argument("--no-pipeline", action="store_true", help="skip pipeline, orbit, C2 and C4-single")
+    ap.add_argument("--no-c4", action="store_true", help="skip the 1024^3 single-GPU C4 measurement")
+    ap.add_argument("--no-cull", action="store_true", help="debug: disable unit culling")
     ap.add_argument("--cpu-planes", type=int, default=64)
     ap.add_argument("--cpu-slabs", type=int, default=10)
     ap.add_argument("--cpu-workers", type=int, default=0, help="N-core CPU baseline workers (0 = host cores)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
-                    help="per-launch HBM bytes of the integrate kernel from rocprofv3 PMC (see profiles/)")
+                    help="per-launch HBM bytes of the integrate kernel from rocprofv3 PMC (tools/traffic.py)")
     args = ap.parse_args()
 
     rank, world, local, pg = dist_setup(args.gpus)
-    # probe: one rank's shard of an N-way volume in a single process (per-rank cost of the
-    # N-GPU weak-scaling run, measurable on one GPU); not a scaling result
+    # probe: one rank's shard of an N-way C4 volume in a single process (per-rank integrate
+    # cost, measurable on one GPU); not a scaling result
     emu_world = int(os.environ.get("BENCH_EMULATE_WORLD", "0"))
     emu_rank = int(os.environ.get("BENCH_EMULATE_RANK", "0"))
-    shard_world, shard_rank = (emu_world, emu_rank) if (emu_world > 1 and world == 1) else (world, rank)
     import semtsdf
     from semtsdf import _lib as L
     from semtsdf.synth import SyntheticStream
-    from semtsdf.volume import DeviceBuffer
 
     semtsdf.load()
-    D = args.dim
-    W, H = 640, 480
     t_gen = time.perf_counter()
     stream = SyntheticStream(seed=1, noise=True)
     f0 = stream.frame(0)
     frames = [stream.frame(k) for k in range(1, args.frames + 1)]
     log(f"[bench rank {rank}] generated {len(frames) + 1} frames in {time.perf_counter() - t_gen:.1f}s")
 
-    p = semtsdf.default_params(D, KI, W, H)
-    p.dim[2] = D * shard_world
-    semtsdf.place_from_frame(p, f0.depth, float(np.mean(f0.depth[f0.depth > 0])) / 5000.0, L.PLACE_SFM)
+    if world > 1:
+        r = run_c4_dist(semtsdf, L, rank, world, local, pg, frames, f0, args.steps, args.warmup, args.c4_chunk)
+        if rank == 0:
+            value = 1024 ** 3 * args.steps / r["elapsed"] / 1e6
+            rec = {
+                "metric": METRIC, "value": round(value, 2), "unit": "Mvoxel-updates/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(r["elapsed"] * 1e3 / args.steps, 4),
+                "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+                "data": "synthetic",
+                "config": {"workload": "C4: 1024^3 semantic TSDF (sdf f32, weight i32, colour u8x3, 32-bin u32 "
+                                       "histogram) Z-slab sharded over the ranks (interleaved chunks), per step "
+                                       "integrate + one label raycast view composited across the shards (RCCL "
+                                       "all-reduce MIN between protocol steps); speed-up = value / the N=1 line's "
+                                       "c4_single_gpu.value",
+                           "volume": [1024, 1024, 1024], "z_chunk": args.c4_chunk, "frames_cycled": len(frames),
+                           "parallelism": f"zslab{world}"},
+                "integrate_kernel_ms_max_rank": round(r["integrate_kernel_ms_max"], 4),
+                "prep_ms_max_rank": round(r["prep_ms_max"], 4),
+                "composite_ms_per_view_rank0": round(r["composite_ms_per_view"], 4),
+                "touched_per_frame": int(r["touched_per_frame"]),
+                "local_planes_rank0": r["local_planes"], "device_gib_rank0": r["device_gib"],
+            }
+            print(json.dumps(rec), flush=True)
+        pg.destroy_process_group()
+        return
+
+    D = args.dim
+    p = place(semtsdf, L, D, f0)
     p.flags = L.F_SEMANTIC | L.F_GATE_COLOR | (L.F_NO_CULL if args.no_cull else 0)
-    if shard_world > 1:
-        p.z_nshards = shard_world
-        p.z_shard = shard_rank
-        p.z_chunk = args.z_chunk
+    if emu_world > 1:
+        p = c4_params(semtsdf, L, f0, emu_world, emu_rank, args.c4_chunk)
     # CPU baseline first: the forked N-core workers then start from a process that has not
     # touched the GPU yet.
     cpu = cpu_n = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if emu_world <= 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(frames, p, f0, args.cpu_planes, args.cpu_slabs, 1)
         nw = args.cpu_workers or host_cores()
         if nw > 1:
@@ -239,179 +596,89 @@ def main():
 
     vol = semtsdf.Volume(p, local)
     st0 = vol.state()
-    voxels_per_rank = D * D * D  # owned voxels (halo planes are integrated redundantly, not counted)
-    log(f"[bench rank {rank}] volume {list(p.dim)} local {list(st0.local_dim)} "
-        f"device bytes {st0.device_bytes / 2**30:.2f} GiB")
-
-    # frames resident in HBM
-    npx = W * H
-    dbuf = DeviceBuffer(len(frames) * npx * 2)
-    rbuf = DeviceBuffer(len(frames) * npx * 3)
-    mbuf = DeviceBuffer(len(frames) * npx)
-    Es = []
-    for i, fr in enumerate(frames):
-        dbuf.upload(fr.depth, None, i * npx * 2)
-        rbuf.upload(fr.rgb, None, i * npx * 3)
-        mbuf.upload(fr.gt_ids, None, i * npx)  # globally consistent ids: integrate-only step
-        Es.append((fr.w2c @ f0.c2w).astype(np.float32))
+    log(f"[bench] volume {list(p.dim)} local {list(st0.local_dim)} device bytes {st0.device_bytes / 2**30:.2f} GiB")
+    dbuf, rbuf, mbuf = resident_frames(frames, ids=True)  # globally consistent ids: integrate-only step
+    Es = [(fr.w2c @ f0.c2w).astype(np.float32) for fr in frames]
     vol.sync()
 
     def step(k):
         i = k % len(frames)
-        vol.integrate_dev(dbuf.ptr + i * npx * 2, rbuf.ptr + i * npx * 3, mbuf.ptr + i * npx, Es[i])
+        vol.integrate_dev(dbuf.ptr + i * NPX * 2, rbuf.ptr + i * NPX * 3, mbuf.ptr + i * NPX, Es[i])
 
-    for k in range(args.warmup):
-        step(k)
-    vol.sync()
-    # timed region: the K steps alone (no timing events on the stream)
-    barrier(pg, local)
-    vol.sync()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(args.warmup + k)
-    vol.sync()
-    barrier(pg, local)
-    t1 = time.perf_counter()
-    elapsed = max_over_ranks(pg, local, t1 - t0)
-
-    # kernel-level timing of the same K steps: HIP events on the volume's stream around the
-    # prepass (pyramid + cull) and around the integrate kernel
-    vol.reset_timing()
-    vol.set_instrumentation(events=True, count=False)
-    for k in range(args.steps):
-        step(args.warmup + k)
-    vol.sync()
-    tm = vol.timing()
-    vol.set_instrumentation(events=False, count=False)
+    elapsed, tm, tc = timed_integrate(vol, step, args.steps, args.warmup)
     kern_ms = tm.integrate_ms / max(tm.n_integrate, 1)
     prep_ms = tm.prep_ms / max(tm.n_prep, 1)
-
-    # algorithmic bytes of the same launches (counts are a function of the frame only)
-    vol.reset_timing()
-    vol.set_instrumentation(events=False, count=True)
-    for k in range(args.steps):
-        step(args.warmup + k)
-    tc = vol.timing()
-    vol.set_instrumentation(events=False, count=False)
     touched = tc.touched / args.steps
     gated = tc.gated / args.steps
-    bricks = tc.bricks / args.steps
-    free_units = tc.free_units / args.steps
-    bytes_per_launch = 16.0 * touched + 14.0 * gated + 6.0 * npx
+    bytes_per_launch = 16.0 * touched + 14.0 * gated + 6.0 * NPX
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-
-    total_vox = sum_over_ranks(pg, local, float(voxels_per_rank) * args.steps)
-    value = total_vox / elapsed / 1e6
-
-    traffic = None
-    if os.path.exists(args.traffic_json):
-        try:
-            with open(args.traffic_json) as f:
-                tj = json.load(f)
-            if tj.get("dim") == D and tj.get("n_gpus", 1) == world:
-                traffic = tj.get("bytes_per_launch")
-        except Exception:
-            traffic = None
-
-    pipeline = None
-    if world == 1 and not args.no_pipeline:
-        # full per-frame pipeline (SfM launch_kernel order): association raycast + relabel on
-        # device, then integrate; per-frame instance labels permuted as Mask R-CNN would emit.
-        vol.reset()
-        # per-frame detection masks resident in HBM like the depth/RGB frames (a detector
-        # on the same GPU hands over device masks); each frame copies its mask into the
-        # work buffer the association relabels in place
-        dmask = DeviceBuffer(len(frames) * npx)
-        for i, fr in enumerate(frames):
-            dmask.upload(fr.mask, vol.stream, i * npx)
-        mwork = DeviceBuffer(npx)
-        n_pipe = max(args.steps, 2 * len(frames))
-        vol.parse_frame_dev(dbuf.ptr, rbuf.ptr, mbuf.ptr, Es[0])  # first integrated frame
-        for i in range(1, 3):
-            mwork.copy_from(dmask.ptr + i * npx, npx, vol.stream)
-            vol.parse_frame_dev(dbuf.ptr + i * npx * 2, rbuf.ptr + i * npx * 3, mwork.ptr, Es[i])
-        vol.sync()
-        vol.reset_timing()
-        vol.set_instrumentation(events=True, count=False)
-        tp0 = time.perf_counter()
-        for k in range(n_pipe):
-            i = (3 + k) % len(frames)
-            mwork.copy_from(dmask.ptr + i * npx, npx, vol.stream)  # 307 KB per-frame mask
-            vol.parse_frame_dev(dbuf.ptr + i * npx * 2, rbuf.ptr + i * npx * 3, mwork.ptr, Es[i])
-        vol.sync()
-        tp1 = time.perf_counter()
-        tp = vol.timing()
-        s2w, c = semtsdf.orbit_camera(list(p.Kinv), 0.3, float(np.mean(f0.depth[f0.depth > 0]) / 5000.0))
-        obuf = DeviceBuffer(npx * 3)
-        vol.reset_timing()
-        for _ in range(5):
-            vol.raycast_dev(s2w, c, L.RENDER_LABEL, obuf.ptr)
-        tr = vol.timing()
-        st = vol.state()
-        pipeline = {
-            "frames_per_s": n_pipe / (tp1 - tp0),
-            "ms_per_frame": (tp1 - tp0) * 1e3 / n_pipe,
-            "assoc_ms_per_frame": tp.assoc_ms / max(tp.n_assoc, 1),
-            "integrate_ms_per_frame": tp.integrate_ms / max(tp.n_integrate, 1),
-            "render_ms_per_view": tr.render_ms / max(tr.n_render, 1),
-            "num_objs": int(st.num_objs),
-        }
-        obuf.free()
-        mwork.free()
-        dmask.free()
-
-    copy_bw = None
-    if rank == 0 and not args.no_pipeline:
-        copy_bw = copy_bandwidth(local)
-
-    if rank == 0:
-        rec = {
-            "metric": METRIC,
-            "value": round(value, 2),
-            "unit": "Mvoxel-updates/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic",
-            "config": {
-                "workload": "C3: 512^3 semantic TSDF integrate (sdf f32, weight i32, colour u8x3, 32-bin u32 "
-                            "instance histogram), synthetic 640x480 depth+RGB+mask stream (seed 1, noise on), "
-                            "frames resident in HBM; N>1: interleaved Z-slab shards of 512x512x(512N)",
-                "volume": list(p.dim),
-                "z_chunk": int(p.z_chunk) if world > 1 else None,
-                "frames_cycled": len(frames),
-            },
-            "frames_per_s": round(args.steps / elapsed, 2),
-            "integrate_kernel_ms": round(kern_ms, 4),
-            "prep_ms": round(prep_ms, 4),
-            "touched_per_frame": int(touched),
-            "gated_per_frame": int(gated),
-            "live_units_per_frame": int(bricks),
-            "free_units_per_frame": int(free_units),
-            "touched_mvox_per_s": round(touched / (kern_ms * 1e-3) / 1e6, 1),
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "algorithmic_bytes_per_launch": int(bytes_per_launch),
-            },
-            "cpu_baseline": cpu,
-            "cpu_baseline_ncores": cpu_n,
-            "hbm_copy_gbs": round(copy_bw, 1) if copy_bw else None,
-            "pipeline": pipeline,
-        }
-        print(json.dumps(rec), flush=True)
+    voxels = int(p.dim[0]) * int(p.dim[1]) * int(p.dim[2]) if emu_world <= 1 else (1024 ** 3) // emu_world
+    value = voxels * args.steps / elapsed / 1e6
+    traffic, traffic_src = read_traffic(args.traffic_json, D, 1)
+    live_units = tc.bricks / args.steps
+    free_units = tc.free_units / args.steps
     vol.close()
-    if pg is not None:
-        pg.destroy_process_group()
+    for b in (dbuf, rbuf, mbuf):
+        b.free()
+
+    pipeline = orbit = c2 = c4 = None
+    if not args.no_pipeline and emu_world <= 1:
+        pipeline, orbit = run_pipeline(semtsdf, L, p, local)
+        c2 = run_c2(semtsdf, L, local, frames, f0, args.steps, args.warmup)
+        if not args.no_c4:
+            c4 = run_c4_single(semtsdf, L, local, frames, f0, max(10, args.steps // 3), args.warmup)
+    copy_bw = copy_bandwidth(local) if not args.no_pipeline else None
+
+    rec = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "Mvoxel-updates/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {
+            "workload": "C3: 512^3 semantic TSDF integrate (sdf f32, weight i32, colour u8x3, 32-bin u32 instance "
+                        "histogram), synthetic 640x480 depth+RGB+mask stream (seed 1, noise on), frames resident in "
+                        "HBM" if emu_world <= 1 else
+                        f"probe: shard {emu_rank} of the {emu_world}-way C4 volume (integrate only)",
+            "volume": list(p.dim),
+            "frames_cycled": len(frames),
+        },
+        "frames_per_s": pipeline["frames_per_s"] if pipeline else None,
+        "integrate_frames_per_s": round(args.steps / elapsed, 2),
+        "integrate_kernel_ms": round(kern_ms, 4),
+        "prep_ms": round(prep_ms, 4),
+        "touched_per_frame": int(touched),
+        "gated_per_frame": int(gated),
+        "live_units_per_frame": int(live_units),
+        "free_units_per_frame": int(free_units),
+        "touched_mvox_per_s": round(touched / (kern_ms * 1e-3) / 1e6, 1),
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "algorithmic_bytes_per_launch": int(bytes_per_launch),
+            "bytes_rule": "16 N_touch + 14 N_gate + 6 W H (SURVEY §8d, the reference's storage types)",
+        },
+        "cpu_baseline": cpu,
+        "cpu_baseline_ncores": cpu_n,
+        "hbm_copy_gbs": round(copy_bw, 1) if copy_bw else None,
+        "pipeline": pipeline,
+        "orbit": orbit,
+        "c2": c2,
+        "c4_single_gpu": c4,
+    }
+    print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":

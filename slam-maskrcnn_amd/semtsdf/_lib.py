@@ -170,11 +170,27 @@ _lib = None
 _load_error = None
 
 
+def _bind_torch_runtime():
+    """PyTorch-ROCm ships its own copy of the HIP runtime (torch/lib/libamdhip64.so, same
+    SONAME as /opt/rocm's) and loads it by path.  Two HIP runtimes in one process do not
+    work: the second one to initialise finds no device.  Importing torch (no GPU call)
+    before the library makes the library's libamdhip64.so.7 dependency resolve to torch's
+    copy, so a process that also uses torch (torch.distributed shard groups, the bench's
+    pinned buffers and streams) has a single runtime.  SEMTSDF_NO_TORCH=1 skips it."""
+    if os.environ.get("SEMTSDF_NO_TORCH") == "1":
+        return
+    try:
+        import torch  # noqa: F401
+    except Exception:  # torch absent: the library uses the system ROCm runtime alone
+        pass
+
+
 def load(path: str | None = None):
     """Load libsemtsdf.so once.  Raises SemTSDFError (loudly) if it is missing."""
     global _lib, _load_error
     if _lib is not None:
         return _lib
+    _bind_torch_runtime()
     p = path or os.environ.get("SEMTSDF_LIB", LIB_PATH)
     if not os.path.exists(p):
         raise SemTSDFError(ERR_STATE, f"HIP library not built: {p} (run __graft_entry__.build())")
