@@ -386,6 +386,128 @@ def run_pipeline(semtsdf, L, p, local, n_frames=100, n_warm=5):
     }
 
 
+# ----------------------------------------------------------------------------- mask producer
+def detector_masks(mask):
+    """Detector-format masks[H, W, N] for a frame: one detection per instance of the frame's
+    label mask, one large box overlapping them (its shared pixels go to the smaller
+    detections, dmask.py:21-32) and one tiny detection (dropped, dmask.py:42)."""
+    ids = [int(i) for i in np.unique(mask) if i]
+    ms = [mask == i for i in ids]
+    box = np.zeros((H, W), bool)
+    box[H // 4:3 * H // 4, W // 4:3 * W // 4] = True
+    tiny = np.zeros((H, W), bool)
+    tiny[:20, :20] = True
+    return np.stack(ms + [box, tiny], axis=2).astype(np.uint8)
+
+
+def run_mask_overlap(semtsdf, L, p, local, frames, f0, n_frames=48, n_warm=4, gemm=4096, n_gemm=2):
+    """§8f rank 1 harness: a detector stand-in (n_gemm bf16 GEMMs of gemm^3, then its
+    masks[H, W, N] landing in HBM) and semtsdf_masks_to_labels on a producer stream feed
+    parse_frame_dev (association + relabel + integrate) on the volume's stream.  "serial":
+    producer and fusion in one stream order; "overlapped": the producer of frame k+1 runs
+    on its own stream while frame k fuses (2 label slots, events both ways)."""
+    import torch
+
+    from semtsdf.masks import masks_to_labels_dev
+
+    dev = torch.device("cuda", local)
+    F = len(frames)
+    dets = [detector_masks(fr.mask) for fr in frames]
+    N = max(m.shape[2] for m in dets)
+    det = torch.zeros((F, NPX * N), dtype=torch.uint8, device=dev)
+    for i, m in enumerate(dets):
+        mm = np.zeros((H, W, N), np.uint8)
+        mm[:, :, :m.shape[2]] = m
+        det[i].copy_(torch.from_numpy(mm.reshape(-1)))
+    out_det = torch.empty(NPX * N, dtype=torch.uint8, device=dev)
+    ga = torch.randn((gemm, gemm), dtype=torch.bfloat16, device=dev)
+    gb = torch.randn((gemm, gemm), dtype=torch.bfloat16, device=dev)
+    gc = torch.empty((gemm, gemm), dtype=torch.bfloat16, device=dev)
+    labels = torch.empty((2, NPX), dtype=torch.uint8, device=dev)
+    dbuf, rbuf, _ = resident_frames(frames, with_mask=False)
+    Es = [(fr.w2c @ f0.c2w).astype(np.float32) for fr in frames]
+    pstream = torch.cuda.Stream(device=dev)
+
+    def run(mode):
+        vol = semtsdf.Volume(p, local)
+        vstream = torch.cuda.ExternalStream(vol.stream, device=dev)
+        ready = [torch.cuda.Event() for _ in range(2)]
+        used = [torch.cuda.Event() for _ in range(2)]
+        ps = vstream if mode == "serial" else pstream
+
+        def produce(k):
+            s = k % 2
+            with torch.cuda.stream(ps):
+                ps.wait_event(used[s])
+                for _ in range(n_gemm):
+                    torch.matmul(ga, gb, out=gc)
+                out_det.copy_(det[k % F])
+                masks_to_labels_dev(out_det.data_ptr(), W, H, N, labels[s].data_ptr(), stream=ps.cuda_stream)
+                ready[s].record(ps)
+
+        def fuse(k):
+            s, i = k % 2, k % F
+            vstream.wait_event(ready[s])
+            vol.parse_frame_dev(dbuf.ptr + i * NPX * 2, rbuf.ptr + i * NPX * 3, labels[s].data_ptr(), Es[i])
+            used[s].record(vstream)
+
+        def frames_(k0, k1):
+            if mode == "serial":
+                for k in range(k0, k1):
+                    produce(k)
+                    fuse(k)
+            else:
+                produce(k0)
+                for k in range(k0, k1):
+                    if k + 1 < k1:
+                        produce(k + 1)
+                    fuse(k)
+
+        frames_(0, n_warm)
+        vol.sync()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        frames_(n_warm, n_warm + n_frames)
+        vol.sync()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        objs = int(vol.state().num_objs)
+        vol.close()
+        return dt, objs
+
+    def producer_only(with_gemm):
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(pstream):
+            ev0.record(pstream)
+            for k in range(n_frames):
+                if with_gemm:
+                    for _ in range(n_gemm):
+                        torch.matmul(ga, gb, out=gc)
+                out_det.copy_(det[k % F])
+                masks_to_labels_dev(out_det.data_ptr(), W, H, N, labels[k % 2].data_ptr(), stream=pstream.cuda_stream)
+            ev1.record(pstream)
+        ev1.synchronize()
+        return ev0.elapsed_time(ev1) / n_frames
+
+    producer_only(True)
+    t_ser, objs_ser = run("serial")
+    t_ovl, objs_ovl = run("overlapped")
+    prod_ms = producer_only(True)
+    labels_ms = producer_only(False)
+    for b in (dbuf, rbuf):
+        b.free()
+    return {
+        "serial_frames_per_s": round(n_frames / t_ser, 2),
+        "overlapped_frames_per_s": round(n_frames / t_ovl, 2),
+        "producer_ms_per_frame": round(prod_ms, 4),
+        "masks_copy_and_labels_ms_per_frame": round(labels_ms, 4),
+        "detections_per_frame": N, "frames": n_frames,
+        "num_objs_serial": objs_ser, "num_objs_overlapped": objs_ovl,
+        "producer": f"stand-in detector: {n_gemm} bf16 GEMMs {gemm}^3 + masks[H,W,{N}] written to HBM + "
+                    "semtsdf_masks_to_labels (dmask.py:47-59 rule)",
+    }
+
+
 # ----------------------------------------------------------------------------- C2
 def run_c2(semtsdf, L, local, frames, f0, K=30, warmup=3):
     """C2: 256^3 TSDF + colour (NumPy rule: int32 colour, no gate), synthetic stream."""
@@ -423,6 +545,7 @@ def run_c2(semtsdf, L, local, frames, f0, K=30, warmup=3):
         "integrate_kernel_ms": round(kern_ms, 4),
         "frames_per_s_upload_integrate": round(K / t_up, 1),
         "touched_per_frame": int(touched),
+        "live_units_per_frame": int(tc.bricks / K),
         "roofline": {"bound": "hbm", "achieved": round(b / (kern_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(b / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                      "algorithmic_bytes_per_launch": int(b), "bytes_rule": "22 N_touch + 5 W H (SURVEY §8d)"},
@@ -529,6 +652,8 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true", help="skip pipeline, orbit, C2 and C4-single")
     ap.add_argument("--no-c4", action="store_true", help="skip the 1024^3 single-GPU C4 measurement")
     ap.add_argument("--no-cull", action="store_true", help="debug: disable unit culling")
+    ap.add_argument("--only", choices=["pipeline", "masks", "c2", "c4"], default=None,
+                    help="debug: run one section alone and print its record")
     ap.add_argument("--cpu-planes", type=int, default=64)
     ap.add_argument("--cpu-slabs", type=int, default=10)
     ap.add_argument("--cpu-workers", type=int, default=0, help="N-core CPU baseline workers (0 = host cores)")
@@ -581,6 +706,17 @@ def main():
     D = args.dim
     p = place(semtsdf, L, D, f0)
     p.flags = L.F_SEMANTIC | L.F_GATE_COLOR | (L.F_NO_CULL if args.no_cull else 0)
+    if args.only:
+        if args.only == "pipeline":
+            r = dict(zip(("pipeline", "orbit"), run_pipeline(semtsdf, L, p, local)))
+        elif args.only == "masks":
+            r = run_mask_overlap(semtsdf, L, p, local, frames, f0)
+        elif args.only == "c2":
+            r = run_c2(semtsdf, L, local, frames, f0, args.steps, args.warmup)
+        else:
+            r = run_c4_single(semtsdf, L, local, frames, f0, max(10, args.steps // 3), args.warmup)
+        print(json.dumps({"only": args.only, args.only: r}), flush=True)
+        return
     if emu_world > 1:
         p = c4_params(semtsdf, L, f0, emu_world, emu_rank, args.c4_chunk)
     # CPU baseline first: the forked N-core workers then start from a process that has not
@@ -621,10 +757,11 @@ def main():
     for b in (dbuf, rbuf, mbuf):
         b.free()
 
-    pipeline = orbit = c2 = c4 = None
+    pipeline = orbit = c2 = c4 = masks = None
     if not args.no_pipeline and emu_world <= 1:
         pipeline, orbit = run_pipeline(semtsdf, L, p, local)
-        c2 = run_c2(semtsdf, L, local, frames, f0, args.steps, args.warmup)
+        masks = run_mask_overlap(semtsdf, L, p, local, frames, f0)
+        c2 =run_c2(semtsdf, L, local, frames, f0, args.steps, args.warmup)
         if not args.no_c4:
             c4 = run_c4_single(semtsdf, L, local, frames, f0, max(10, args.steps // 3), args.warmup)
     copy_bw = copy_bandwidth(local) if not args.no_pipeline else None
@@ -675,6 +812,7 @@ def main():
         "hbm_copy_gbs": round(copy_bw, 1) if copy_bw else None,
         "pipeline": pipeline,
         "orbit": orbit,
+        "mask_producer": masks,
         "c2": c2,
         "c4_single_gpu": c4,
     }

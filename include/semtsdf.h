@@ -220,6 +220,18 @@ int semtsdf_min_i64(int64_t* dst_d, const int64_t* src_d, size_t n, void* stream
  * n_obs > 0), then integrate_dev, then note_integrated (n_obs++, first-frame object count). */
 int semtsdf_shard_note_integrated(semtsdf_vol* v, const uint8_t* mask_d, void* stream);
 
+/* ---- mask producer contract --------------------------------------
+ * Detector output -> the u8 instance-label mask the fusion consumes, as Mask_RCNN/dmask.py's
+ * mask_detect (dmask.py:47-59, without the optional depth filter that mask_process.py does
+ * not use): detection i is kept when its area > min_area (filter_tiny_objects, 2000 in the
+ * reference), a pixel belongs to the smallest kept detection containing it (preserve_small_objs;
+ * equal areas: the lower index), labelled 1 + its index among the kept ones.
+ * masks_d: bytes [height][width][n] (nonzero = inside; the detector's masks[H, W, N]),
+ * labels_d: u8 [height * width]; 0 <= n <= 256; device pointers, async on stream.
+ * n_kept (optional, host) receives the number of kept detections (synchronises). */
+int semtsdf_masks_to_labels(const uint8_t* masks_d, int width, int height, int n, int min_area,
+                            uint8_t* labels_d, int* n_kept, void* stream);
+
 /* Achievable HBM bandwidth on `device` (GB/s, read + write bytes) of a float4 device copy
  * of `bytes` bytes, best of `reps` runs: the practical ceiling beside the 8 TB/s spec peak. */
 int semtsdf_copy_bandwidth(int device, size_t bytes, int reps, double* gbs);

@@ -306,3 +306,28 @@ def numpy_integrate(sdf, wt, color, vol_dim, vol_start, voxel, mu, K, E, depth, 
         np.add.at(h, (sel, lab[sel]), 1)
     s_wt[ok] += 1
     return int(ok.sum()), int(gated.sum())
+
+
+# ------------------------------------------------------------------------------------
+# NumPy restatement of Mask_RCNN/dmask.py:21-59 (mask_detect, depth_image=None as
+# mask_process.py:100 calls it)
+# ------------------------------------------------------------------------------------
+def masks_to_labels(masks, min_area=2000):
+    """masks bool [H, W, N] -> (labels u8 [H, W], kept).  filter_tiny_objects (:34-45) keeps
+    detections with area > min_area; preserve_small_objs (:21-32) leaves each pixel to the
+    first detection in ascending-area order that covers it (the sequential removal reduces
+    to that); :56-58 writes 1 + index among the kept.  Equal areas: the stable order (lower
+    index first) -- dmask.py's np.argsort (quicksort) leaves that order unspecified."""
+    m = np.asarray(masks).astype(bool)
+    H, W, n = m.shape
+    areas = m.sum(axis=(0, 1))
+    kept = np.nonzero(areas > min_area)[0]
+    out = np.zeros((H, W), np.uint8)
+    if kept.size == 0:
+        return out, 0
+    order = np.argsort(areas[kept], kind="stable")
+    mk = m[:, :, kept[order]]
+    any_ = mk.any(axis=2)
+    first = mk.argmax(axis=2)
+    out[any_] = (order[first[any_]] + 1).astype(np.uint8)
+    return out, int(kept.size)

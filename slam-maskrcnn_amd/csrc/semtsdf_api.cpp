@@ -619,7 +619,11 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     const size_t n = g.nvox;
     const size_t px = (size_t)p->width * p->height;
     auto bail = [&](int code) { free_all(v); delete v; return code; };
-    if (hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking) != hipSuccess)
+    // the fusion stream takes the device's greatest priority: the per-frame kernels are the
+    // latency-critical consumer of a frame, the detector feeding it is throughput work
+    int prio_least = 0, prio_greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_greatest = 0;
+    if (hipStreamCreateWithPriority(&v->stream, hipStreamNonBlocking, prio_greatest) != hipSuccess)
         return bail(fail(SEMTSDF_ERR_HIP, "hipStreamCreate failed"));
     const bool ci32 = p->flags & SEMTSDF_F_COLOR_I32;
     if ((rc = dev_alloc(v, (void**)&v->b.sdf, n * 4))) return bail(rc);
@@ -1070,6 +1074,29 @@ int semtsdf_shard_note_integrated(semtsdf_vol* v, const uint8_t* mask_d, void* s
         HIPC(launch_first_frame_objs(v->tables_d, v->num_objs_d, s));
     }
     v->n_obs++;
+    return SEMTSDF_OK;
+}
+
+int semtsdf_masks_to_labels(const uint8_t* masks_d, int width, int height, int n, int min_area, uint8_t* labels_d,
+                            int* n_kept, void* stream) {
+    if (!masks_d && n > 0) return fail(SEMTSDF_ERR_INVALID, "masks is NULL");
+    if (!labels_d) return fail(SEMTSDF_ERR_INVALID, "labels is NULL");
+    if (width <= 0 || height <= 0 || (int64_t)width * height > (1 << 28)) return fail(SEMTSDF_ERR_INVALID, "bad size");
+    if (n < 0 || n > kMaxDetections) return fail(SEMTSDF_ERR_INVALID, "n=%d detections outside [0, %d]", n, kMaxDetections);
+    hipStream_t s = (hipStream_t)stream;
+    void* scratch = nullptr;
+    HIPC(hipMallocAsync(&scratch, mask_scratch_bytes(), s));
+    hipError_t e = launch_masks_to_labels(masks_d, width * height, n, min_area, scratch, labels_d, s);
+    if (e == hipSuccess && n_kept) {
+        unsigned k = 0;
+        e = hipMemcpyAsync(&k, (char*)scratch + mask_scratch_kept_offset(), sizeof(unsigned), hipMemcpyDeviceToHost,
+                           s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        *n_kept = (int)k;
+    }
+    const hipError_t ef = hipFreeAsync(scratch, s);
+    if (e != hipSuccess) return fail(SEMTSDF_ERR_HIP, "masks_to_labels: %s", hipGetErrorString(e));
+    HIPC(ef);
     return SEMTSDF_OK;
 }
 

@@ -8,6 +8,7 @@
 namespace semtsdf {
 
 constexpr int kMaxObjects = 32;
+constexpr int kMaxDetections = 256;  // detections per frame accepted by semtsdf_masks_to_labels
 constexpr int kRcpTable = 1024;  // RN(1/n) table of the running means (w + 1 <= kRcpTable)
 constexpr int kZAlign = 32;      // stored z planes per x,y column: a multiple of the unit z-extent
 #ifndef SEMTSDF_BRICK_DIST_CAP
@@ -221,6 +222,11 @@ hipError_t launch_shard_assoc_partial(const ShardRayArgs& a, hipStream_t s);
 hipError_t launch_tables_from_partial(const long long* reduced, AssocTables* t, hipStream_t s);
 hipError_t launch_copy_f4(const void* src, void* dst, size_t n16, hipStream_t s);
 hipError_t launch_min_i64(long long* dst, const long long* src, size_t n, hipStream_t s);
+// detector masks [npx][n] (bytes) -> u8 labels (dmask.py:34-59); scratch of mask_scratch_bytes()
+hipError_t launch_masks_to_labels(const uint8_t* masks, int npx, int n, int min_area, void* scratch, uint8_t* out,
+                                  hipStream_t s);
+size_t mask_scratch_bytes();
+size_t mask_scratch_kept_offset();
 hipError_t launch_brick_min(const VolGeom& g, const VolBufs& b, bool all, hipStream_t s);
 hipError_t launch_fill_volume(const VolGeom& g, const VolBufs& b, uint32_t flags, hipStream_t s);
 hipError_t launch_depth_pyramid(const uint16_t* depth, const uint8_t* rgb, const uint8_t* mask, int w, int h,

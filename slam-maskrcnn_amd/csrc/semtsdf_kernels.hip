@@ -25,6 +25,7 @@
 #include <hip/hip_ext.h>
 #include <stdint.h>
 #include <limits.h>
+#include <stddef.h>
 #include <stdlib.h>
 #include "semtsdf_internal.h"
 
@@ -1054,25 +1055,26 @@ __device__ __forceinline__ void stage_compute(const IntegrateArgs& a, const floa
     for (int k = 0; k < 4; ++k) cross |= (so[k] < a.skip_thr) != (sn[k] < a.skip_thr);
     O.cross = cross;
     if (FREE) return;  // no colour, histogram or vote state
-    if (CI32) {  // unchanged lines of a stored row
+    if (CI32) {  // tsdf.cu:57-62 on i32 colour; unchanged voxels of a stored row pass through
+        // (element-wise selects: a select of whole int4 values is lowered through scratch)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) O.c32[k] = L.c32[k];
+        for (int k = 0; k < 4; ++k) {
+            const int4 o = L.c32[k];
+            const bool gk = (gmask >> k) & 1u;
+            const int wi = wo[k], dw = wo[k] + 1;
+            const int r0 = C.pix[k] & 0xFF, r1 = (C.pix[k] >> 8) & 0xFF, r2 = (C.pix[k] >> 16) & 0xFF;
+            int4 n;
+            n.x = gk ? avg_div(o.x * wi + r0, dw) : o.x;
+            n.y = gk ? avg_div(o.y * wi + r1, dw) : o.y;
+            n.z = gk ? avg_div(o.z * wi + r2, dw) : o.z;
+            n.w = o.w;
+            O.c32[k] = n;
+        }
     } else {
         O.c8 = L.c8;
     }
     if (gmask) {  // tsdf.cu:57-62
         if (CI32) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const bool gk = (gmask >> k) & 1u;
-                const int wi = wo[k];
-                const int r0 = C.pix[k] & 0xFF, r1 = (C.pix[k] >> 8) & 0xFF, r2 = (C.pix[k] >> 16) & 0xFF;
-                int4 n = L.c32[k];
-                n.x = avg_div(n.x * wi + r0, wi + 1);
-                n.y = avg_div(n.y * wi + r1, wi + 1);
-                n.z = avg_div(n.z * wi + r2, wi + 1);
-                O.c32[k] = gk ? n : L.c32[k];
-            }
         } else {
             const unsigned co[4] = {L.c8.x, L.c8.y, L.c8.z, L.c8.w};
             unsigned cw[4];
@@ -1298,7 +1300,7 @@ __device__ __forceinline__ unsigned integrate_list(const IntegrateArgs& a, const
 #define SEMTSDF_INTEGRATE_WPE 4  // waves per SIMD the register allocation targets (5 spills; measured equal)
 #endif
 template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT, bool SHARD, bool PIN>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_INTEGRATE_WPE))) void k_integrate(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : SEMTSDF_INTEGRATE_WPE))) void k_integrate(
     IntegrateArgs a, UnitGrid ug, unsigned seg_cap) {
     __shared__ float s_rcp[kRcpTable];
     for (int i = (int)threadIdx.x; i < kRcpTable; i += (int)blockDim.x) s_rcp[i] = a.rcp_table[i];
@@ -2154,11 +2156,13 @@ __device__ __forceinline__ void shade_hit(const VolGeom& g, const VolBufs& vb, c
         }
     } else {
         float cc[3];
+#pragma unroll
         for (int ch = 0; ch < 3; ++ch) {
             // colour is stored padded to 4 channels: [v*4 + ch]
             const uint64_t i000 = (uint64_t)tr.i000 * 4 + ch;
             const uint64_t sx = (uint64_t)tr.dx * 4, sy = (uint64_t)tr.dy * 4, sz = (uint64_t)tr.dz * 4;
             float d[8];
+#pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const uint64_t off = ((k & 4) ? sx : 0) + ((k & 2) ? sy : 0) + ((k & 1) ? sz : 0);
                 d[k] = color_i32 ? (float)reinterpret_cast<const int32_t*>(vb.color)[i000 + off]
@@ -2174,6 +2178,9 @@ __device__ __forceinline__ void shade_hit(const VolGeom& g, const VolBufs& vb, c
     }
 }
 
+// STATS: instrumentation build of the kernel (a run-time select of the stats pointer would
+// keep MarchStats in scratch memory)
+template <bool STATS>
 __global__ __launch_bounds__(256) void k_render(RenderArgs a) {
     const int x = blockIdx.x * 16 + (threadIdx.x & 15);
     const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
@@ -2184,8 +2191,8 @@ __global__ __launch_bounds__(256) void k_render(RenderArgs a) {
     uint8_t b = 0, gch = 0, r = 0;
     float th = -1.0f;
     MarchStats ms;
-    const uint64_t t_start = a.ray_stats ? __builtin_amdgcn_s_memrealtime() : 0;
-    if (march_ray(a.g, a.b, ox, oy, oz, dx, dy, dz, &t, a.ray_stats ? &ms : nullptr)) {
+    const uint64_t t_start = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
+    if (march_ray(a.g, a.b, ox, oy, oz, dx, dy, dz, &t, STATS ? &ms : nullptr)) {
         th = t;
         const Tri tr = tri_setup(a.g, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
         shade_hit(a.g, a.b, tr, a.mode, a.color_i32, a.palette, &b, &gch, &r);
@@ -2194,7 +2201,7 @@ __global__ __launch_bounds__(256) void k_render(RenderArgs a) {
     a.out_bgr[(size_t)px * 3 + 1] = gch;
     a.out_bgr[(size_t)px * 3 + 2] = r;
     if (a.out_t) a.out_t[px] = th;
-    if (a.ray_stats) {  // instrumentation
+    if (STATS) {  // instrumentation
         unsigned* q = a.ray_stats + (size_t)px * 4;
         q[0] = ms.iters; q[1] = ms.lookups; q[2] = ms.evals; q[3] = ms.skipped;
         const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
@@ -2209,7 +2216,11 @@ __global__ __launch_bounds__(256) void k_render(RenderArgs a) {
 }
 
 hipError_t launch_render(const RenderArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_render, dim3((a.width + 15) / 16, (a.height + 15) / 16), dim3(256), 0, s, a);
+    const dim3 grid((a.width + 15) / 16, (a.height + 15) / 16);
+    if (a.ray_stats)
+        hipLaunchKernelGGL(k_render<true>, grid, dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_render<false>, grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
@@ -2644,5 +2655,111 @@ hipError_t launch_color_chunk(const void* src, void* dst, bool to_ref, bool i32,
     }
     return hipGetLastError();
 }
+
+
+// ------------------------------------------------------------------------------------
+// Mask R-CNN detections -> instance-label mask (the fusion's mask input contract,
+// Mask_RCNN/dmask.py:34-59 mask_detect without its optional depth filter):
+//   filter_tiny_objects (dmask.py:34-45): keep detection i when its area > min_area;
+//   preserve_small_objs (dmask.py:21-32): over the kept detections sorted by area, each
+//     smaller one removes its pixels from every larger one, i.e. a pixel belongs to the
+//     smallest kept detection containing it (equal areas: the lower detection index, the
+//     stable order; NumPy's argsort leaves ties in an implementation-defined order);
+//   cls[masks[:, :, i]] = i + 1 (dmask.py:56-58), i = index among the kept detections.
+// Three passes over the detector's [H][W][N] byte masks: areas (wave ballots, LDS then
+// global sums), the per-detection keep/rank/label decision (one workgroup), and labels.
+// ------------------------------------------------------------------------------------
+struct MaskScratch {
+    unsigned area[kMaxDetections];
+    unsigned short rank[kMaxDetections];  // order among the kept detections by (area, index); 0xFFFF dropped
+    unsigned char label[kMaxDetections];  // 1 + index among the kept detections
+    unsigned n_kept;
+};
+
+__global__ __launch_bounds__(256) void k_mask_areas(const uint8_t* __restrict__ masks, int npx, int n,
+                                                     MaskScratch* __restrict__ sc) {
+    __shared__ unsigned s_area[kMaxDetections];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) s_area[i] = 0u;
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    for (int base = blockIdx.x * blockDim.x; base < npx; base += gridDim.x * blockDim.x) {
+        const int p = base + (int)threadIdx.x;
+        const uint8_t* row = masks + (size_t)p * n;
+        for (int i = 0; i < n; ++i) {
+            const bool on = p < npx && row[i] != 0;
+            const unsigned c = (unsigned)__popcll(__ballot(on));
+            if (lane == 0 && c) atomicAdd(&s_area[i], c);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x)
+        if (s_area[i]) atomicAdd(&sc->area[i], s_area[i]);
+}
+
+__global__ __launch_bounds__(256) void k_mask_decide(MaskScratch* __restrict__ sc, int n, int min_area) {
+    const int i = threadIdx.x;
+    __shared__ unsigned s_area[kMaxDetections];
+    __shared__ unsigned char s_keep[kMaxDetections];
+    if (i < n) {
+        s_area[i] = sc->area[i];
+        s_keep[i] = (long long)sc->area[i] > (long long)min_area ? 1 : 0;
+    }
+    __syncthreads();
+    if (i < n) {
+        unsigned rank = 0, before = 0;
+        for (int j = 0; j < n; ++j) {
+            if (!s_keep[j]) continue;
+            rank += (s_area[j] < s_area[i] || (s_area[j] == s_area[i] && j < i)) ? 1u : 0u;
+            before += j < i ? 1u : 0u;
+        }
+        sc->rank[i] = s_keep[i] ? (unsigned short)rank : (unsigned short)0xFFFF;
+        sc->label[i] = (unsigned char)(before + 1);  // uint8 label (dmask.py:56), wraps as the reference's
+    }
+    if (i == 0) {
+        unsigned k = 0;
+        for (int j = 0; j < n; ++j) k += s_keep[j];
+        sc->n_kept = k;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_mask_labels(const uint8_t* __restrict__ masks, int npx, int n,
+                                                      const MaskScratch* __restrict__ sc, uint8_t* __restrict__ out) {
+    __shared__ unsigned short s_rank[kMaxDetections];
+    __shared__ unsigned char s_label[kMaxDetections];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        s_rank[i] = sc->rank[i];
+        s_label[i] = sc->label[i];
+    }
+    __syncthreads();
+    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < npx; p += gridDim.x * blockDim.x) {
+        const uint8_t* row = masks + (size_t)p * n;
+        unsigned best = 0xFFFFu;
+        unsigned char lab = 0;
+        for (int i = 0; i < n; ++i) {
+            const unsigned r = row[i] ? s_rank[i] : 0xFFFFu;
+            if (r < best) {
+                best = r;
+                lab = s_label[i];
+            }
+        }
+        out[p] = lab;
+    }
+}
+
+hipError_t launch_masks_to_labels(const uint8_t* masks, int npx, int n, int min_area, void* scratch, uint8_t* out,
+                                  hipStream_t s) {
+    MaskScratch* sc = (MaskScratch*)scratch;
+    hipError_t e = hipMemsetAsync(sc, 0, sizeof(MaskScratch), s);
+    if (e != hipSuccess) return e;
+    int blocks = (npx + 255) / 256;
+    if (blocks > 1024) blocks = 1024;
+    if (n > 0) hipLaunchKernelGGL(k_mask_areas, dim3(blocks), dim3(256), 0, s, masks, npx, n, sc);
+    hipLaunchKernelGGL(k_mask_decide, dim3(1), dim3(kMaxDetections), 0, s, sc, n, min_area);
+    hipLaunchKernelGGL(k_mask_labels, dim3(blocks), dim3(256), 0, s, masks, npx, n, (const MaskScratch*)sc, out);
+    return hipGetLastError();
+}
+
+size_t mask_scratch_bytes() { return sizeof(MaskScratch); }
+size_t mask_scratch_kept_offset() { return offsetof(MaskScratch, n_kept); }
 
 }  // namespace semtsdf

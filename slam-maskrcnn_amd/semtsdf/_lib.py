@@ -156,6 +156,7 @@ SIGNATURES = {
     "semtsdf_shard_assoc_apply": (_I, [_P, _P, _P, C.POINTER(AssocStats), _P]),
     "semtsdf_shard_note_integrated": (_I, [_P, _P, _P]),
     "semtsdf_min_i64": (_I, [_P, _P, C.c_size_t, _P]),
+    "semtsdf_masks_to_labels": (_I, [_P, _I, _I, _I, _I, _P, C.POINTER(C.c_int), _P]),
     "semtsdf_copy_bandwidth": (_I, [_I, C.c_size_t, _I, C.POINTER(C.c_double)]),
     "semtsdf_download": (_I, [_P, _P, _P, _P, _P, _P, _P]),
     "semtsdf_download_slab": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P]),
