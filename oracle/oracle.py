@@ -25,13 +25,18 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "semtsdf_oracle.c")
-LIB = os.path.join(HERE, "liboracle.so")
+# ORACLE_SANITIZE=1: an AddressSanitizer + UndefinedBehaviorSanitizer build (host code only;
+# the Python process needs libasan preloaded, tests/test_oracle_sanitize.py does that)
+SANITIZE = os.environ.get("ORACLE_SANITIZE") == "1"
+LIB = os.path.join(HERE, "liboracle_san.so" if SANITIZE else "liboracle.so")
+SAN_FLAGS = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-fno-sanitize-recover=all"]
 OMAX = 32
 
 
 def build(force: bool = False) -> str:
     if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(SRC):
-        cmd = ["gcc", "-O2", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared", "-std=c11", SRC, "-o", LIB,
+        opt = SAN_FLAGS if SANITIZE else ["-O2"]
+        cmd = ["gcc", *opt, "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared", "-std=c11", SRC, "-o", LIB,
                "-lm"]
         subprocess.check_call(cmd)
     return LIB

@@ -1182,6 +1182,9 @@ static int raycast_impl(semtsdf_vol* v, const float s2w[16], const float c[3], i
     static const char* rs_path = getenv("SEMTSDF_RAY_STATS");
     const size_t rs_words = npx(v) * 4 + ((npx(v) + 63) / 64 + 64) * 4;
     if (rs_path) HIPC(hipMalloc((void**)&a.ray_stats, rs_words * 4));
+    if (rs_path) HIPC(hipMemsetAsync(a.ray_stats, 0, rs_words * 4, s));
+    static const char* rows = getenv("SEMTSDF_RENDER_ROWS");  // instrumentation: "r0,r1"
+    if (rows && sscanf(rows, "%d,%d", &a.row0, &a.row1) != 2) a.row0 = a.row1 = 0;
     timing_begin(v, v->ev_render, s, &ep);
     HIPC(launch_render(a, s));
     timing_end(v, v->ev_render, s, &ep);

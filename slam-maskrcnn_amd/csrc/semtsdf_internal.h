@@ -180,6 +180,7 @@ struct RenderArgs {
     float* out_t;
     unsigned* ray_stats;     // instrumentation (SEMTSDF_RAY_STATS): per pixel iterations, lookups,
                              // evaluations, skipped samples; per wave start/end ticks after them
+    int row0, row1;          // instrumentation (SEMTSDF_RENDER_ROWS): only 16-px tile rows [row0, row1)
 };
 
 // Z-sharded raycast protocol (k_shard_* in semtsdf_kernels.hip): per-pixel march state.

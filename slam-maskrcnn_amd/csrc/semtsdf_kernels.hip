@@ -68,7 +68,13 @@ __device__ __forceinline__ float div_by_rcp(float a, float b, float y) {
 __device__ __forceinline__ float vox_coord(float p, float start, float voxel, float rvox) {
     const float a = p - start;
     float q = div_by_rcp(a, voxel, rvox);
-    if (!(fabsf(a) >= 0x1p-60f)) q = a == 0.0f ? a / voxel : a / voxel;
+    // tiny |a| takes the IEEE quotient; the wave-uniform branch keeps the compiler from
+    // if-converting the division into every sample (it is rare: a sample within 2^-60 of
+    // the volume origin)
+    const bool tiny = !(fabsf(a) >= 0x1p-60f);
+    if (__builtin_expect(__ballot(tiny) != 0ull, 0)) {
+        if (tiny) q = a / voxel;
+    }
     return q;
 }
 
@@ -1439,17 +1445,22 @@ __device__ __forceinline__ TriCoord tri_coord(const VolGeom& g, float px, float 
     const float ix = vox_coord(px, g.start[0], g.voxel[0], g.rvox[0]);
     const float iy = vox_coord(py, g.start[1], g.voxel[1], g.rvox[1]);
     const float iz = vox_coord(pz, g.start[2], g.voxel[2], g.rvox[2]);
-    const int x = f2i_rd(ix), y = f2i_rd(iy), z = f2i_rd(iz);
+    // floor and clamp in the float domain: a sample lies within a few voxels of the volume
+    // box, so floor(i) is an integer far inside the int range and (float)f2i_rd(i) ==
+    // floorf(i); clamp(x, 0, dim - 1) and clamp(x + 1, 0, dim - 1) - clamp(x, 0, dim - 1)
+    // (1 strictly inside [0, dim - 1), else 0) are the same integers as the int forms
+    const float flx = floorf(ix), fly = floorf(iy), flz = floorf(iz);
+    const float hx = (float)(g.dimx - 1), hy = (float)(g.dimy - 1), hz = (float)(g.dimz - 1);
     TriCoord c;
-    c.fx = ix - (float)x;
-    c.fy = iy - (float)y;
-    c.fz = iz - (float)z;
-    c.xc = min(max(x, 0), g.dimx - 1);
-    c.yc = min(max(y, 0), g.dimy - 1);
-    c.zc = min(max(z, 0), g.dimz - 1);
-    c.dxv = min(max(x + 1, 0), g.dimx - 1) - c.xc;
-    c.dyv = min(max(y + 1, 0), g.dimy - 1) - c.yc;
-    c.dzv = min(max(z + 1, 0), g.dimz - 1) - c.zc;
+    c.fx = ix - flx;
+    c.fy = iy - fly;
+    c.fz = iz - flz;
+    c.xc = (int)fminf(fmaxf(flx, 0.0f), hx);
+    c.yc = (int)fminf(fmaxf(fly, 0.0f), hy);
+    c.zc = (int)fminf(fmaxf(flz, 0.0f), hz);
+    c.dxv = ((flx >= 0.0f) & (flx < hx)) ? 1 : 0;
+    c.dyv = ((fly >= 0.0f) & (fly < hy)) ? 1 : 0;
+    c.dzv = ((flz >= 0.0f) & (flz < hz)) ? 1 : 0;
     // global plane -> local plane of this shard (the caller only samples planes it owns;
     // zc + 1 is then the chunk's next plane or its halo plane)
     c.zl = g.nshards == 1 ? c.zc : global_to_local_z(g, c.zc);
@@ -1707,7 +1718,7 @@ struct MarchStats {
 };
 
 #ifndef SEMTSDF_MARCH_SPEC
-#define SEMTSDF_MARCH_SPEC 3
+#define SEMTSDF_MARCH_SPEC 5
 #endif
 constexpr int kMarchSpec = SEMTSDF_MARCH_SPEC;  // speculative samples per evaluated sample
 
@@ -2185,6 +2196,7 @@ __global__ __launch_bounds__(256) void k_render(RenderArgs a) {
     const int x = blockIdx.x * 16 + (threadIdx.x & 15);
     const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
     if (x >= a.width || y >= a.height) return;
+    if (STATS && a.row1 > 0 && ((int)blockIdx.y < a.row0 || (int)blockIdx.y >= a.row1)) return;
     const int px = y * a.width + x;
     float ox, oy, oz, dx, dy, dz, t;
     ray_render(a.cam, x, y, &ox, &oy, &oz, &dx, &dy, &dz);
