@@ -753,6 +753,7 @@ def main():
     traffic, traffic_src = read_traffic(args.traffic_json, D, 1)
     live_units = tc.bricks / args.steps
     free_units = tc.free_units / args.steps
+    full_units = tc.full_units / args.steps
     vol.close()
     for b in (dbuf, rbuf, mbuf):
         b.free()
@@ -795,6 +796,7 @@ def main():
         "gated_per_frame": int(gated),
         "live_units_per_frame": int(live_units),
         "free_units_per_frame": int(free_units),
+        "full_free_units_per_frame": int(full_units),
         "touched_mvox_per_s": round(touched / (kern_ms * 1e-3) / 1e6, 1),
         "roofline": {
             "bound": "hbm",

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SEMTSDF_ABI_VERSION 3
+#define SEMTSDF_ABI_VERSION 4
 #define SEMTSDF_MAX_OBJECTS 32 /* tsdf.cuh:4 */
 
 /* ---- status codes ------------------------------------------------------------ */
@@ -108,6 +108,7 @@ typedef struct semtsdf_timing {
     double prep_ms;       /* sum over the per-frame depth-pyramid + brick-cull passes */
     uint64_t n_prep;
     uint64_t free_units;  /* of those, units whose touched voxels all have f == 1 (count mode only) */
+    uint64_t full_units;  /* of those, free units whose every voxel is touched (no projection; count mode only) */
 } semtsdf_timing;
 
 /* ---- library ------------------------------------------------------------------------ */

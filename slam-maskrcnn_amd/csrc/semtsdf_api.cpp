@@ -88,7 +88,7 @@ struct semtsdf_vol {
     float* render_t_d = nullptr;
     unsigned long long* counters_d = nullptr;
     unsigned* unit_list_d = nullptr;  // live units of the frame (cull pass)
-    unsigned* list_count_d = nullptr; // [2][kListSegs * kListCountStride] (general, free)
+    unsigned* list_count_d = nullptr; // [kLists][kListSegs * kListCountStride] (general, free, full free)
     float* rcp_table_d = nullptr;    // RN(1/n), n = 1..kRcpTable
     AssocDecision* decision_h = nullptr;  // pinned
     // Z-sharded raycast protocol (allocated on first use)
@@ -656,10 +656,11 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     pyr.w1 = (p->width + 31) / 32; pyr.h1 = (p->height + 31) / 32;
     if ((rc = dev_alloc(v, (void**)&pyr.px, (px + 1) * 8))) return bail(rc);
     if (hipMemset(pyr.px, 0, (px + 1) * 8) != hipSuccess) return bail(fail(SEMTSDF_ERR_HIP, "memset failed"));
-    if ((rc = dev_alloc(v, (void**)&pyr.l0, (size_t)pyr.w1 * 4 * pyr.h1 * 4 * 4))) return bail(rc);
-    if ((rc = dev_alloc(v, (void**)&pyr.l1, (size_t)pyr.w1 * pyr.h1 * 4))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&pyr.l0, (size_t)pyr.w1 * 4 * pyr.h1 * 4 * sizeof(uint2)))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&pyr.l1, (size_t)pyr.w1 * pyr.h1 * sizeof(uint2)))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->unit_list_d, unit_list_capacity(g) * sizeof(unsigned)))) return bail(rc);
-    if ((rc = dev_alloc(v, (void**)&v->list_count_d, 2 * kListSegs * kListCountStride * sizeof(unsigned)))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&v->list_count_d, kLists * kListSegs * kListCountStride * sizeof(unsigned))))
+        return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->rcp_table_d, kRcpTable * sizeof(float)))) return bail(rc);
     {
         float t[kRcpTable];
@@ -1431,6 +1432,7 @@ int semtsdf_get_timing(semtsdf_vol* v, semtsdf_timing* out) {
     out->gated = c[1];
     out->bricks = c[3];
     out->free_units = c[4];
+    out->full_units = c[5];
     out->prep_ms = v->t_prep;
     out->n_prep = v->n_prep;
     return SEMTSDF_OK;

@@ -17,6 +17,7 @@ constexpr int kZAlign = 32;      // stored z planes per x,y column: a multiple o
 constexpr int kBrickDistCap = SEMTSDF_BRICK_DIST_CAP;  // brick distance map: radius of the largest skip box (bricks)
 constexpr int kListSegs = 64;    // segments (and counters) of the live-unit list
 constexpr int kListCountStride = 64;  // counters 256 B apart (separate memory channels)
+constexpr int kLists = 3;             // live-unit lists: general, free (projected), full free (no projection)
 
 // Geometry of the locally stored part of the volume.
 struct VolGeom {
@@ -82,8 +83,8 @@ struct DepthPyramid {
     uint2* px;      // [H][W] pixel records {bits of depth / depth_scale (IEEE, tsdf.cu:49),
                     //                       r | g << 8 | b << 16 | label << 24}: one 8-B gather per voxel;
                     // record W*H is zero (the target of off-image voxels)
-    uint32_t* l0;  // [ceil(H/8)][ceil(W/8)]
-    uint32_t* l1;  // [ceil(H/32)][ceil(W/32)]
+    uint2* l0;  // [ceil(H/8)][ceil(W/8)]  {max | (0xFFFF - min nonzero) << 16, 1 if a pixel has depth 0}
+    uint2* l1;  // [ceil(H/32)][ceil(W/32)]
     int w0, h0, w1, h1;
 };
 
@@ -111,11 +112,12 @@ struct IntegrateArgs {
     const int32_t* cls;     // vote
     DepthPyramid pyr;
     unsigned long long* counters;  // [0] touched, [1] gated, [2] bad-label flag, [3] live units, [4] free units
+                                   // (projected and full), [5] full free units
     int pinhole;                   // K rows are (fx 0 cx; 0 fy cy; 0 0 1)
     float rmu;                     // RN(1/mu), for the exact division by mu (k_integrate)
     int fastdiv;                   // mu in [2^-20, 2^20]: divisions by mu/(w+1) via RN reciprocals
-    unsigned* unit_list;           // live units: two lists (general, free) of kListSegs segments (k_cull_units)
-    unsigned* list_count;          // [2][kListSegs * kListCountStride] entries per segment (zeroed by the frame prepass)
+    unsigned* unit_list;           // live units: three lists (general, free, full free) of kListSegs segments (k_cull_units)
+    unsigned* list_count;          // [3][kListSegs * kListCountStride] entries per segment (zeroed by the frame prepass)
     int free_ok;                   // free units allowed: gated colour with gate <= 1 (f == 1 updates sdf/weight only)
 };
 

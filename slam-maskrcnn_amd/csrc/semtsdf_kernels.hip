@@ -47,6 +47,16 @@ __device__ __forceinline__ float dot3(float a0, float a1, float a2, float b0, fl
     return fmaf(a2, b2, fmaf(a1, b1, a0 * b0));
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));  // packed f32 pairs (v_pk_* on gfx950)
+
+// floor and convert in one VALU operation (v_cvt_flr_i32_f32); callers use it only where
+// the operand is finite and far inside the int range
+__device__ __forceinline__ int cvt_flr(float x) {
+    int r;
+    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
 __device__ __forceinline__ float mixf(float a, float b, float t) {
     return fmaf(t, b, (1.0f - t) * a);
 }
@@ -130,36 +140,21 @@ __global__ __launch_bounds__(256) void k_fill_f32(float* __restrict__ p, uint64_
     }
 }
 
-// Achievable-bandwidth probe: a float4 copy with kCopyUnroll independent 16-B loads in flight
-// per lane before their stores (one load per lane per grid step left too few bytes in flight
-// per CU to cover the HBM latency), over a grid of whole residency.
-#ifndef SEMTSDF_COPY_UNROLL
-#define SEMTSDF_COPY_UNROLL 4
-#endif
-#ifndef SEMTSDF_COPY_BLOCKS_PER_CU
-#define SEMTSDF_COPY_BLOCKS_PER_CU 8
-#endif
-constexpr int kCopyUnroll = SEMTSDF_COPY_UNROLL;
+// Achievable-bandwidth probe (semtsdf_copy_bandwidth, the bench's hbm_copy_gbs).
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+// One float4 per thread and one pass over the grid (n/256 workgroups): the shape that
+// reaches the achievable copy rate (6.2 TB/s on MI355X, tools/copybench.hip; persistent
+// grid-stride loops stay at 4.2-5.3 TB/s whatever their unroll, grid or cache policy).
 __global__ __launch_bounds__(256) void k_copy_f4(const f32x4* __restrict__ a, f32x4* __restrict__ b, size_t n) {
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + (kCopyUnroll - 1) * stride < n; i += kCopyUnroll * stride) {
-        f32x4 v[kCopyUnroll];
-#pragma unroll
-        for (int k = 0; k < kCopyUnroll; ++k) v[k] = __builtin_nontemporal_load(a + i + k * stride);
-#pragma unroll
-        for (int k = 0; k < kCopyUnroll; ++k) __builtin_nontemporal_store(v[k], b + i + k * stride);
-    }
-    for (; i < n; i += stride) b[i] = a[i];
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        b[i] = a[i];
 }
 
 hipError_t launch_copy_f4(const void* src, void* dst, size_t n16, hipStream_t s) {
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        cus = 256;
-    hipLaunchKernelGGL(k_copy_f4, dim3((unsigned)cus * SEMTSDF_COPY_BLOCKS_PER_CU), dim3(256), 0, s, (const f32x4*)src,
-                       (f32x4*)dst, n16);
+    size_t blocks = (n16 + 255) / 256;
+    if (blocks > 0x7FFFFFFFu) blocks = 0x7FFFFFFFu;
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_copy_f4, dim3((unsigned)blocks), dim3(256), 0, s, (const f32x4*)src, (f32x4*)dst, n16);
     return hipGetLastError();
 }
 
@@ -331,14 +326,15 @@ __global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restric
                                                        int vec, DepthPyramid p, unsigned* list_count) {
     const int tx = blockIdx.x, ty = blockIdx.y;
     const int t = threadIdx.x;
-    if (list_count && tx == 0 && ty == 0 && t < 2 * kListSegs)  // this frame's two lists (general, free)
+    if (list_count && tx == 0 && ty == 0 && t < kLists * kListSegs)  // this frame's lists (general, free, full)
         list_count[(t & (kListSegs - 1)) * kListCountStride + (t >> 6) * kListSegs * kListCountStride] = 0u;
     const int r = t >> 3;          // row in tile
     const int c4 = (t & 7) * 4;    // first column in tile
     const int yy = ty * 32 + r;
     const int x0 = tx * 32 + c4;
-    // m: max raw depth; n: 0xFFFF - min nonzero raw depth (0: no nonzero pixel); both reduce by max
-    unsigned m = 0, n = 0;
+    // m: max raw depth; n: 0xFFFF - min nonzero raw depth (0: no nonzero pixel); both reduce by
+    // max; z: 1 when a pixel of the lane has depth 0 (reduces by max too)
+    unsigned m = 0, n = 0, z = 0;
     if (yy < h && x0 < w) {
         const size_t px0 = (size_t)yy * w + x0;
         if (vec && x0 + 3 < w) {
@@ -347,6 +343,7 @@ __global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restric
             m = max(max(d[0], d[1]), max(d[2], d[3]));
 #pragma unroll
             for (int k = 0; k < 4; ++k) n = max(n, d[k] ? 0xFFFFu - d[k] : 0u);
+            z = (d[0] == 0u) | (d[1] == 0u) | (d[2] == 0u) | (d[3] == 0u);
             uint4 o = make_uint4(0, 0, 0, 0);
             if (rgb) {
                 const uint32_t* c = reinterpret_cast<const uint32_t*>(rgb + px0 * 3);
@@ -367,6 +364,7 @@ __global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restric
                 const unsigned d = depth[px];
                 m = max(m, d);
                 n = max(n, d ? 0xFFFFu - d : 0u);
+                z |= d == 0u ? 1u : 0u;
                 unsigned c = 0;
                 if (rgb) {
                     const unsigned lab = mask ? (unsigned)mask[px] : 0u;
@@ -383,23 +381,26 @@ __global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restric
     for (int b : {1, 8, 16, 32}) {
         m = max(m, (unsigned)__shfl_xor((int)m, b));
         n = max(n, (unsigned)__shfl_xor((int)n, b));
+        z = max(z, (unsigned)__shfl_xor((int)z, b));
     }
     const int wv = t >> 6, ln = t & 63;
     if (ln < 8 && (ln & 1) == 0) {
         const int gx0 = tx * 4 + (ln >> 1), gy0 = ty * 4 + wv;
-        if (gx0 < p.w0 && gy0 < p.h0) p.l0[gy0 * p.w0 + gx0] = m | (n << 16);
+        if (gx0 < p.w0 && gy0 < p.h0) p.l0[gy0 * p.w0 + gx0] = make_uint2(m | (n << 16), z);
     }
 #pragma unroll
     for (int b : {2, 4}) {
         m = max(m, (unsigned)__shfl_xor((int)m, b));
         n = max(n, (unsigned)__shfl_xor((int)n, b));
+        z = max(z, (unsigned)__shfl_xor((int)z, b));
     }
-    __shared__ unsigned s_w[4], s_n[4];
-    if (ln == 0) { s_w[wv] = m; s_n[wv] = n; }
+    __shared__ unsigned s_w[4], s_n[4], s_z[4];
+    if (ln == 0) { s_w[wv] = m; s_n[wv] = n; s_z[wv] = z; }
     __syncthreads();
     if (t == 0)
-        p.l1[ty * p.w1 + tx] = max(max(s_w[0], s_w[1]), max(s_w[2], s_w[3])) |
-                               (max(max(s_n[0], s_n[1]), max(s_n[2], s_n[3])) << 16);
+        p.l1[ty * p.w1 + tx] = make_uint2(max(max(s_w[0], s_w[1]), max(s_w[2], s_w[3])) |
+                                              (max(max(s_n[0], s_n[1]), max(s_n[2], s_n[3])) << 16),
+                                          max(max(s_z[0], s_z[1]), max(s_z[2], s_z[3])));
 }
 
 hipError_t launch_depth_pyramid(const uint16_t* depth, const uint8_t* rgb, const uint8_t* mask, int w, int h,
@@ -541,38 +542,43 @@ __device__ int unit_cull(const IntegrateArgs& a, int x0, int y0, int lz0) {
     // max depth (and min nonzero depth) over the footprint, on the finest pyramid level
     // covering it with <= 4x4 tiles: the 16 loads are issued together (predicated), one round trip
     unsigned m = 0, nz = 0;  // nz: 0xFFFF - min nonzero raw depth (0: none)
+    unsigned zf = 0;         // a pixel of the covering tiles has depth 0
     const bool fit0 = ((u1 >> 3) - (u0 >> 3)) < 4 && ((v1 >> 3) - (v0 >> 3)) < 4;
     const bool fit1 = ((u1 >> 5) - (u0 >> 5)) < 4 && ((v1 >> 5) - (v0 >> 5)) < 4;
     if (!fit0 && ((u1 >> 3) - (u0 >> 3) + 1) * ((v1 >> 3) - (v0 >> 3) + 1) <= 16) {  // thin footprints
         for (int ty = v0 >> 3; ty <= (v1 >> 3); ++ty)
             for (int tx = u0 >> 3; tx <= (u1 >> 3); ++tx) {
-                const unsigned w = a.pyr.l0[ty * a.pyr.w0 + tx];
-                m = max(m, w & 0xFFFFu);
-                nz = max(nz, w >> 16);
+                const uint2 w = a.pyr.l0[ty * a.pyr.w0 + tx];
+                m = max(m, w.x & 0xFFFFu);
+                nz = max(nz, w.x >> 16);
+                zf |= w.y;
             }
     } else if (fit0 || fit1) {
         const int sh = fit0 ? 3 : 5;
-        const uint32_t* lv = fit0 ? a.pyr.l0 : a.pyr.l1;
+        const uint2* lv = fit0 ? a.pyr.l0 : a.pyr.l1;
         const int wl = fit0 ? a.pyr.w0 : a.pyr.w1;
         const int tx0 = u0 >> sh, ty0 = v0 >> sh, nx = (u1 >> sh) - tx0, ny = (v1 >> sh) - ty0;
-        unsigned t[16];
+        uint2 t[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             const bool ok = (j & 3) <= nx && (j >> 2) <= ny;
             t[j] = lv[ok ? (ty0 + (j >> 2)) * wl + tx0 + (j & 3) : 0];
-            t[j] = ok ? t[j] : 0u;
+            t[j].x = ok ? t[j].x : 0u;
+            t[j].y = ok ? t[j].y : 0u;
         }
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-            m = max(m, t[j] & 0xFFFFu);
-            nz = max(nz, t[j] >> 16);
+            m = max(m, t[j].x & 0xFFFFu);
+            nz = max(nz, t[j].x >> 16);
+            zf |= t[j].y;
         }
     } else if (((u1 >> 5) - (u0 >> 5) + 1) * ((v1 >> 5) - (v0 >> 5) + 1) <= 64) {
         for (int ty = v0 >> 5; ty <= (v1 >> 5); ++ty)
             for (int tx = u0 >> 5; tx <= (u1 >> 5); ++tx) {
-                const unsigned w = a.pyr.l1[ty * a.pyr.w1 + tx];
-                m = max(m, w & 0xFFFFu);
-                nz = max(nz, w >> 16);
+                const uint2 w = a.pyr.l1[ty * a.pyr.w1 + tx];
+                m = max(m, w.x & 0xFFFFu);
+                nz = max(nz, w.x >> 16);
+                zf |= w.y;
             }
     } else {
         return 0;  // footprint wider than 256x256 px (units at the near plane): keep
@@ -587,7 +593,17 @@ __device__ int unit_cull(const IntegrateArgs& a, int x0, int y0, int lz0) {
     // f == 1 exactly; with the gate at or below 1 such a voxel updates only its sdf and weight
     if (a.free_ok && nz != 0) {
         const float dmin = (float)(0xFFFFu - nz) / a.depth_scale;
-        if (dmin - zmax > g.mu + margin) return 2;
+        if (dmin - zmax > g.mu + margin) {
+            // full free unit: besides, every voxel is stored and inside the volume, projects
+            // into the image (hull 1 px inside it: the cull map's ~1e-4 px error cannot move a
+            // pixel out) and its pixel has depth != 0 (no zero in the covering tiles), so every
+            // voxel is touched with f == 1: the integrate needs no projection
+            const bool inside = x0 + UX <= g.dimx && y0 + UY <= g.dimy && lz0 + UZ <= g.lz &&
+                                local_to_global_z(g, lz0 + UZ - 1) < g.dimz;
+            if (inside && zf == 0u && umin >= 1.0f && vmin >= 1.0f && umax <= W - 2.0f && vmax <= H - 2.0f)
+                return 3;
+            return 2;
+        }
     }
     return 0;
 }
@@ -628,8 +644,8 @@ __host__ __device__ inline unsigned list_seg_cap(const UnitGrid& ug) {
 // list 1 (free units, unit_cull == 2), each kListSegs segments of seg_cap entries with its
 // own counters (their order is irrelevant: units are independent).
 __global__ __launch_bounds__(256) void k_cull_units(IntegrateArgs a, UnitGrid ug, unsigned seg_cap) {
-    __shared__ unsigned s_cnt[2][4];
-    __shared__ unsigned s_base[2];
+    __shared__ unsigned s_cnt[kLists][4];
+    __shared__ unsigned s_base[kLists];
     // grid (x runs of 256 units, uy, uz): no integer division by the runtime unit counts
     const unsigned ux = blockIdx.x * blockDim.x + threadIdx.x, uy = blockIdx.y, uz = blockIdx.z;
     const unsigned u = pack_unit(ux, uy, uz);
@@ -637,22 +653,24 @@ __global__ __launch_bounds__(256) void k_cull_units(IntegrateArgs a, UnitGrid ug
     int c = 1;  // dead
     if (ux < ug.nux) c = a.cull ? unit_cull(a, (int)ux * UX, (int)uy * UY, (int)uz * UZ) : 0;
     const int lane = (int)(threadIdx.x & 63u), wv = (int)(threadIdx.x >> 6);
-    const unsigned long long bal0 = __ballot(c == 0), bal1 = __ballot(c == 2);
+    // list of class c: 0 general (c == 0), 1 free (c == 2), 2 full free (c == 3)
+    const unsigned long long bal0 = __ballot(c == 0), bal1 = __ballot(c == 2), bal2 = __ballot(c == 3);
     if (lane == 0) {
         s_cnt[0][wv] = (unsigned)__popcll(bal0);
         s_cnt[1][wv] = (unsigned)__popcll(bal1);
+        s_cnt[2][wv] = (unsigned)__popcll(bal2);
     }
     __syncthreads();
     const unsigned seg = bid % (unsigned)kListSegs;
-    if (threadIdx.x < 2) {
+    if (threadIdx.x < kLists) {
         const unsigned l = threadIdx.x;
         const unsigned tot = s_cnt[l][0] + s_cnt[l][1] + s_cnt[l][2] + s_cnt[l][3];
         s_base[l] = tot ? atomicAdd(a.list_count + (l * kListSegs + seg) * kListCountStride, tot) : 0u;
     }
     __syncthreads();
     if (c != 1) {
-        const unsigned l = c == 2 ? 1u : 0u;
-        unsigned off = s_base[l] + (unsigned)__popcll((l ? bal1 : bal0) & ((1ull << lane) - 1ull));
+        const unsigned l = c == 2 ? 1u : c == 3 ? 2u : 0u;
+        unsigned off = s_base[l] + (unsigned)__popcll((l == 1 ? bal1 : l == 2 ? bal2 : bal0) & ((1ull << lane) - 1ull));
         for (int w = 0; w < wv; ++w) off += s_cnt[l][w];
         a.unit_list[(size_t)l * kListSegs * seg_cap + seg * seg_cap + off] = u;
     }
@@ -667,7 +685,7 @@ hipError_t launch_cull(const IntegrateArgs& a, hipStream_t s) {
 }
 
 uint64_t unit_count(const VolGeom& g) { return unit_grid(g).n; }
-uint64_t unit_list_capacity(const VolGeom& g) { return (uint64_t)list_seg_cap(unit_grid(g)) * kListSegs * 2; }
+uint64_t unit_list_capacity(const VolGeom& g) { return (uint64_t)list_seg_cap(unit_grid(g)) * kListSegs * kLists; }
 
 // Exact floor of the colour running mean (c*w + x) / (w + 1) for 0 <= c, x <= 255 and
 // w + 1 <= kRcpTable, from r = RN(1/(w+1)): floor(RN(num*r + 2^-12)) equals the integer
@@ -778,9 +796,17 @@ struct Out {
 
 // Screen position s = M p + m (DESIGN.md §4 contract; per-row bases then one fma per
 // coordinate per voxel), the exact pixel through the reciprocal, and the record gather.
-template <bool SHARD, bool PIN, bool FREE>
+template <bool SHARD, bool PIN, bool FREE, bool FULL>
 __device__ __forceinline__ void stage_project(const IntegrateArgs& a, const UnitPos& up, int lane, Proj& P) {
     const VolGeom& g = a.g;
+    if (FULL) {  // full free unit (unit_cull == 3): every voxel touched with f == 1, nothing to project
+        P.sflag = SEMTSDF_STEADY ? (unsigned)a.b.sflag[(unit_tile(g, up) + (unsigned)lane_zq(lane) * 32u +
+                                                        (unsigned)lane_y(lane) * 4u) >> 5]
+                                 : 0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) P.rec[k] = make_uint2(up.ok ? 1u : 0u, 0u);  // "depth != 0" of a real unit
+        return;
+    }
     const int npx = a.width * a.height;
     const int x = up.x * UX + lane_x(lane);
     const int y = up.uy * UY + lane_y(lane);
@@ -792,6 +818,10 @@ __device__ __forceinline__ void stage_project(const IntegrateArgs& a, const Unit
     const float bsy = fmaf(a.M[4], py, fmaf(a.M[3], px, a.m[1]));
     const float bsz = fmaf(a.M[7], py, fmaf(a.M[6], px, a.m[2]));
     const float bqz = PIN ? bsz : fmaf(a.E[9], py, fmaf(a.E[8], px, a.E[11]));
+    // (sx, sy) pairs in packed f32 (v_pk_fma / v_pk_mul / v_pk_add: each lane of a packed op is
+    // the scalar IEEE operation, so the values are those of the scalar contract)
+    const f32x2 bsxy = {bsx, bsy}, Mxy = {a.M[2], a.M[5]};
+    const float fl0 = (float)l0;  // (float)(l0 + k) == fl0 + k: integers far below 2^24
     unsigned slow = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -801,9 +831,8 @@ __device__ __forceinline__ void stage_project(const IntegrateArgs& a, const Unit
             gz = local_to_global_z(g, l0 + k);
             zok = zok & (gz < g.dimz);
         }
-        const float pz = fmaf((float)gz, g.voxel[2], g.start[2]);
-        const float sx = fmaf(a.M[2], pz, bsx);
-        const float sy = fmaf(a.M[5], pz, bsy);
+        const float pz = fmaf(SHARD ? (float)gz : fl0 + (float)k, g.voxel[2], g.start[2]);
+        const f32x2 sxy = __builtin_elementwise_fma(Mxy, (f32x2){pz, pz}, bsxy);
         const float sz = fmaf(a.M[8], pz, bsz);
         P.qz[k] = PIN ? sz : fmaf(a.E[10], pz, bqz);
         // floor(sx/sz), floor(sy/sz) through the reciprocal: |qu - RN(sx/sz)| <= 2^-22 |qu|,
@@ -811,10 +840,10 @@ __device__ __forceinline__ void stage_project(const IntegrateArgs& a, const Unit
         // B 2^-21 from 0 and 1 floors like the IEEE quotient; |qu| >= B is off-image either
         // way; NaN/Inf and near-integers fail the window and are redone exactly below.
         const float r = __builtin_amdgcn_rcpf(sz);
-        const float qu = sx * r, qv = sy * r;
-        const float eu = __builtin_amdgcn_fractf(qu) - 0.5f, ev = __builtin_amdgcn_fractf(qv) - 0.5f;
-        const bool fast = (fabsf(eu) < a.ftol) & (fabsf(ev) < a.ftol);
-        const int iu = (int)floorf(qu), iv = (int)floorf(qv);
+        const f32x2 q = sxy * r;
+        const f32x2 e = (f32x2){__builtin_amdgcn_fractf(q.x), __builtin_amdgcn_fractf(q.y)} - 0.5f;
+        const bool fast = (fabsf(e.x) < a.ftol) & (fabsf(e.y) < a.ftol);
+        const int iu = cvt_flr(q.x), iv = cvt_flr(q.y);  // the window holds only |q| < 2^23
         slow |= ((zok & !fast) ? 1u : 0u) << k;
         const bool in = zok & fast & ((unsigned)iu < (unsigned)a.width) & ((unsigned)iv < (unsigned)a.height);
         P.img[k] = in ? (int)__umul24((unsigned)iv, (unsigned)a.width) + iu : npx;
@@ -840,7 +869,9 @@ __device__ __forceinline__ void stage_project(const IntegrateArgs& a, const Unit
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         if (FREE)
-            P.rec[k] = make_uint2(reinterpret_cast<const unsigned*>(a.pyr.px)[2u * (unsigned)P.img[k]], 0u);
+            P.rec[k] = make_uint2(
+                reinterpret_cast<const unsigned*>(a.pyr.px)[(kProbes && a.debug == 21) ? 0u : 2u * (unsigned)P.img[k]],
+                0u);
         else
             P.rec[k] = a.pyr.px[(kProbes && a.debug == 21) ? 0u : (unsigned)P.img[k]];  // 21: probe, one address
 #if SEMTSDF_PROBE_GATHER2
@@ -865,6 +896,7 @@ __device__ __forceinline__ void stage_classify(const IntegrateArgs& a, const Pro
             C.pix[k] = 0u;
         }
         C.sflag = P.sflag;
+        if (kProbes && (a.debug == 3 || a.debug == 21)) tm = 0u;  // probe: no state traffic
         C.tmask = tm;
         C.gmask = 0u;
         C.hlab = 0xFFu;
@@ -1217,7 +1249,7 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
 // One list of the frame (general or free units) by the persistent waves: wave w takes the
 // groups w', w' + nwaves, ... with w' = (w - rot) mod nwaves (rot balances the extra groups of
 // the two lists), a group being kSlots consecutive entries, one unit per slot.
-template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT, bool SHARD, bool PIN, bool FREE>
+template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT, bool SHARD, bool PIN, bool FREE, bool FULL = false>
 __device__ __forceinline__ unsigned integrate_list(const IntegrateArgs& a, const UnitGrid& ug, unsigned seg_cap,
                                                    const float* __restrict__ s_rcp, const unsigned* list,
                                                    const unsigned* list_count, unsigned wave, unsigned nwaves,
@@ -1277,7 +1309,7 @@ __device__ __forceinline__ unsigned integrate_list(const IntegrateArgs& a, const
         Cls C;
         Ld L;
         Out O;
-        stage_project<SHARD, PIN, FREE>(a, cur, lane, P);
+        stage_project<SHARD, PIN, FREE, FULL>(a, cur, lane, P);
         stage_classify<SEM, GATE, VOTE, COUNT, FREE>(a, P, C, true, n_touch, n_gate);
         stage_load<SEM, CI32, VOTE, FREE>(a, cur, coff, C, L);
         while (true) {
@@ -1286,7 +1318,7 @@ __device__ __forceinline__ unsigned integrate_list(const IntegrateArgs& a, const
             // operations issued per iteration do not depend on the branch
             const UnitPos nxt = has ? lane_pos(en) : cur;
             if (i + 2u * nwaves < ngroups) group_entries(i + 2u * nwaves, en);
-            stage_project<SHARD, PIN, FREE>(a, nxt, lane, P);
+            stage_project<SHARD, PIN, FREE, FULL>(a, nxt, lane, P);
             if (SEMTSDF_FULLROW || C.tmask) stage_compute<SEM, GATE, CI32, VOTE, FREE>(a, s_rcp, C, L, O);
             const StoreMeta Mc = store_meta(C);
             stage_classify<SEM, GATE, VOTE, COUNT, FREE>(a, P, C, has, n_touch, n_gate);
@@ -1317,12 +1349,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
     unsigned n_touch = 0, n_gate = 0;
     unsigned rot = 0, nlive = 0;
     if (GATE && !VOTE) {  // free units exist only in gated modes (free_ok)
-        const unsigned n1 = integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, true>(
+        const unsigned n1 = integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, true, false>(
             a, ug, seg_cap, s_rcp, a.unit_list + (size_t)kListSegs * seg_cap, a.list_count + kListSegs * kListCountStride,
             wave, nwaves, 0u, n_touch, n_gate);
-        rot = (n1 + kSlots - 1) / kSlots % nwaves;
-        if (COUNT && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.counters + 4, (unsigned long long)n1);
-        if (COUNT) nlive += n1;
+        const unsigned g1 = (n1 + kSlots - 1) / kSlots;
+        const unsigned n2 = integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, true, true>(
+            a, ug, seg_cap, s_rcp, a.unit_list + (size_t)2 * kListSegs * seg_cap,
+            a.list_count + 2 * kListSegs * kListCountStride, wave, nwaves, g1 % nwaves, n_touch, n_gate);
+        rot = (g1 + (n2 + kSlots - 1) / kSlots) % nwaves;
+        if (COUNT && blockIdx.x == 0 && threadIdx.x == 0) {
+            atomicAdd(a.counters + 4, (unsigned long long)(n1 + n2));
+            atomicAdd(a.counters + 5, (unsigned long long)n2);
+        }
+        if (COUNT) nlive += n1 + n2;
     }
     const unsigned n0 = integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, false>(
         a, ug, seg_cap, s_rcp, a.unit_list, a.list_count, wave, nwaves, rot, n_touch, n_gate);
@@ -1782,7 +1821,7 @@ __device__ bool march_ray(const VolGeom& g, const VolBufs& b, float ox, float oy
         if (f_tt < 0.0f) break;
         f_t = f_tt;
         prev_skipped = false;
-        if (f_tt < vx / 2.0f) {  // sticky quarter step
+        if (f_tt < vx / 2.0f && step != vx / 4.0f) {  // sticky quarter step (switches once)
             step = vx / 4.0f;
             t += step;
             continue;
@@ -1811,7 +1850,7 @@ __device__ bool march_ray(const VolGeom& g, const VolBufs& b, float ox, float oy
                     break;
                 }
                 f_t = f_tt;
-                if (f_tt < vx / 2.0f) {
+                if (f_tt < vx / 2.0f && step != vx / 4.0f) {  // the step switches: the rest is stale
                     step = vx / 4.0f;
                     t += step;
                     break;

@@ -108,6 +108,7 @@ class Timing(C.Structure):
         ("prep_ms", C.c_double),
         ("n_prep", C.c_uint64),
         ("free_units", C.c_uint64),
+        ("full_units", C.c_uint64),
     ]
 
 

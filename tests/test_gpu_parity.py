@@ -663,3 +663,31 @@ def test_steady_lines_repeated_frames_and_weight_limit(S, oracle, stream):
         oracle.integrate(g, ost, list(p.K), E, fr.depth, fr.rgb, fr.gt_ids, flags=0x3)
     assert_same(vol, ost, hist=True)
     vol.close()
+
+
+def test_full_free_units_hole_free_frames(S, oracle, stream):
+    """Full free units (cull class 3: every voxel in the image with a nonzero depth pixel and
+    f == 1, integrated without projection): frames whose depth holes are filled make them
+    common; every array stays bit-identical to the exhaustive oracle."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    st, frames = stream
+    filled = []
+    for fr in frames[:4]:
+        d = fr.depth.copy()
+        d[d == 0] = np.uint16(d[d > 0].max())  # holes become far samples
+        filled.append(d)
+    p, vol, g, ost = make(S, oracle, (256, 256, 256), frames[0], 0x3)
+    vol.set_instrumentation(events=False, count=True)
+    slabs = [(x, x + 32) for x in range(0, 256, 32)]
+    with ThreadPoolExecutor(8) as ex:
+        for k in range(1, 4):
+            fr = frames[k]
+            E = (fr.w2c @ frames[0].c2w).astype(np.float32)
+            vol.integrate(filled[k], fr.rgb, fr.gt_ids, E)
+            list(ex.map(lambda r: oracle.integrate(g, ost, list(p.K), E, filled[k], fr.rgb, fr.gt_ids, flags=0x3,
+                                                   x_range=r), slabs))
+    tm = vol.timing()
+    assert tm.full_units > 1000 and tm.free_units >= tm.full_units
+    assert_same(vol, ost, hist=True)
+    vol.close()
