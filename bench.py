@@ -246,17 +246,22 @@ def resident_frames(frames, with_mask=True, ids=False):
     return dbuf, rbuf, mbuf
 
 
-def timed_integrate(vol, step, K, warmup, pg=None, device=0):
-    """Wall time of K steps (barrier + sync on both sides), then the same K steps again
-    with kernel events (integrate kernel, prepass) and once more counting voxels."""
+def timed_integrate(vol, step, K, warmup, pg=None, device=0, finish=None):
+    """Wall time of K steps (barrier + sync on both sides; `finish`, if given, runs once
+    after them inside the timed region), then the same K steps again with kernel events
+    (integrate kernel, prepass) and once more counting voxels."""
     for k in range(warmup):
         step(k)
+    if finish is not None:
+        finish()
     vol.sync()
     barrier(pg, device)
     vol.sync()
     t0 = time.perf_counter()
     for k in range(K):
         step(warmup + k)
+    if finish is not None:
+        finish()
     vol.sync()
     barrier(pg, device)
     elapsed = time.perf_counter() - t0
@@ -561,9 +566,14 @@ def c4_params(semtsdf, L, f0, world=1, rank=0, chunk=64):
     return p
 
 
+C4_SPEC = ("C4: 1024^3 semantic TSDF (sdf f32, weight i32, colour u8x3, 32-bin u32 histogram); per step one frame "
+           "integrated, and after the K steps one label raycast view (the north star's final raycast composite)")
+
+
 def run_c4_single(semtsdf, L, local, frames, f0, K, warmup):
-    """C4's 1024^3 semantic volume whole on one GPU: integrate + one label raycast view per
-    step (the single-GPU base of the strong-scaling lines)."""
+    """C4's 1024^3 semantic volume whole on one GPU (the base of the strong-scaling lines):
+    K integrated frames + the final label raycast, then the per-frame variant (integrate +
+    one raycast view every step)."""
     from semtsdf.volume import DeviceBuffer
 
     p = c4_params(semtsdf, L, f0)
@@ -573,20 +583,33 @@ def run_c4_single(semtsdf, L, local, frames, f0, K, warmup):
     mean_m = float(np.mean(f0.depth[f0.depth > 0]) / 5000.0)
     out = DeviceBuffer(NPX * 3)
 
-    def step(k):
+    def integ(k):
         i = k % len(frames)
         vol.integrate_dev(dbuf.ptr + i * NPX * 2, rbuf.ptr + i * NPX * 3, mbuf.ptr + i * NPX, Es[i])
+
+    def view(k=0):
         s2w, c = semtsdf.orbit_camera(list(p.Kinv), 0.01 * k, mean_m)
         vol.raycast_dev(s2w, c, L.RENDER_LABEL, out.ptr)
 
-    elapsed, tm, tc = timed_integrate(vol, step, K, warmup)
+    elapsed, tm, tc = timed_integrate(vol, integ, K, warmup, finish=view)
+    vol.reset_timing()
+    vol.set_instrumentation(events=True, count=False)
+    view()
+    vol.sync()
+    render_ms = vol.timing().render_ms
+    vol.set_instrumentation(events=False, count=False)
+    Kf = max(4, K // 3)
+    elapsed_f, _, _ = timed_integrate(vol, lambda k: (integ(k), view(k)), Kf, 1)
     res = {
-        "workload": "C4 on one GPU: 1024^3 semantic TSDF (144 GiB), integrate + 1 label raycast view per step",
+        "workload": "C4 on one GPU: " + C4_SPEC + " (144 GiB)",
         "value": round(1024 ** 3 * K / elapsed / 1e6, 2), "unit": "Mvoxel-updates/s",
-        "ms_per_step": round(elapsed * 1e3 / K, 4),
+        "ms_per_step": round(elapsed * 1e3 / K, 4), "steps": K,
         "integrate_kernel_ms": round(tm.integrate_ms / max(tm.n_integrate, 1), 4),
         "prep_ms": round(tm.prep_ms / max(tm.n_prep, 1), 4),
-        "render_ms_per_view": round(tm.render_ms / max(tm.n_render, 1), 4),
+        "final_render_ms": round(render_ms, 4),
+        "per_frame_view": {"value": round(1024 ** 3 * Kf / elapsed_f / 1e6, 2), "unit": "Mvoxel-updates/s",
+                           "ms_per_step": round(elapsed_f * 1e3 / Kf, 4), "steps": Kf,
+                           "step": "integrate + one label raycast view per frame"},
         "touched_per_frame": int(tc.touched / K),
         "device_gib": round(vol.state().device_bytes / 2 ** 30, 1),
     }
@@ -598,9 +621,10 @@ def run_c4_single(semtsdf, L, local, frames, f0, K, warmup):
 
 
 def run_c4_dist(semtsdf, L, rank, world, local, pg, frames, f0, K, warmup, chunk):
-    """C4 strong scaling: rank r integrates shard r of the 1024^3 volume and every step
-    composites one label raycast view across the shards (DistShardGroup, RCCL all-reduce
-    MIN between protocol steps)."""
+    """C4 strong scaling: rank r integrates shard r of the 1024^3 volume (no collective on
+    that path); after the K frames one label raycast view is composited across the shards
+    (DistShardGroup: RCCL all-reduce MIN between the protocol steps).  Then the per-frame
+    variant: the composite after every frame."""
     import torch
 
     from semtsdf.shard import DistShardGroup
@@ -614,21 +638,34 @@ def run_c4_dist(semtsdf, L, rank, world, local, pg, frames, f0, K, warmup, chunk
     out = torch.empty(NPX * 3, dtype=torch.uint8, device=torch.device("cuda", local))
     torch.cuda.synchronize()
 
-    def step(k):
+    def integ(k):
         i = k % len(frames)
         vol.integrate_dev(dbuf.ptr + i * NPX * 2, rbuf.ptr + i * NPX * 3, mbuf.ptr + i * NPX, Es[i])
+
+    def view(k=0):
         s2w, c = semtsdf.orbit_camera(list(p.Kinv), 0.01 * k, mean_m)
         grp.raycast_dev(s2w, c, L.RENDER_LABEL, out.data_ptr())
 
-    elapsed, tm, tc = timed_integrate(vol, step, K, warmup, pg, local)
+    elapsed, tm, tc = timed_integrate(vol, integ, K, warmup, pg, local, finish=view)
     t_max = max_over_ranks(pg, local, elapsed)
     kern = tm.integrate_ms / max(tm.n_integrate, 1)
     prep = tm.prep_ms / max(tm.n_prep, 1)
+    # the composite alone, timed around one view (barriers on both sides)
+    vol.sync()
+    barrier(pg, local)
+    tc0 = time.perf_counter()
+    view()
+    vol.sync()
+    barrier(pg, local)
+    comp = max_over_ranks(pg, local, time.perf_counter() - tc0)
+    Kf = max(4, K // 3)
+    elapsed_f, _, _ = timed_integrate(vol, lambda k: (integ(k), view(k)), Kf, 1, pg, local)
     res = {
         "elapsed": t_max,
         "integrate_kernel_ms_max": max_over_ranks(pg, local, kern),
         "prep_ms_max": max_over_ranks(pg, local, prep),
-        "composite_ms_per_view": (tm.render_ms / max(tm.n_render, 1)),
+        "composite_ms": comp * 1e3,
+        "per_frame_elapsed": max_over_ranks(pg, local, elapsed_f), "per_frame_steps": Kf,
         "touched_per_frame": sum_over_ranks(pg, local, tc.touched / K),
         "local_planes": int(vol.state().local_dim[2]),
         "device_gib": round(vol.state().device_bytes / 2 ** 30, 1),
@@ -681,21 +718,24 @@ def main():
         r = run_c4_dist(semtsdf, L, rank, world, local, pg, frames, f0, args.steps, args.warmup, args.c4_chunk)
         if rank == 0:
             value = 1024 ** 3 * args.steps / r["elapsed"] / 1e6
+            kf = r["per_frame_steps"]
             rec = {
                 "metric": METRIC, "value": round(value, 2), "unit": "Mvoxel-updates/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(r["elapsed"] * 1e3 / args.steps, 4),
                 "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
                 "data": "synthetic",
-                "config": {"workload": "C4: 1024^3 semantic TSDF (sdf f32, weight i32, colour u8x3, 32-bin u32 "
-                                       "histogram) Z-slab sharded over the ranks (interleaved chunks), per step "
-                                       "integrate + one label raycast view composited across the shards (RCCL "
-                                       "all-reduce MIN between protocol steps); speed-up = value / the N=1 line's "
-                                       "c4_single_gpu.value",
+                "config": {"workload": C4_SPEC + "; Z-slab sharded over the ranks (interleaved chunks), composite by "
+                                       "RCCL all-reduce MIN between protocol steps; speed-up = value / the N=1 "
+                                       "line's c4_single_gpu.value",
                            "volume": [1024, 1024, 1024], "z_chunk": args.c4_chunk, "frames_cycled": len(frames),
                            "parallelism": f"zslab{world}"},
                 "integrate_kernel_ms_max_rank": round(r["integrate_kernel_ms_max"], 4),
                 "prep_ms_max_rank": round(r["prep_ms_max"], 4),
-                "composite_ms_per_view_rank0": round(r["composite_ms_per_view"], 4),
+                "final_composite_ms": round(r["composite_ms"], 4),
+                "per_frame_composite": {"value": round(1024 ** 3 * kf / r["per_frame_elapsed"] / 1e6, 2),
+                                        "unit": "Mvoxel-updates/s",
+                                        "ms_per_step": round(r["per_frame_elapsed"] * 1e3 / kf, 4), "steps": kf,
+                                        "step": "integrate + one composited label view per frame"},
                 "touched_per_frame": int(r["touched_per_frame"]),
                 "local_planes_rank0": r["local_planes"], "device_gib_rank0": r["device_gib"],
             }
@@ -714,7 +754,7 @@ def main():
         elif args.only == "c2":
             r = run_c2(semtsdf, L, local, frames, f0, args.steps, args.warmup)
         else:
-            r = run_c4_single(semtsdf, L, local, frames, f0, max(10, args.steps // 3), args.warmup)
+            r = run_c4_single(semtsdf, L, local, frames, f0, args.steps, args.warmup)
         print(json.dumps({"only": args.only, args.only: r}), flush=True)
         return
     if emu_world > 1:
@@ -764,7 +804,7 @@ def main():
         masks = run_mask_overlap(semtsdf, L, p, local, frames, f0)
         c2 =run_c2(semtsdf, L, local, frames, f0, args.steps, args.warmup)
         if not args.no_c4:
-            c4 = run_c4_single(semtsdf, L, local, frames, f0, max(10, args.steps // 3), args.warmup)
+            c4 = run_c4_single(semtsdf, L, local, frames, f0, args.steps, args.warmup)
     copy_bw = copy_bandwidth(local) if not args.no_pipeline else None
 
     rec = {

@@ -2311,11 +2311,62 @@ __device__ __forceinline__ int2 gather_min(const int2* __restrict__ g, int n, in
     return best;
 }
 
-__device__ __forceinline__ float replay_t(float t, int ncoarse, int nfine, float vx) {
-    for (int i = 0; i < ncoarse; ++i) t += vx;
-    const float q = vx / 4.0f;
-    for (int i = 0; i < nfine; ++i) t += q;
+// t += step repeated n times (t > 0), in O(1) per binade of t: the closed form of skip_steps
+// (inside a binade every RN(t + step) adds the same d, so m additions are t + m d while the
+// result stays in the binade; ties and binade crossings are single additions).
+__device__ __forceinline__ float advance_n(float t, float step, int n) {
+    while (n > 0) {
+        const float t1 = t + step;
+        const int eb = __float_as_int(t) & 0x7F800000;
+        const float ulp = __int_as_float(eb - (23 << 23)), top = __int_as_float(eb + (1 << 23));
+        const float d = t1 - t;  // exact (t1 within a factor 2 of t)
+        int m = 0;
+        if (fabsf(step - d) * 2.0f != ulp && t1 < top) {
+            m = min(max((int)((top - t) * __builtin_amdgcn_rcpf(d)), 1), n);  // estimate, fixed up below
+            while (m > 1 && !(t + (float)m * d < top)) --m;
+        }
+        if (m <= 1) {
+            t = t1;
+            --n;
+            continue;
+        }
+        t = t + (float)m * d;
+        n -= m;
+    }
     return t;
+}
+
+// skip_steps counting its additions in n (t stops at the first value >= tend)
+__device__ __forceinline__ void skip_steps_n(float& t, float step, float tend, int& n) {
+    while (t < tend) {
+        const float t1 = t + step;
+        if (!(t1 < tend)) {
+            t = t1;
+            ++n;
+            break;
+        }
+        const int eb = __float_as_int(t) & 0x7F800000;
+        const float ulp = __int_as_float(eb - (23 << 23)), top = __int_as_float(eb + (1 << 23));
+        const float d = t1 - t;
+        const float lim = fminf(tend, top);
+        int m = 0;
+        if (fabsf(step - d) * 2.0f != ulp && t1 < top) {
+            m = max((int)((lim - t) * __builtin_amdgcn_rcpf(d)), 1);
+            while (m > 1 && !(t + (float)m * d < lim)) --m;
+            while (t + (float)(m + 1) * d < lim) ++m;
+        }
+        if (m <= 1) {
+            t = t1;
+            ++n;
+            continue;
+        }
+        t = t + (float)m * d;
+        n += m;
+    }
+}
+
+__device__ __forceinline__ float replay_t(float t, int ncoarse, int nfine, float vx) {
+    return advance_n(advance_n(t, vx, ncoarse), vx / 4.0f, nfine);
 }
 
 struct RayGeo {
@@ -2339,10 +2390,65 @@ __device__ __forceinline__ float sample_at(const ShardRayArgs& a, const RayGeo& 
     return sample_sdf(a.g, a.b.sdf, fmaf(t, r.dx, r.ox), fmaf(t, r.dy, r.oy), fmaf(t, r.dz, r.oz));
 }
 
-// false when the brick map proves the sample >= voxel/2 (see march_ray)
+// false when the brick map proves the sample >= voxel/2 (see march_ray).  A skippable brick
+// whose 8 local planes lie in one chunk block (so they are 8 consecutive global planes) also
+// leaves its box, in global voxel coordinates, in the cursor: every sample inside it is >=
+// voxel/2 whoever owns it, so the march may step through it with exact additions.
 __device__ __forceinline__ bool sample_at_skip(const ShardRayArgs& a, const RayGeo& r, float t, float thr,
                                                SkipCursor& cur, float* f) {
-    return sample_or_skip(a.g, a.b, thr, cur, fmaf(t, r.dx, r.ox), fmaf(t, r.dy, r.oy), fmaf(t, r.dz, r.oz), f);
+    const VolGeom& g = a.g;
+    const TriCoord c = tri_coord(g, fmaf(t, r.dx, r.ox), fmaf(t, r.dy, r.oy), fmaf(t, r.dz, r.oz));
+    if (a.b.bmin) {
+        const int br = brick_of(g, c);
+        if (br != cur.brick) {
+            cur.brick = br;
+            cur.skip = a.b.bmin[br] >= thr;
+            cur.lo[0] = 1e30f;  // no box unless set below
+            cur.hi[0] = -1e30f;
+            const int per = g.nshards > 1 ? g.chunk + g.halo : INT_MAX;  // local planes per chunk block
+            const int l0 = (c.zl >> 3) << 3;
+            if (cur.skip && l0 / per == (l0 + 7) / per) {
+                // samples based on planes w < chunk of the block read planes this shard stores
+                // (w + 1 <= chunk: the halo at most); a base on the halo plane would read the
+                // next chunk's second plane, which the brick's minimum does not cover
+                const int w0 = g.nshards > 1 ? l0 % per : 0;
+                const int nz = g.nshards > 1 ? min(8, g.chunk - w0) : 8;
+                const int gz0 = local_to_global_z(g, l0);
+                const int bx = c.xc >> 3, by = c.yc >> 3;
+                skip_box(g, cur, bx * 8, by * 8, gz0, 8, bx == 0, bx == g.nbx - 1, by == 0, by == g.nby - 1, gz0 == 0,
+                         gz0 + 8 >= g.dimz);
+                if (nz < 8) cur.hi[2] = (float)(gz0 + nz) - 0.01f;
+            }
+        }
+        if (cur.skip) return false;
+    }
+    *f = tri_eval(a.b.sdf, tri_from(g, c));
+    return true;
+}
+
+// Ray parameter a little before the ray's samples enter the next chunk this shard owns
+// (along the direction of travel), or false when none lies ahead.  Approximate (half a
+// voxel early): the caller jumps there with exact additions and tests ownership sample by
+// sample from then on.
+__device__ __forceinline__ bool next_owned_t(const ShardRayArgs& a, const RayGeo& r, float t, float* tend) {
+    const VolGeom& g = a.g;
+    if (r.dz == 0.0f) return false;
+    const float iz = ((fmaf(t, r.dz, r.oz)) - g.start[2]) * g.rvox[2];
+    const int zc = min(max((int)floorf(fminf(fmaxf(iz, -1.0f), (float)g.dimz)), 0), g.dimz - 1);
+    const int c = zc / g.chunk, n = g.nshards, nch = (g.dimz + g.chunk - 1) / g.chunk;
+    float zb;  // voxel coordinate of the boundary the samples cross into the owned chunk
+    if (r.dz > 0.0f) {
+        const int cn = c + ((g.shard - c % n + n) % n);
+        if (cn <= c || cn >= nch) return false;
+        zb = (float)(cn * g.chunk);
+    } else {
+        const int cp = c - ((c % n - g.shard + n) % n);
+        if (cp >= c || cp < 0) return false;
+        zb = (float)((cp + 1) * g.chunk);
+    }
+    const float tb = (fmaf(zb, g.voxel[2], g.start[2]) - r.oz) / r.dz;
+    *tend = tb - 0.5f * g.voxel[2] / fabsf(r.dz);
+    return true;
 }
 
 __global__ __launch_bounds__(256) void k_shard_ray_step(ShardRayArgs a) {
@@ -2362,6 +2468,7 @@ __global__ __launch_bounds__(256) void k_shard_ray_step(ShardRayArgs a) {
             bool dead = false;
             const float thr = skip_threshold(a.g);
             SkipCursor cur;
+            const RayVox rv = ray_vox(a.g, r.ox, r.oy, r.oz, r.dx, r.dy, r.dz);
             float f0;
             if (owns_at(a, r, t) && sample_at_skip(a, r, t, thr, cur, &f0)) {
                 if (!(f0 > 0.0f)) { rec = mk_rec(-1, 0); dead = true; }
@@ -2370,11 +2477,37 @@ __global__ __launch_bounds__(256) void k_shard_ray_step(ShardRayArgs a) {
                 if (!(t < r.t1)) {
                     rec = mk_rec(-1, 0);
                 } else {
-                    for (int k = 0; t < r.t1; ++k, t += vx) {
-                        if (!owns_at(a, r, t)) continue;
-                        float f;
-                        if (!sample_at_skip(a, r, t, thr, cur, &f)) continue;
-                        if (f < vx / 2.0f) { rec = mk_rec(k, __float_as_int(f)); break; }
+                    // the samples of the owned chunks only: runs of foreign samples are jumped
+                    // with exact additions (sample k is still t0 + vx added k times)
+                    int k = 0;
+                    while (t < r.t1) {
+                        if (cur.skip && in_skip_box(cur, rv, t)) {  // a skippable brick: no event inside
+                            skip_steps_n(t, vx, fminf(r.t1, skip_box_exit(cur, rv)), k);
+                            while (t < r.t1 && in_skip_box(cur, rv, t)) {
+                                t += vx;
+                                ++k;
+                            }
+                            continue;
+                        }
+                        if (owns_at(a, r, t)) {
+                            float f;
+                            if (sample_at_skip(a, r, t, thr, cur, &f) && f < vx / 2.0f) {
+                                rec = mk_rec(k, __float_as_int(f));
+                                break;
+                            }
+                            t += vx;
+                            ++k;
+                            continue;
+                        }
+                        float tend;
+                        if (!next_owned_t(a, r, t, &tend)) break;
+                        tend = fminf(tend, r.t1);
+                        if (t < tend) {
+                            skip_steps_n(t, vx, tend, k);
+                        } else {
+                            t += vx;
+                            ++k;
+                        }
                     }
                 }
             }
@@ -2397,13 +2530,38 @@ __global__ __launch_bounds__(256) void k_shard_ray_step(ShardRayArgs a) {
                 const float q = vx / 4.0f;
                 const float thr = skip_threshold(a.g);
                 SkipCursor cur;
-                for (int j = 1;; ++j) {
-                    t += q;
-                    if (!(t < r.t1)) break;
-                    if (!owns_at(a, r, t)) continue;
-                    float f;
-                    if (!sample_at_skip(a, r, t, thr, cur, &f)) continue;
-                    if (f < 0.0f) { rec = mk_rec(j, __float_as_int(f)); break; }
+                const RayVox rv = ray_vox(a.g, r.ox, r.oy, r.oz, r.dx, r.dy, r.dz);
+                int j = 0;  // sample j of the quarter-step march is t_k + q added j times
+                t += q;
+                ++j;
+                while (t < r.t1) {
+                    if (cur.skip && in_skip_box(cur, rv, t)) {
+                        skip_steps_n(t, q, fminf(r.t1, skip_box_exit(cur, rv)), j);
+                        while (t < r.t1 && in_skip_box(cur, rv, t)) {
+                            t += q;
+                            ++j;
+                        }
+                        continue;
+                    }
+                    if (owns_at(a, r, t)) {
+                        float f;
+                        if (sample_at_skip(a, r, t, thr, cur, &f) && f < 0.0f) {
+                            rec = mk_rec(j, __float_as_int(f));
+                            break;
+                        }
+                        t += q;
+                        ++j;
+                        continue;
+                    }
+                    float tend;
+                    if (!next_owned_t(a, r, t, &tend)) break;
+                    tend = fminf(tend, r.t1);
+                    if (t < tend) {
+                        skip_steps_n(t, q, tend, j);
+                    } else {
+                        t += q;
+                        ++j;
+                    }
                 }
             }
         }
