@@ -2391,9 +2391,12 @@ __device__ __forceinline__ float sample_at(const ShardRayArgs& a, const RayGeo& 
 }
 
 // false when the brick map proves the sample >= voxel/2 (see march_ray).  A skippable brick
-// whose 8 local planes lie in one chunk block (so they are 8 consecutive global planes) also
-// leaves its box, in global voxel coordinates, in the cursor: every sample inside it is >=
-// voxel/2 whoever owns it, so the march may step through it with exact additions.
+// also leaves a box in the cursor, in global voxel coordinates: its distance box ((2r-1)^3
+// bricks of the local distance map, or the brick alone without one) clipped in z to the
+// sample's chunk block and, inside it, to the base planes w < chunk (their +1 plane is stored:
+// the halo at most; local bricks across a block boundary are not global neighbours).  Every
+// sample inside the box is >= voxel/2 whoever owns it, so the march steps through it with
+// exact additions.
 __device__ __forceinline__ bool sample_at_skip(const ShardRayArgs& a, const RayGeo& r, float t, float thr,
                                                SkipCursor& cur, float* f) {
     const VolGeom& g = a.g;
@@ -2402,22 +2405,34 @@ __device__ __forceinline__ bool sample_at_skip(const ShardRayArgs& a, const RayG
         const int br = brick_of(g, c);
         if (br != cur.brick) {
             cur.brick = br;
-            cur.skip = a.b.bmin[br] >= thr;
+            int rad = 0;
+            if (SEMTSDF_BRICK_DIST && a.b.bdist) {
+                rad = a.b.bdist[br];
+                cur.skip = rad > 0;
+            } else {
+                cur.skip = a.b.bmin[br] >= thr;
+                rad = cur.skip ? 1 : 0;
+            }
             cur.lo[0] = 1e30f;  // no box unless set below
             cur.hi[0] = -1e30f;
-            const int per = g.nshards > 1 ? g.chunk + g.halo : INT_MAX;  // local planes per chunk block
-            const int l0 = (c.zl >> 3) << 3;
-            if (cur.skip && l0 / per == (l0 + 7) / per) {
-                // samples based on planes w < chunk of the block read planes this shard stores
-                // (w + 1 <= chunk: the halo at most); a base on the halo plane would read the
-                // next chunk's second plane, which the brick's minimum does not cover
-                const int w0 = g.nshards > 1 ? l0 % per : 0;
-                const int nz = g.nshards > 1 ? min(8, g.chunk - w0) : 8;
-                const int gz0 = local_to_global_z(g, l0);
-                const int bx = c.xc >> 3, by = c.yc >> 3;
-                skip_box(g, cur, bx * 8, by * 8, gz0, 8, bx == 0, bx == g.nbx - 1, by == 0, by == g.nby - 1, gz0 == 0,
-                         gz0 + 8 >= g.dimz);
-                if (nz < 8) cur.hi[2] = (float)(gz0 + nz) - 0.01f;
+            if (cur.skip) {
+                const int bx = c.xc >> 3, by = c.yc >> 3, bz = c.zl >> 3;
+                const int per = g.nshards > 1 ? g.chunk + g.halo : g.lz;  // local planes per chunk block
+                const int blk0 = g.nshards > 1 ? c.zl / per * per : 0;   // first local plane of the block
+                const int own = g.nshards > 1 ? g.chunk : g.lz;          // base planes w < own in the block
+                const int lz0 = max((bz - (rad - 1)) * 8, blk0), lz1 = min((bz + rad) * 8, blk0 + own);  // local, excl.
+                if (lz0 < lz1) {
+                    const int gz0 = local_to_global_z(g, blk0) + (lz0 - blk0);
+                    const int gz1 = gz0 + (lz1 - lz0);
+                    const int x0 = bx - (rad - 1), y0 = by - (rad - 1), x1 = bx + rad, y1 = by + rad;
+                    const float m = 0.01f;
+                    cur.lo[0] = x0 <= 0 ? -1e30f : (float)(x0 * 8) + m;
+                    cur.hi[0] = x1 >= g.nbx ? 1e30f : (float)(x1 * 8) - m;
+                    cur.lo[1] = y0 <= 0 ? -1e30f : (float)(y0 * 8) + m;
+                    cur.hi[1] = y1 >= g.nby ? 1e30f : (float)(y1 * 8) - m;
+                    cur.lo[2] = gz0 <= 0 ? -1e30f : (float)gz0 + m;
+                    cur.hi[2] = gz1 >= g.dimz ? 1e30f : (float)gz1 - m;
+                }
             }
         }
         if (cur.skip) return false;
@@ -2531,9 +2546,8 @@ __global__ __launch_bounds__(256) void k_shard_ray_step(ShardRayArgs a) {
                 const float thr = skip_threshold(a.g);
                 SkipCursor cur;
                 const RayVox rv = ray_vox(a.g, r.ox, r.oy, r.oz, r.dx, r.dy, r.dz);
-                int j = 0;  // sample j of the quarter-step march is t_k + q added j times
+                int j = 1;  // sample j of the quarter-step march is t_k + q added j times
                 t += q;
-                ++j;
                 while (t < r.t1) {
                     if (cur.skip && in_skip_box(cur, rv, t)) {
                         skip_steps_n(t, q, fminf(r.t1, skip_box_exit(cur, rv)), j);
