@@ -283,7 +283,11 @@ def timed_integrate(vol, step, K, warmup, pg=None, device=0, finish=None):
 # ----------------------------------------------------------------------------- C3 pipeline
 def run_pipeline(semtsdf, L, p, local, n_frames=100, n_warm=5):
     """§8d frames/s of C3: host pose path + async H2D (pinned, copy stream) + association
-    raycast + relabel + integrate + one live raycast view per frame."""
+    raycast + relabel + integrate + one live raycast view per frame, in the volume stream's
+    order (the reported rate).  "overlapped": the live view of frame k on a render stream
+    beside the association of frame k+1 (both only read the volume; frame k+1's integrate
+    waits for the view, semtsdf_parse_frame_dev_after) — measured slower: two latency-bound
+    marches sharing the CUs stretch each other's tails."""
     import torch
 
     from semtsdf import pose as P
@@ -300,11 +304,8 @@ def run_pipeline(semtsdf, L, p, local, n_frames=100, n_warm=5):
         with open(gt, "w") as f:
             f.write("\n".join(st.tum_lines(n_all)) + "\n")
         traj = tum.read_traj(gt)  # tsdf_utils.py:23-29
-    vol = semtsdf.Volume(p, local)
     dev = torch.device("cuda", local)
-    vstream = torch.cuda.ExternalStream(vol.stream, device=dev)
-    cstream = torch.cuda.Stream(device=dev)
-    # pinned host frames (a capture pipeline's DMA buffers) and a device ring of 2 slots
+    # pinned host frames (a capture pipeline's DMA buffers)
     h_d = torch.empty((n_all, NPX), dtype=torch.int16).pin_memory()
     h_r = torch.empty((n_all, NPX * 3), dtype=torch.uint8).pin_memory()
     h_m = torch.empty((n_all, NPX), dtype=torch.uint8).pin_memory()
@@ -312,54 +313,79 @@ def run_pipeline(semtsdf, L, p, local, n_frames=100, n_warm=5):
         h_d[k].copy_(torch.from_numpy(fr.depth.reshape(-1).view(np.int16)))
         h_r[k].copy_(torch.from_numpy(fr.rgb.reshape(-1)))
         h_m[k].copy_(torch.from_numpy(fr.mask.reshape(-1)))
-    ring = 2
-    d_d = torch.empty((ring, NPX), dtype=torch.int16, device=dev)
-    d_r = torch.empty((ring, NPX * 3), dtype=torch.uint8, device=dev)
-    d_m = torch.empty((ring, NPX), dtype=torch.uint8, device=dev)
-    out = torch.empty(NPX * 3, dtype=torch.uint8, device=dev)
-    copied = [torch.cuda.Event() for _ in range(ring)]
-    used = [torch.cuda.Event() for _ in range(ring)]
     mean_m = tum.mean_depth_m(frames[0].depth)
     ext0_inv = np.linalg.inv(P.parse_pos(traj[0, 1:]))  # frame 0 places the volume (tsdf.cu:173-214)
-    torch.cuda.synchronize()
 
-    def upload(k):
-        s = k % ring
-        with torch.cuda.stream(cstream):
-            cstream.wait_event(used[s])
-            d_d[s].copy_(h_d[k], non_blocking=True)
-            d_r[s].copy_(h_r[k], non_blocking=True)
-            d_m[s].copy_(h_m[k], non_blocking=True)
-            copied[s].record(cstream)
+    def run(overlap):
+        vol = semtsdf.Volume(p, local)
+        vstream = torch.cuda.ExternalStream(vol.stream, device=dev)
+        cstream = torch.cuda.Stream(device=dev)
+        rstream = torch.cuda.Stream(device=dev) if overlap else vstream
+        ring = 2
+        d_d = torch.empty((ring, NPX), dtype=torch.int16, device=dev)
+        d_r = torch.empty((ring, NPX * 3), dtype=torch.uint8, device=dev)
+        d_m = torch.empty((ring, NPX), dtype=torch.uint8, device=dev)
+        outs = [torch.empty(NPX * 3, dtype=torch.uint8, device=dev) for _ in range(2)]
+        copied = [torch.cuda.Event() for _ in range(ring)]
+        used = [torch.cuda.Event() for _ in range(ring)]
+        integrated = torch.cuda.Event()
+        rendered = torch.cuda.Event()
+        torch.cuda.synchronize()
 
-    def frame(k):
-        s = k % ring
-        E = P.relative_pose(P.parse_pos(traj[k, 1:]), ext0_inv)  # host pose path (tsdf.cu:217)
-        vstream.wait_event(copied[s])
-        vol.parse_frame_dev(d_d[s].data_ptr(), d_r[s].data_ptr(), d_m[s].data_ptr(), E)
-        s2w, c = semtsdf.orbit_camera(list(p.Kinv), 0.01 * k, mean_m)
-        vol.raycast_dev(s2w, c, L.RENDER_LABEL, out.data_ptr())
-        used[s].record(vstream)
-        if k + ring < n_all:
-            upload(k + ring)
+        def upload(k):
+            s = k % ring
+            with torch.cuda.stream(cstream):
+                cstream.wait_event(used[s])
+                d_d[s].copy_(h_d[k], non_blocking=True)
+                d_r[s].copy_(h_r[k], non_blocking=True)
+                d_m[s].copy_(h_m[k], non_blocking=True)
+                copied[s].record(cstream)
 
-    for k in range(ring):
-        upload(1 + k)
-    for k in range(1, 1 + n_warm):
-        frame(k)
-    vol.sync()
-    torch.cuda.synchronize()
-    vol.reset_timing()
-    vol.set_instrumentation(events=True, count=False)
-    t0 = time.perf_counter()
-    for k in range(1 + n_warm, n_all):
-        frame(k)
-    vol.sync()
-    t1 = time.perf_counter()
-    tm = vol.timing()
-    vol.set_instrumentation(events=False, count=False)
+        def frame(k, first):
+            s = k % ring
+            E = P.relative_pose(P.parse_pos(traj[k, 1:]), ext0_inv)  # host pose path (tsdf.cu:217)
+            vstream.wait_event(copied[s])
+            after = rendered.cuda_event if (overlap and not first) else None
+            vol.parse_frame_dev(d_d[s].data_ptr(), d_r[s].data_ptr(), d_m[s].data_ptr(), E,
+                                integrate_after_event=after)
+            used[s].record(vstream)
+            s2w, c = semtsdf.orbit_camera(list(p.Kinv), 0.01 * k, mean_m)
+            if overlap:
+                integrated.record(vstream)
+                rstream.wait_event(integrated)
+            vol.raycast_dev(s2w, c, L.RENDER_LABEL, outs[k % 2].data_ptr(), stream=rstream.cuda_stream)
+            if overlap:
+                rendered.record(rstream)
+            if k + ring < n_all:
+                upload(k + ring)
+
+        for k in range(ring):
+            upload(1 + k)
+        for k in range(1, 1 + n_warm):
+            frame(k, k == 1)
+        vol.sync()
+        torch.cuda.synchronize()
+        vol.reset_timing()
+        vol.set_instrumentation(events=True, count=False)
+        t0 = time.perf_counter()
+        for k in range(1 + n_warm, n_all):
+            frame(k, False)
+        vol.sync()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        tm = vol.timing()
+        vol.set_instrumentation(events=False, count=False)
+        return vol, t1 - t0, tm, outs[(n_all - 1) % 2]
+
+    vol_s, t_ser, tm, img_s = run(False)
+    ref_img = img_s.cpu()
+    objs_s = int(vol_s.state().num_objs)
+    vol_s.close()
+    vol, t_ovl, _, img_o = run(True)
+    same = bool(torch.equal(img_o.cpu(), ref_img)) and int(vol.state().num_objs) == objs_s
     st_ = vol.state()
     # live orbit (kernel.cpp:101-107): angle += 0.01 per view, distance = mean depth
+    out = torch.empty(NPX * 3, dtype=torch.uint8, device=dev)
     n_views = 60
     vol.reset_timing()
     vol.set_instrumentation(events=True, count=False)
@@ -373,8 +399,10 @@ def run_pipeline(semtsdf, L, p, local, n_frames=100, n_warm=5):
     vol.set_instrumentation(events=False, count=False)
     vol.close()
     return {
-        "frames_per_s": n_frames / (t1 - t0),
-        "ms_per_frame": (t1 - t0) * 1e3 / n_frames,
+        "frames_per_s": n_frames / t_ser,
+        "ms_per_frame": t_ser * 1e3 / n_frames,
+        "overlapped_frames_per_s": n_frames / t_ovl,
+        "overlapped_equals_serial": same,
         "frames": n_frames, "warmup_frames": n_warm,
         "per_frame": "host TUM pose (read_traj -> parse_pos) + async pinned H2D of depth/RGB/mask on a copy stream "
                      "+ association raycast + relabel + integrate + 1 label raycast view",

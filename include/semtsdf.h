@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SEMTSDF_ABI_VERSION 4
+#define SEMTSDF_ABI_VERSION 5
 #define SEMTSDF_MAX_OBJECTS 32 /* tsdf.cuh:4 */
 
 /* ---- status codes ------------------------------------------------------------ */
@@ -176,6 +176,11 @@ int semtsdf_parse_frame(semtsdf_vol* v, const uint16_t* depth, const uint8_t* rg
                         uint8_t* mask_inout, const float E[16], semtsdf_assoc_stats* stats, void* stream);
 int semtsdf_parse_frame_dev(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d,
                             uint8_t* mask_d, const float E[16], void* stream);
+/* parse_frame_dev whose integrate (the frame's only write of the volume) first waits for
+ * `integrate_after_event` (a hipEvent_t, or NULL), e.g. the end of the previous frame's live
+ * render on another stream; the association, which only reads the volume, may overlap it. */
+int semtsdf_parse_frame_dev_after(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d,
+                                  uint8_t* mask_d, const float E[16], void* integrate_after_event, void* stream);
 
 /* ---- raycast render (a8: Viewer::show_tsdf viewer.cu:137-179) -------------------------
  * Orbit camera helper: s2w = rot(angle, dist) * Kinv, c = ((dist+0.5) sin, 0, (dist+0.5)(1-cos)). */

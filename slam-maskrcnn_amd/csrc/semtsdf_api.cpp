@@ -100,6 +100,8 @@ struct semtsdf_vol {
     uint32_t n_obs = 0;
     bool bmin_dirty = false;       // integrated since the last map update: update marked bricks
     bool bmin_stale = true;        // reset/upload: rebuild the whole map
+    hipEvent_t bmin_ev = nullptr;  // recorded after the last map update, on the stream that ran it
+    bool bmin_ev_set = false;
     // instrumentation
     int instr = 0;
     std::vector<EventPair> ev_integrate, ev_assoc, ev_render, ev_prep;
@@ -133,10 +135,12 @@ void free_all(semtsdf_vol* v) {
     if (v->decision_h) (void)hipHostFree(v->decision_h);
     for (auto* vec : {&v->ev_integrate, &v->ev_assoc, &v->ev_render, &v->ev_prep})
         for (auto& e : *vec) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
+    if (v->bmin_ev) (void)hipEventDestroy(v->bmin_ev);
     if (v->stream) (void)hipStreamDestroy(v->stream);
 }
 
 int local_planes(const semtsdf_params* p, int* chunk, int* halo);
+int after_bmin(semtsdf_vol* v, hipStream_t s);
 
 int check_params(const semtsdf_params* p) {
     if (!p) return fail(SEMTSDF_ERR_INVALID, "params is NULL");
@@ -289,6 +293,7 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
                     ? 1
                     : 0;
     if (a.debug == 2) return SEMTSDF_OK;
+    if (int rc = after_bmin(v, s)) return rc;
     EventPair epp;
     timing_begin(v, v->ev_prep, s, &epp);
     HIPC(launch_depth_pyramid(depth_d, rgb_d, mask_d, v->p.width, v->p.height, v->p.depth_scale, v->pyr,
@@ -327,13 +332,31 @@ MarchCamera assoc_camera(const semtsdf_vol* v, const float E[16]) {
     return c;
 }
 
-// Rebuild the empty-space map after the volume changed (integrate, upload, reset).
+// Rebuild the empty-space map after the volume changed (integrate, upload, reset).  The
+// update runs on the stream of the first march that needs it; marches on other streams (a
+// render overlapping the next frame's association) and the next writer of the volume wait
+// for it through bmin_ev.
 int ensure_bmin(semtsdf_vol* v, hipStream_t s) {
-    if (!v->bmin_dirty && !v->bmin_stale) return SEMTSDF_OK;
+    if (!v->bmin_dirty && !v->bmin_stale) {
+        if (v->bmin_ev_set) HIPC(hipStreamWaitEvent(s, v->bmin_ev, 0));
+        return SEMTSDF_OK;
+    }
     // stale (reset/upload): every brick; dirty (integrate): the bricks the cull marked
+    if (v->bmin_ev_set) HIPC(hipStreamWaitEvent(s, v->bmin_ev, 0));
     HIPC(launch_brick_min(v->g, v->b, v->bmin_stale, s));
+    if (!v->bmin_ev && hipEventCreateWithFlags(&v->bmin_ev, hipEventDisableTiming) != hipSuccess) v->bmin_ev = nullptr;
+    if (v->bmin_ev) {
+        HIPC(hipEventRecord(v->bmin_ev, s));
+        v->bmin_ev_set = true;
+    }
     v->bmin_dirty = false;
     v->bmin_stale = false;
+    return SEMTSDF_OK;
+}
+
+// A writer of the volume (integrate, upload, reset) orders itself after the last map update.
+int after_bmin(semtsdf_vol* v, hipStream_t s) {
+    if (v->bmin_ev_set) HIPC(hipStreamWaitEvent(s, v->bmin_ev, 0));
     return SEMTSDF_OK;
 }
 
@@ -728,6 +751,7 @@ int semtsdf_reset(semtsdf_vol* v, void* stream) {
     HIPC(hipSetDevice(v->device));
     hipStream_t s = pick(v, stream);
     const size_t n = v->g.nvox;
+    if (int rc = after_bmin(v, s)) return rc;
     HIPC(launch_fill_volume(v->g, v->b, v->p.flags, s));
     HIPC(hipMemsetAsync(v->b.wt, 0, n * 4, s));
     HIPC(hipMemsetAsync(v->b.sflag, 0, n / 32 + 1, s));  // steady flags: unknown
@@ -897,6 +921,11 @@ int semtsdf_parse_frame(semtsdf_vol* v, const uint16_t* depth, const uint8_t* rg
 
 int semtsdf_parse_frame_dev(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d, uint8_t* mask_d,
                             const float E[16], void* stream) {
+    return semtsdf_parse_frame_dev_after(v, depth_d, rgb_d, mask_d, E, nullptr, stream);
+}
+
+int semtsdf_parse_frame_dev_after(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d, uint8_t* mask_d,
+                                  const float E[16], void* integrate_after_event, void* stream) {
     if (!v || !E) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
     hipStream_t s = pick(v, stream);
     const bool sem = v->p.flags & SEMTSDF_F_SEMANTIC;
@@ -912,6 +941,9 @@ int semtsdf_parse_frame_dev(semtsdf_vol* v, const uint16_t* depth_d, const uint8
             HIPC(launch_first_frame_objs(v->tables_d, v->num_objs_d, s));
         }
     }
+    // the integrate is the frame's only write of the volume: readers of the previous state on
+    // other streams (a live render) finish first; the association above, a read, may overlap them
+    if (integrate_after_event) HIPC(hipStreamWaitEvent(s, (hipEvent_t)integrate_after_event, 0));
     int rc = integrate_impl(v, depth_d, rgb_d, sem ? mask_d : nullptr, nullptr, E, s);
     if (rc) return rc;
     v->n_obs++;
@@ -1348,6 +1380,7 @@ int semtsdf_upload(semtsdf_vol* v, const float* sdf, const int32_t* wt, const vo
     HIPC(hipSetDevice(v->device));
     hipStream_t s = v->stream;
     int rc;
+    if ((rc = after_bmin(v, s))) return rc;
     // derived maps first: a transfer that fails half-way must not leave steady flags or an
     // empty-space map that describe the old contents (0 = unknown is always safe)
     v->bmin_stale = true;

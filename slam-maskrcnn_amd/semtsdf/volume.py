@@ -182,10 +182,15 @@ class Volume:
         L.check(L.load().semtsdf_integrate_vote_dev(self._h, C.c_void_p(depth_ptr), C.c_void_p(rgb_ptr),
                                                     C.c_void_p(cls_ptr), L.ptr(e), stream))
 
-    def parse_frame_dev(self, depth_ptr: int, rgb_ptr: int, mask_ptr: int | None, E, stream=None):
+    def parse_frame_dev(self, depth_ptr: int, rgb_ptr: int, mask_ptr: int | None, E, stream=None,
+                        integrate_after_event: int | None = None):
+        """integrate_after_event: a raw hipEvent_t (e.g. torch.cuda.Event.cuda_event) the
+        frame's integrate waits for (readers of the previous state on other streams)."""
         e = L.f32(E, 16)
-        L.check(L.load().semtsdf_parse_frame_dev(self._h, C.c_void_p(depth_ptr), C.c_void_p(rgb_ptr),
-                                                 C.c_void_p(mask_ptr) if mask_ptr else None, L.ptr(e), stream))
+        L.check(L.load().semtsdf_parse_frame_dev_after(self._h, C.c_void_p(depth_ptr), C.c_void_p(rgb_ptr),
+                                                       C.c_void_p(mask_ptr) if mask_ptr else None, L.ptr(e),
+                                                       C.c_void_p(integrate_after_event) if integrate_after_event
+                                                       else None, stream))
 
     def associate_dev(self, mask_ptr: int, E, stream=None, want_stats=False):
         e = L.f32(E, 16)
