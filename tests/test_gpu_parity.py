@@ -691,3 +691,61 @@ def test_full_free_units_hole_free_frames(S, oracle, stream):
     assert tm.full_units > 1000 and tm.free_units >= tm.full_units
     assert_same(vol, ost, hist=True)
     vol.close()
+
+
+def test_render_stream_beside_association_equals_serial(S, stream):
+    """A live view on its own stream beside the next frame's association (both only read the
+    volume; the brick-map update is ordered across streams by the library, the integrate waits
+    for the view through parse_frame_dev_after) gives the same views, labels and volume as the
+    serial order."""
+    import torch
+
+    semtsdf, L = S
+    st, frames = stream
+    dev = torch.device("cuda", 0)
+    npx = 640 * 480
+    d_in = [torch.from_numpy(fr.depth.reshape(-1).view(np.int16)).to(dev) for fr in frames]
+    r_in = [torch.from_numpy(fr.rgb.reshape(-1)).to(dev) for fr in frames]
+    m_in = [torch.from_numpy(np.ascontiguousarray(fr.mask).reshape(-1)).to(dev) for fr in frames]
+    torch.cuda.synchronize()
+
+    def run(overlap):
+        p = semtsdf.default_params(96, KI, 640, 480)
+        semtsdf.place_from_frame(p, frames[0].depth, float(np.mean(frames[0].depth[frames[0].depth > 0])) / 5000.0,
+                                 L.PLACE_SFM)
+        p.flags = L.F_SEMANTIC | L.F_GATE_COLOR
+        vol = semtsdf.Volume(p, 0)
+        vs = torch.cuda.ExternalStream(vol.stream, device=dev)
+        rs = torch.cuda.Stream(device=dev) if overlap else vs
+        done, integrated = torch.cuda.Event(), torch.cuda.Event()
+        masks = [m.clone() for m in m_in]
+        torch.cuda.synchronize()
+        views = []
+        for k in range(1, len(frames)):
+            fr = frames[k]
+            E = (fr.w2c @ frames[0].c2w).astype(np.float32)
+            vol.parse_frame_dev(d_in[k].data_ptr(), r_in[k].data_ptr(), masks[k].data_ptr(), E,
+                                integrate_after_event=done.cuda_event if (overlap and k > 1) else None)
+            if overlap:
+                integrated.record(vs)
+                rs.wait_event(integrated)
+            out = torch.zeros(npx * 3, dtype=torch.uint8, device=dev)
+            s2w, c = semtsdf.orbit_camera(list(p.Kinv), 0.05 * k, 1.5)
+            vol.raycast_dev(s2w, c, L.RENDER_LABEL, out.data_ptr(), stream=rs.cuda_stream)
+            if overlap:
+                done.record(rs)
+            views.append(out)
+        vol.sync()
+        torch.cuda.synchronize()
+        state = vol.download(hist=True)
+        res = [v.cpu() for v in views], [m.cpu() for m in masks]
+        vol.close()
+        return res, state
+
+    (va, ma), sa = run(False)
+    (vb, mb), sb = run(True)
+    assert any(int(v.count_nonzero()) > 0 for v in va)
+    for x, y in zip(va + ma, vb + mb):
+        assert torch.equal(x, y)
+    for key in ("sdf", "wt", "color", "hist"):
+        assert np.array_equal(sa[key], sb[key]), key
