@@ -126,7 +126,7 @@ int dev_alloc(semtsdf_vol* v, void** p, size_t bytes) {
 }
 
 void free_all(semtsdf_vol* v) {
-    void* ptrs[] = {v->b.sdf, v->b.wt, v->b.bmin, v->b.bplain, v->b.sbmin, v->b.bdist, v->b.bdtmp, v->b.bdirty, v->b.sflag, v->b.color, v->b.hist, v->b.hmask, v->b.cls, v->b.cls_cnt, v->depth_d, v->rgb_d,
+    void* ptrs[] = {v->b.sdf, v->b.wt, v->b.bmin, v->b.bplain, v->b.sbmin, v->b.bdist, v->b.boct, v->b.botmp, v->b.bdirty, v->b.sflag, v->b.color, v->b.hist, v->b.hmask, v->b.cls, v->b.cls_cnt, v->depth_d, v->rgb_d,
                     v->mask_d, v->cls_d, v->pyr.px, v->pyr.l0, v->pyr.l1, v->tables_d, v->decision_d,
                     v->num_objs_d, v->probs_d, v->box_d, v->palette_d, v->render_d, v->render_t_d,
                     v->counters_d, v->ray_state_d, v->unit_list_d, v->list_count_d, v->rcp_table_d};
@@ -657,7 +657,8 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     if ((rc = dev_alloc(v, (void**)&v->b.bplain, nbricks * 4))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->b.sbmin, (size_t)g.nsx * g.nsy * g.nsz * 4))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->b.bdist, nbricks))) return bail(rc);
-    if ((rc = dev_alloc(v, (void**)&v->b.bdtmp, nbricks))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&v->b.boct, nbricks * 8))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&v->b.botmp, nbricks * 8))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->b.bdirty, nbricks))) return bail(rc);
     if (nbricks && hipMemset(v->b.bdirty, 0, nbricks) != hipSuccess) return bail(fail(SEMTSDF_ERR_HIP, "memset failed"));
     if ((rc = dev_alloc(v, &v->b.color, g.nvox * 4 * (ci32 ? 4 : 1)))) return bail(rc);

@@ -69,7 +69,10 @@ struct VolBufs {
     float* sbmin;      // per 64^3 super-brick (8^3 bricks): min of bmin over its bricks
     uint8_t* bdist;    // per 8^3 brick: L-inf distance in bricks to the nearest non-skippable
                        // brick (0: not skippable), capped at kBrickDistCap
-    uint8_t* bdtmp;    // scratch of the distance passes
+    uint64_t* boct;    // per 8^3 brick, byte o: the same distance within octant o only (bit a of o
+                       // set: negative along axis a), so a ray heading into octant o may step
+                       // through the box reaching that many bricks ahead of it (bdist = the min)
+    uint64_t* botmp;   // scratch of the distance passes
     uint8_t* bdirty;   // per 8^3 brick: overlaps a unit integrated since the last map update
     uint8_t* sflag;    // per 128-B sdf line (32 voxels): 1 = every sdf is 1.0f and every weight
                        // < 2^23 (k_integrate skips the sdf traffic of such lines); 0 = unknown

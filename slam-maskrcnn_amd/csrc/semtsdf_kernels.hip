@@ -230,9 +230,12 @@ __device__ __forceinline__ float skip_threshold(const VolGeom& g);
 #ifndef SEMTSDF_BRICK_DIST
 #define SEMTSDF_BRICK_DIST 1
 #endif
+#ifndef SEMTSDF_BRICK_OCT
+#define SEMTSDF_BRICK_OCT 1  // unsharded marches use the octant boxes of their direction
+#endif
 
 __global__ __launch_bounds__(256) void k_brick_dilate(VolGeom g, const float* __restrict__ plain, float* __restrict__ bmin,
-                                                      uint8_t* __restrict__ d0) {
+                                                      uint64_t* __restrict__ d0) {
     const unsigned nb = (unsigned)g.nbx * g.nby * g.nbz;
     const unsigned br = blockIdx.x * blockDim.x + threadIdx.x;
     if (br >= nb) return;
@@ -245,15 +248,19 @@ __global__ __launch_bounds__(256) void k_brick_dilate(VolGeom g, const float* __
                 if (xx < g.nbx && yy < g.nby && zz < g.nbz) m = fminf(m, plain[((unsigned)xx * g.nby + yy) * g.nbz + zz]);
             }
     bmin[br] = m;
-    if (d0) d0[br] = m >= skip_threshold(g) ? (uint8_t)kBrickDistCap : (uint8_t)0;
+    if (d0) d0[br] = m >= skip_threshold(g) ? (uint64_t)kBrickDistCap * 0x0101010101010101ull : 0ull;
 }
 
-// Brick distance map, one axis per pass: out[b] = min over |k| < cap of max(|k|, in[b + k e])
-// (neighbours inside the volume).  Three passes (x, y, z) from d0 (0 = not skippable, cap =
-// skippable) give the L-inf distance to the nearest non-skippable brick, capped: every brick
-// closer than d[b] to b is skippable, so the march may step through that whole box.
-__global__ __launch_bounds__(256) void k_brick_dist_axis(VolGeom g, const uint8_t* __restrict__ in,
-                                                         uint8_t* __restrict__ out, int axis) {
+// Octant brick distance maps, one axis per pass: for octant o (bit a set: negative along axis
+// a) out_o[b] = min over 0 <= k < cap of max(k, in_o[b + s k e]), s the octant's sign on this
+// axis (neighbours inside the volume).  Three passes (x, y, z) from d0 (0 = not skippable, cap
+// = skippable, in every byte) give, per octant, the L-inf distance to the nearest non-skippable
+// brick of that octant, capped: the box of the d bricks from b on along each of the octant's
+// directions is skippable.  The last pass also writes the symmetric distance (the min over
+// the octants: every brick lies in some octant of b) for the sharded march.
+__global__ __launch_bounds__(256) void k_brick_oct_axis(VolGeom g, const uint64_t* __restrict__ in,
+                                                        uint64_t* __restrict__ out, uint8_t* __restrict__ sym,
+                                                        int axis) {
     const unsigned nb = (unsigned)g.nbx * g.nby * g.nbz;
     const unsigned br = blockIdx.x * blockDim.x + threadIdx.x;
     if (br >= nb) return;
@@ -261,12 +268,34 @@ __global__ __launch_bounds__(256) void k_brick_dist_axis(VolGeom g, const uint8_
     const int pos = axis == 0 ? bx : axis == 1 ? by : bz;
     const int n = axis == 0 ? g.nbx : axis == 1 ? g.nby : g.nbz;
     const int stride = axis == 0 ? g.nby * g.nbz : axis == 1 ? g.nbz : 1;
-    int d = in[br];
-    for (int k = 1; k < kBrickDistCap && k < d; ++k) {
-        if (pos - k >= 0) d = min(d, max(k, (int)in[(int)br - k * stride]));
-        if (pos + k < n) d = min(d, max(k, (int)in[(int)br + k * stride]));
+    const uint64_t v = in[br];
+    int d[8];
+    int dmax = 0;
+#pragma unroll
+    for (int o = 0; o < 8; ++o) {
+        d[o] = (int)((v >> (8 * o)) & 0xFFu);
+        dmax = max(dmax, d[o]);
     }
-    out[br] = (uint8_t)d;
+    for (int k = 1; k < kBrickDistCap && k < dmax; ++k) {
+        const uint64_t wp = pos + k < n ? in[(int)br + k * stride] : ~0ull;   // octants positive on axis
+        const uint64_t wn = pos - k >= 0 ? in[(int)br - k * stride] : ~0ull;  // octants negative on axis
+        dmax = 0;
+#pragma unroll
+        for (int o = 0; o < 8; ++o) {
+            const uint64_t w = ((o >> axis) & 1) ? wn : wp;
+            d[o] = min(d[o], max(k, (int)((w >> (8 * o)) & 0xFFu)));
+            dmax = max(dmax, d[o]);
+        }
+    }
+    uint64_t r = 0;
+    int dmin = kBrickDistCap;
+#pragma unroll
+    for (int o = 0; o < 8; ++o) {
+        r |= (uint64_t)d[o] << (8 * o);
+        dmin = min(dmin, d[o]);
+    }
+    out[br] = r;
+    if (sym) sym[br] = (uint8_t)dmin;
 }
 
 // Super-brick level: sbmin[s] = min of bmin over the (up to) 8^3 bricks of super-brick s,
@@ -291,13 +320,13 @@ hipError_t launch_brick_min(const VolGeom& g, const VolBufs& b, bool all, hipStr
     if (nb == 0) return hipSuccess;
     const unsigned nq = (unsigned)g.nbx * g.nby * (unsigned)((g.nbz + 3) / 4);
     hipLaunchKernelGGL(k_brick_plain, dim3((nq + 3) / 4), dim3(256), 0, s, g, b.sdf, b.bplain, b.bdirty, all ? 1 : 0);
-    const bool dist = SEMTSDF_BRICK_DIST && b.bdist && b.bdtmp;
+    const bool dist = SEMTSDF_BRICK_DIST && b.bdist && b.boct && b.botmp;
     hipLaunchKernelGGL(k_brick_dilate, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.bplain, b.bmin,
-                       dist ? b.bdtmp : nullptr);
-    if (dist) {  // d0 in bdtmp -> x -> bdist -> y -> bdtmp -> z -> bdist
-        hipLaunchKernelGGL(k_brick_dist_axis, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.bdtmp, b.bdist, 0);
-        hipLaunchKernelGGL(k_brick_dist_axis, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.bdist, b.bdtmp, 1);
-        hipLaunchKernelGGL(k_brick_dist_axis, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.bdtmp, b.bdist, 2);
+                       dist ? b.botmp : nullptr);
+    if (dist) {  // d0 in botmp -> x -> boct -> y -> botmp -> z -> boct (+ bdist)
+        hipLaunchKernelGGL(k_brick_oct_axis, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.botmp, b.boct, nullptr, 0);
+        hipLaunchKernelGGL(k_brick_oct_axis, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.boct, b.botmp, nullptr, 1);
+        hipLaunchKernelGGL(k_brick_oct_axis, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.botmp, b.boct, b.bdist, 2);
     } else {
         const unsigned ns = (unsigned)g.nsx * g.nsy * g.nsz;
         if (b.sbmin && ns) hipLaunchKernelGGL(k_brick_super, dim3((ns + 3) / 4), dim3(256), 0, s, g, b.bmin, b.sbmin);
@@ -1689,20 +1718,24 @@ __device__ __forceinline__ void skip_box(const VolGeom& g, SkipCursor& cur, int 
 }
 
 __device__ __forceinline__ bool sample_or_skip(const VolGeom& g, const VolBufs& b, float thr, SkipCursor& cur,
-                                               float px, float py, float pz, float* f, bool box = false) {
+                                               float px, float py, float pz, float* f, bool box = false,
+                                               int oct = -1) {
     const TriCoord c = tri_coord(g, px, py, pz);
     if (SEMTSDF_BRICK_DIST && box && b.bdist) {
-        // the brick's distance r to the nearest non-skippable brick: the (2r-1)^3 bricks
-        // around it are skippable, one box for the march to step through
+        // the brick's distance r to the nearest non-skippable brick of the ray's octant: the
+        // r^3 bricks from it on towards the ray's direction are skippable, one box for the
+        // march to step through (without an octant: the (2r-1)^3 bricks around it)
         const int br = brick_of(g, c);
         if (br != cur.brick) {
             cur.brick = br;
-            const int r = b.bdist[br];
+            const int r = oct >= 0 ? (int)reinterpret_cast<const uint8_t*>(b.boct)[(size_t)br * 8 + oct] : b.bdist[br];
             cur.skip = r > 0;
             if (cur.skip) {
                 const int bx = c.xc >> 3, by = c.yc >> 3, bz = c.zl >> 3;
-                const int x0 = bx - (r - 1), y0 = by - (r - 1), z0 = bz - (r - 1);
-                const int x1 = bx + r, y1 = by + r, z1 = bz + r;  // exclusive
+                const int nx = oct < 0 || (oct & 1), ny = oct < 0 || (oct & 2), nz = oct < 0 || (oct & 4);
+                const int px_ = oct < 0 || !(oct & 1), py_ = oct < 0 || !(oct & 2), pz_ = oct < 0 || !(oct & 4);
+                const int x0 = bx - (nx ? r - 1 : 0), y0 = by - (ny ? r - 1 : 0), z0 = bz - (nz ? r - 1 : 0);
+                const int x1 = bx + (px_ ? r : 1), y1 = by + (py_ ? r : 1), z1 = bz + (pz_ ? r : 1);  // exclusive
                 const float m = 0.01f;
                 cur.lo[0] = x0 <= 0 ? -1e30f : (float)(x0 * 8) + m;
                 cur.hi[0] = x1 >= g.nbx ? 1e30f : (float)(x1 * 8) - m;
@@ -1770,12 +1803,13 @@ __device__ bool march_ray(const VolGeom& g, const VolBufs& b, float ox, float oy
     SkipCursor cur;
     const RayVox rv = ray_vox(g, ox, oy, oz, dx, dy, dz);
     const bool box = g.nshards == 1 && b.bmin;  // local z == global z only unsharded
+    const int oct = SEMTSDF_BRICK_OCT && b.boct ? (dx < 0.0f ? 1 : 0) | (dy < 0.0f ? 2 : 0) | (dz < 0.0f ? 4 : 0) : -1;
     float f_t = 1.0f, f_tt = 0.0f;
     bool prev_skipped = false;  // f_t not evaluated: re-evaluate it at t_prev if needed
     float t_prev = t;
     {
         float f;
-        if (sample_or_skip(g, b, thr, cur, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz), &f, box)) {
+        if (sample_or_skip(g, b, thr, cur, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz), &f, box, oct)) {
             if (!(f > 0.0f)) return false;
             f_t = f;
         } else {
@@ -1805,7 +1839,7 @@ __device__ bool march_ray(const VolGeom& g, const VolBufs& b, float ox, float oy
         float f;
         const int brick_before = cur.brick;
         const bool evaluated =
-            sample_or_skip(g, b, thr, cur, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz), &f, box);
+            sample_or_skip(g, b, thr, cur, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz), &f, box, oct);
         if (st) {
             st->lookups += cur.brick != brick_before;
             st->evals += evaluated;
