@@ -12,7 +12,7 @@ constexpr int kMaxDetections = 256;  // detections per frame accepted by semtsdf
 constexpr int kRcpTable = 1024;  // RN(1/n) table of the running means (w + 1 <= kRcpTable)
 constexpr int kZAlign = 32;      // stored z planes per x,y column: a multiple of the unit z-extent
 #ifndef SEMTSDF_BRICK_DIST_CAP
-#define SEMTSDF_BRICK_DIST_CAP 8
+#define SEMTSDF_BRICK_DIST_CAP 16
 #endif
 constexpr int kBrickDistCap = SEMTSDF_BRICK_DIST_CAP;  // brick distance map: radius of the largest skip box (bricks)
 constexpr int kListSegs = 64;    // segments (and counters) of the live-unit list
