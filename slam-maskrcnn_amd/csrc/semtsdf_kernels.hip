@@ -2440,8 +2440,11 @@ __device__ __forceinline__ bool sample_at_skip(const ShardRayArgs& a, const RayG
         if (br != cur.brick) {
             cur.brick = br;
             int rad = 0;
+            const int oct = SEMTSDF_BRICK_DIST && SEMTSDF_BRICK_OCT && a.b.boct
+                                ? (r.dx < 0.0f ? 1 : 0) | (r.dy < 0.0f ? 2 : 0) | (r.dz < 0.0f ? 4 : 0)
+                                : -1;
             if (SEMTSDF_BRICK_DIST && a.b.bdist) {
-                rad = a.b.bdist[br];
+                rad = oct >= 0 ? (int)reinterpret_cast<const uint8_t*>(a.b.boct)[(size_t)br * 8 + oct] : a.b.bdist[br];
                 cur.skip = rad > 0;
             } else {
                 cur.skip = a.b.bmin[br] >= thr;
@@ -2454,11 +2457,17 @@ __device__ __forceinline__ bool sample_at_skip(const ShardRayArgs& a, const RayG
                 const int per = g.nshards > 1 ? g.chunk + g.halo : g.lz;  // local planes per chunk block
                 const int blk0 = g.nshards > 1 ? c.zl / per * per : 0;   // first local plane of the block
                 const int own = g.nshards > 1 ? g.chunk : g.lz;          // base planes w < own in the block
-                const int lz0 = max((bz - (rad - 1)) * 8, blk0), lz1 = min((bz + rad) * 8, blk0 + own);  // local, excl.
+                // the box: rad bricks along each axis on the ray's side (both sides without an
+                // octant map or with the brick alone)
+                const bool sym = oct < 0;
+                const int nx = sym || (oct & 1) ? rad - 1 : 0, px_ = sym || !(oct & 1) ? rad : 1;
+                const int ny = sym || (oct & 2) ? rad - 1 : 0, py_ = sym || !(oct & 2) ? rad : 1;
+                const int nz = sym || (oct & 4) ? rad - 1 : 0, pz_ = sym || !(oct & 4) ? rad : 1;
+                const int lz0 = max((bz - nz) * 8, blk0), lz1 = min((bz + pz_) * 8, blk0 + own);  // local, excl.
                 if (lz0 < lz1) {
                     const int gz0 = local_to_global_z(g, blk0) + (lz0 - blk0);
                     const int gz1 = gz0 + (lz1 - lz0);
-                    const int x0 = bx - (rad - 1), y0 = by - (rad - 1), x1 = bx + rad, y1 = by + rad;
+                    const int x0 = bx - nx, y0 = by - ny, x1 = bx + px_, y1 = by + py_;
                     const float m = 0.01f;
                     cur.lo[0] = x0 <= 0 ? -1e30f : (float)(x0 * 8) + m;
                     cur.hi[0] = x1 >= g.nbx ? 1e30f : (float)(x1 * 8) - m;
