@@ -2053,7 +2053,11 @@ __device__ __forceinline__ void assoc_accumulate_sparse(AssocLds& s, const float
     }
 }
 
-__global__ __launch_bounds__(256) void k_assoc_march(AssocArgs a) {
+#ifndef SEMTSDF_MARCH_WPE
+#define SEMTSDF_MARCH_WPE 1  // no occupancy request (register-limited: 3 waves per SIMD)
+#endif
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_MARCH_WPE))) void k_assoc_march(AssocArgs a) {
     __shared__ AssocLds s;
     const int tid = threadIdx.x;
     assoc_lds_clear(s);
@@ -2265,7 +2269,7 @@ __device__ __forceinline__ void shade_hit(const VolGeom& g, const VolBufs& vb, c
 // STATS: instrumentation build of the kernel (a run-time select of the stats pointer would
 // keep MarchStats in scratch memory)
 template <bool STATS>
-__global__ __launch_bounds__(256) void k_render(RenderArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_MARCH_WPE))) void k_render(RenderArgs a) {
     const int x = blockIdx.x * 16 + (threadIdx.x & 15);
     const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
     if (x >= a.width || y >= a.height) return;
