@@ -203,6 +203,8 @@ def load(path: str | None = None):
         _load_error = str(e)
         raise SemTSDFError(ERR_HIP, f"cannot load {p}: {e}") from e
     for name, (res, args) in SIGNATURES.items():
+        if p != LIB_PATH and not hasattr(lib, name):  # an older build under A/B (SEMTSDF_LIB)
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
