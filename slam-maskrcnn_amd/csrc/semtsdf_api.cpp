@@ -126,7 +126,7 @@ int dev_alloc(semtsdf_vol* v, void** p, size_t bytes) {
 }
 
 void free_all(semtsdf_vol* v) {
-    void* ptrs[] = {v->b.sdf, v->b.wt, v->b.bmin, v->b.bplain, v->b.sbmin, v->b.bdist, v->b.boct, v->b.botmp, v->b.bdirty, v->b.sflag, v->b.color, v->b.hist, v->b.hmask, v->b.cls, v->b.cls_cnt, v->depth_d, v->rgb_d,
+    void* ptrs[] = {v->b.sdf, v->b.wt, v->b.bmin, v->b.bplain, v->b.sbmin, v->b.bdist, v->b.boct, v->b.botmp, v->b.bdirty, v->b.dlist, v->b.sflag, v->b.color, v->b.hist, v->b.hmask, v->b.cls, v->b.cls_cnt, v->depth_d, v->rgb_d,
                     v->mask_d, v->cls_d, v->pyr.px, v->pyr.l0, v->pyr.l1, v->tables_d, v->decision_d,
                     v->num_objs_d, v->probs_d, v->box_d, v->palette_d, v->render_d, v->render_t_d,
                     v->counters_d, v->ray_state_d, v->unit_list_d, v->list_count_d, v->rcp_table_d};
@@ -367,8 +367,7 @@ int associate_impl(semtsdf_vol* v, uint8_t* mask_d, const float E[16], hipStream
     EventPair ep;
     timing_begin(v, v->ev_assoc, s, &ep);
     if (int rc = ensure_bmin(v, s)) return rc;
-    HIPC(hipMemsetAsync(v->tables_d, 0, sizeof(AssocTables), s));
-    HIPC(hipMemsetAsync(&v->tables_d->first_px[0], 0xFF, sizeof(unsigned) * 256, s));
+    HIPC(launch_tables_init(v->tables_d, s));
     HIPC(launch_mask_stats(mask_d, (int)npx(v), v->tables_d, s));
     AssocArgs a{};
     a.g = v->g;
@@ -659,8 +658,11 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     if ((rc = dev_alloc(v, (void**)&v->b.bdist, nbricks))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->b.boct, nbricks * 8))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->b.botmp, nbricks * 8))) return bail(rc);
-    if ((rc = dev_alloc(v, (void**)&v->b.bdirty, nbricks))) return bail(rc);
-    if (nbricks && hipMemset(v->b.bdirty, 0, nbricks) != hipSuccess) return bail(fail(SEMTSDF_ERR_HIP, "memset failed"));
+    const size_t nquads = (size_t)g.nbx * g.nby * (size_t)((g.nbz + 3) / 4);
+    if ((rc = dev_alloc(v, (void**)&v->b.bdirty, nquads * 4))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&v->b.dlist, (nquads + 1) * 4))) return bail(rc);
+    if (nquads && (hipMemset(v->b.bdirty, 0, nquads * 4) != hipSuccess || hipMemset(v->b.dlist, 0, 4) != hipSuccess))
+        return bail(fail(SEMTSDF_ERR_HIP, "memset failed"));
     if ((rc = dev_alloc(v, &v->b.color, g.nvox * 4 * (ci32 ? 4 : 1)))) return bail(rc);
     if (p->flags & SEMTSDF_F_SEMANTIC)
     {
@@ -891,8 +893,7 @@ int semtsdf_parse_frame(semtsdf_vol* v, const uint16_t* depth, const uint8_t* rg
             int rc = associate_impl(v, v->mask_d, E, s, true);
             if (rc) return rc;
         } else {
-            HIPC(hipMemsetAsync(v->tables_d, 0, sizeof(AssocTables), s));
-            HIPC(hipMemsetAsync(&v->tables_d->first_px[0], 0xFF, sizeof(unsigned) * 256, s));
+            HIPC(launch_tables_init(v->tables_d, s));
             HIPC(launch_mask_stats(v->mask_d, (int)n, v->tables_d, s));
             HIPC(launch_first_frame_objs(v->tables_d, v->num_objs_d, s));
         }
@@ -936,8 +937,7 @@ int semtsdf_parse_frame_dev_after(semtsdf_vol* v, const uint16_t* depth_d, const
             int rc = associate_impl(v, mask_d, E, s, false);
             if (rc) return rc;
         } else {
-            HIPC(hipMemsetAsync(v->tables_d, 0, sizeof(AssocTables), s));
-            HIPC(hipMemsetAsync(&v->tables_d->first_px[0], 0xFF, sizeof(unsigned) * 256, s));
+            HIPC(launch_tables_init(v->tables_d, s));
             HIPC(launch_mask_stats(mask_d, (int)npx(v), v->tables_d, s));
             HIPC(launch_first_frame_objs(v->tables_d, v->num_objs_d, s));
         }
@@ -1080,8 +1080,7 @@ int semtsdf_shard_assoc_apply(semtsdf_vol* v, const int64_t* reduced_d, uint8_t*
     hipStream_t s = pick(v, stream);
     EventPair ep;
     timing_begin(v, v->ev_assoc, s, &ep);
-    HIPC(hipMemsetAsync(v->tables_d, 0, sizeof(AssocTables), s));
-    HIPC(hipMemsetAsync(&v->tables_d->first_px[0], 0xFF, sizeof(unsigned) * 256, s));
+    HIPC(launch_tables_init(v->tables_d, s));
     HIPC(launch_mask_stats(mask_d, (int)npx(v), v->tables_d, s));
     HIPC(launch_tables_from_partial((const long long*)reduced_d, v->tables_d, s));
     HIPC(launch_assoc_decide(v->tables_d, v->decision_d, 0, v->p.prior_mrcnn_err_rate, v->num_objs_d, s));
@@ -1102,8 +1101,7 @@ int semtsdf_shard_note_integrated(semtsdf_vol* v, const uint8_t* mask_d, void* s
     hipStream_t s = pick(v, stream);
     if (v->n_obs == 0 && (v->p.flags & SEMTSDF_F_SEMANTIC)) {
         if (!mask_d) return fail(SEMTSDF_ERR_INVALID, "semantic volume needs a mask");
-        HIPC(hipMemsetAsync(v->tables_d, 0, sizeof(AssocTables), s));
-        HIPC(hipMemsetAsync(&v->tables_d->first_px[0], 0xFF, sizeof(unsigned) * 256, s));
+        HIPC(launch_tables_init(v->tables_d, s));
         HIPC(launch_mask_stats(mask_d, (int)npx(v), v->tables_d, s));
         HIPC(launch_first_frame_objs(v->tables_d, v->num_objs_d, s));
     }

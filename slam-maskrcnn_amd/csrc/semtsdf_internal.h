@@ -73,7 +73,9 @@ struct VolBufs {
                        // set: negative along axis a), so a ray heading into octant o may step
                        // through the box reaching that many bricks ahead of it (bdist = the min)
     uint64_t* botmp;   // scratch of the distance passes
-    uint8_t* bdirty;   // per 8^3 brick: overlaps a unit integrated since the last map update
+    uint32_t* bdirty;  // per quad of 4 z-consecutive 8^3 bricks ((bx, by, bz/4), z fastest): bit j set when
+                       // a voxel of brick 4q + j crossed the skip threshold since the last map update
+    uint32_t* dlist;   // [1 + quads]: count, then the quads whose dirty word is nonzero
     uint8_t* sflag;    // per 128-B sdf line (32 voxels): 1 = every sdf is 1.0f and every weight
                        // < 2^23 (k_integrate skips the sdf traffic of such lines); 0 = unknown
 };
@@ -137,6 +139,7 @@ struct AssocTables {
     unsigned int max_label;                   // max(mask)
     unsigned int pad;
 };
+static_assert(sizeof(AssocTables) % 8 == 0, "AssocTables is cleared as 8-B words");
 
 // Decision output written by the single-workgroup decide kernel.
 struct AssocDecision {
@@ -246,6 +249,7 @@ hipError_t launch_integrate(const IntegrateArgs& a, hipStream_t s, hipEvent_t e0
 uint64_t unit_count(const VolGeom& g);
 uint64_t unit_list_capacity(const VolGeom& g);
 hipError_t launch_cull(const IntegrateArgs& a, hipStream_t s);       // per-unit cull flags
+hipError_t launch_tables_init(AssocTables* t, hipStream_t s);  // zero sums, first_px = UINT_MAX
 hipError_t launch_mask_stats(const uint8_t* mask, int npx, AssocTables* t, hipStream_t s);
 hipError_t launch_assoc_march(const AssocArgs& a, hipStream_t s);
 hipError_t launch_assoc_decide(const AssocTables* t, AssocDecision* d, int num_objs, float eps,

@@ -180,21 +180,16 @@ hipError_t launch_min_i64(long long* dst, const long long* src, size_t n, hipStr
 // the other bricks stay on their side of it).  k_brick_dilate: bmin[b] = min of the
 // plain map over b + {0,1}^3, which covers [8b, 8b + 8] per axis: every voxel a trilinear
 // sample based in brick b reads.
-__global__ __launch_bounds__(256) void k_brick_plain(VolGeom g, const float* __restrict__ sdf, float* __restrict__ plain,
-                                                     uint8_t* __restrict__ dirty, int all) {
-    // one wave per 4 z-consecutive bricks: lane = one (x, y) row of 32 voxels = one whole
-    // 128-B line (a row of a single brick is only 32 B of a line)
+// One wave per 4 z-consecutive bricks (a quad): lane = one (x, y) row of 32 voxels = one
+// whole 128-B line (a row of a single brick is only 32 B of a line).  `want` bit j: recompute
+// brick 4q + j.
+__device__ __forceinline__ void brick_quad_min(const VolGeom& g, const float* __restrict__ sdf,
+                                               float* __restrict__ plain, unsigned q, unsigned want) {
     const unsigned nbq = (unsigned)(g.nbz + 3) / 4;
-    const unsigned nq = (unsigned)g.nbx * g.nby * nbq;
-    const unsigned q = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (q >= nq) return;
     const int lane = threadIdx.x & 63;
     const int bq = q % nbq, by = (q / nbq) % g.nby, bx = q / (nbq * g.nby);
     const unsigned br0 = ((unsigned)bx * g.nby + (unsigned)by) * g.nbz + (unsigned)bq * 4;
     const int nbr = min(4, g.nbz - bq * 4);
-    unsigned want = 0;
-    for (int j = 0; j < nbr; ++j) want |= ((all || dirty[br0 + j]) ? 1u : 0u) << j;
-    if (!want) return;  // wave-uniform
     const int x = bx * 8 + (lane >> 3), y = by * 8 + (lane & 7), z0 = bq * 32;
     float m[4] = {3.0e38f, 3.0e38f, 3.0e38f, 3.0e38f};
     if (x < g.dimx && y < g.dimy) {
@@ -221,7 +216,30 @@ __global__ __launch_bounds__(256) void k_brick_plain(VolGeom g, const float* __r
     if (lane < nbr && ((want >> lane) & 1u)) {
         const float mj = lane == 0 ? m[0] : lane == 1 ? m[1] : lane == 2 ? m[2] : m[3];
         plain[br0 + lane] = mj;
-        dirty[br0 + lane] = 0;
+    }
+}
+
+// all: every quad (one wave each).  Else the quads on the dirty list (dlist[0] entries from
+// dlist[1]; the integrate appends a quad when its dirty word turns nonzero), grid-strided.
+// Both clear the dirty words; k_brick_dilate, next on the stream, resets the list.
+__global__ __launch_bounds__(256) void k_brick_plain(VolGeom g, const float* __restrict__ sdf, float* __restrict__ plain,
+                                                     uint32_t* __restrict__ dirty, const uint32_t* __restrict__ dlist,
+                                                     int all) {
+    const unsigned nbq = (unsigned)(g.nbz + 3) / 4;
+    const unsigned nq = (unsigned)g.nbx * g.nby * nbq;
+    const unsigned w0 = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (all) {
+        if (w0 >= nq) return;
+        brick_quad_min(g, sdf, plain, w0, 0xFu);
+        if ((threadIdx.x & 63) == 0) dirty[w0] = 0u;
+        return;
+    }
+    const unsigned n = dlist[0];
+    for (unsigned i = w0; i < n; i += gridDim.x * 4) {
+        const unsigned q = dlist[1 + i];
+        const unsigned want = dirty[q];
+        brick_quad_min(g, sdf, plain, q, want);
+        if ((threadIdx.x & 63) == 0) dirty[q] = 0u;
     }
 }
 
@@ -235,9 +253,10 @@ __device__ __forceinline__ float skip_threshold(const VolGeom& g);
 #endif
 
 __global__ __launch_bounds__(256) void k_brick_dilate(VolGeom g, const float* __restrict__ plain, float* __restrict__ bmin,
-                                                      uint64_t* __restrict__ d0) {
+                                                      uint64_t* __restrict__ d0, uint32_t* __restrict__ dlist) {
     const unsigned nb = (unsigned)g.nbx * g.nby * g.nbz;
     const unsigned br = blockIdx.x * blockDim.x + threadIdx.x;
+    if (br == 0) dlist[0] = 0u;  // k_brick_plain has consumed the dirty list
     if (br >= nb) return;
     const int bz = br % g.nbz, by = (br / g.nbz) % g.nby, bx = br / (g.nbz * g.nby);
     float m = 3.0e38f;
@@ -276,14 +295,24 @@ __global__ __launch_bounds__(256) void k_brick_oct_axis(VolGeom g, const uint64_
         d[o] = (int)((v >> (8 * o)) & 0xFFu);
         dmax = max(dmax, d[o]);
     }
-    for (int k = 1; k < kBrickDistCap && k < dmax; ++k) {
-        const uint64_t wp = pos + k < n ? in[(int)br + k * stride] : ~0ull;   // octants positive on axis
-        const uint64_t wn = pos - k >= 0 ? in[(int)br - k * stride] : ~0ull;  // octants negative on axis
+    // neighbours in chunks of 4 (loads in flight together; a k >= every d[o] changes nothing,
+    // so the chunk may run past dmax)
+    for (int k0 = 1; k0 < kBrickDistCap && k0 < dmax; k0 += 4) {
+        uint64_t wp[4], wn[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int k = k0 + i;
+            wp[i] = (k < kBrickDistCap && pos + k < n) ? in[(int)br + k * stride] : ~0ull;   // octants positive on axis
+            wn[i] = (k < kBrickDistCap && pos - k >= 0) ? in[(int)br - k * stride] : ~0ull;  // octants negative on axis
+        }
         dmax = 0;
 #pragma unroll
         for (int o = 0; o < 8; ++o) {
-            const uint64_t w = ((o >> axis) & 1) ? wn : wp;
-            d[o] = min(d[o], max(k, (int)((w >> (8 * o)) & 0xFFu)));
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint64_t w = ((o >> axis) & 1) ? wn[i] : wp[i];
+                d[o] = min(d[o], max(k0 + i, (int)((w >> (8 * o)) & 0xFFu)));
+            }
             dmax = max(dmax, d[o]);
         }
     }
@@ -319,10 +348,12 @@ hipError_t launch_brick_min(const VolGeom& g, const VolBufs& b, bool all, hipStr
     const unsigned nb = (unsigned)g.nbx * g.nby * g.nbz;
     if (nb == 0) return hipSuccess;
     const unsigned nq = (unsigned)g.nbx * g.nby * (unsigned)((g.nbz + 3) / 4);
-    hipLaunchKernelGGL(k_brick_plain, dim3((nq + 3) / 4), dim3(256), 0, s, g, b.sdf, b.bplain, b.bdirty, all ? 1 : 0);
+    const unsigned nw = all ? nq : (nq < 4096u ? nq : 4096u);  // waves (list mode: grid-strided)
+    hipLaunchKernelGGL(k_brick_plain, dim3((nw + 3) / 4), dim3(256), 0, s, g, b.sdf, b.bplain, b.bdirty, b.dlist,
+                       all ? 1 : 0);
     const bool dist = SEMTSDF_BRICK_DIST && b.bdist && b.boct && b.botmp;
     hipLaunchKernelGGL(k_brick_dilate, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.bplain, b.bmin,
-                       dist ? b.botmp : nullptr);
+                       dist ? b.botmp : nullptr, b.dlist);
     if (dist) {  // d0 in botmp -> x -> boct -> y -> botmp -> z -> boct (+ bdist)
         hipLaunchKernelGGL(k_brick_oct_axis, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.botmp, b.boct, nullptr, 0);
         hipLaunchKernelGGL(k_brick_oct_axis, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.boct, b.botmp, nullptr, 1);
@@ -1216,9 +1247,13 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
             const int bz = (up.uz * UZ >> 3) + j;
             const uint64_t pj = ((kLineLanes << (2 * (j & 3))) | (kLineLanes << (2 * (j & 3) + 1)))
                                 << (lane_slot(lane) * kUnitLanes);
-            if (j < UZ / 8 && (cb & pj) && bz < g.nbz)
-                a.b.bdirty[__umul24(__umul24((unsigned)(up.x * UX >> 3), (unsigned)g.nby) + (unsigned)(up.uy * UY >> 3),
-                                    (unsigned)g.nbz) + (unsigned)bz] = 1;
+            if (j < UZ / 8 && (cb & pj) && bz < g.nbz) {
+                // the quad's dirty word; the lane that turns it nonzero lists the quad
+                const unsigned nbq = (unsigned)(g.nbz + 3) >> 2;
+                const unsigned q = __umul24(__umul24((unsigned)(up.x * UX >> 3), (unsigned)g.nby) +
+                                                (unsigned)(up.uy * UY >> 3), nbq) + ((unsigned)bz >> 2);
+                if (atomicOr(&a.b.bdirty[q], 1u << (bz & 3)) == 0u) a.b.dlist[1 + atomicAdd(&a.b.dlist[0], 1u)] = q;
+            }
         }
     }
     if (!(kProbes && a.debug == 10)) {  // 10: timing probe, loads but no sdf/weight stores
@@ -1949,6 +1984,20 @@ __global__ __launch_bounds__(256) void k_mask_stats(const uint8_t* __restrict__ 
     for (int k = threadIdx.x; k < 256; k += 256)
         if (s_first[k] != 0xFFFFFFFFu) atomicMin(&t->first_px[k], s_first[k]);
     if (threadIdx.x == 0) atomicMax(&t->max_label, s_max);
+}
+
+// Association tables before a frame: sums and counts 0, first_px UINT_MAX (one launch in
+// place of two fills).
+__global__ __launch_bounds__(256) void k_tables_init(AssocTables* t) {
+    uint2* w = reinterpret_cast<uint2*>(t);
+    for (unsigned i = threadIdx.x; i < sizeof(AssocTables) / 8; i += 256) w[i] = make_uint2(0u, 0u);
+    __syncthreads();
+    t->first_px[threadIdx.x] = 0xFFFFFFFFu;
+}
+
+hipError_t launch_tables_init(AssocTables* t, hipStream_t s) {
+    hipLaunchKernelGGL(k_tables_init, dim3(1), dim3(256), 0, s, t);
+    return hipGetLastError();
 }
 
 hipError_t launch_mask_stats(const uint8_t* mask, int npx, AssocTables* t, hipStream_t s) {

@@ -177,6 +177,35 @@ def test_render_matches_oracle(S, oracle, stream, mode):
     vol.close()
 
 
+def test_render_and_association_256_match_oracle(S, oracle, stream):
+    """At 256^3 (32 bricks per axis: octant distance boxes up to the cap, LDS-staged map
+    passes, dirty-brick refresh between frames) the hit distances and labels of a render and
+    the association probabilities equal the oracle's."""
+    st, frames = stream
+    semtsdf, L = S
+    p, vol, g, ost = make(S, oracle, (256, 256, 256), frames[0], 0x3)
+    dist = float(np.mean(frames[0].depth[frames[0].depth > 0]) / 5000.0)
+    for k in range(1, 4):
+        fr = frames[k]
+        E = (fr.w2c @ frames[0].c2w).astype(np.float32)
+        vol.integrate(fr.depth, fr.rgb, fr.gt_ids, E)
+        oracle.integrate(g, ost, list(p.K), E, fr.depth, fr.rgb, fr.gt_ids, flags=0x3)
+        if k < 3:  # a render between frames: the next refresh is a dirty-brick update
+            vol.raycast(*semtsdf.orbit_camera(list(p.Kinv), 0.1, dist), L.RENDER_LABEL)
+    s2w, c = semtsdf.orbit_camera(list(p.Kinv), 0.3, dist)
+    img, t = vol.raycast(s2w, c, L.RENDER_LABEL, want_t=True)
+    ref, t_ref = oracle.render(g, s2w, c, 640, 480, L.RENDER_LABEL, ost.sdf, ost.hist, ost.color)
+    assert (t >= 0).mean() > 0.2
+    assert np.array_equal(t.view(np.uint32), t_ref.view(np.uint32))
+    assert (img == ref).all(axis=-1).mean() >= 0.995
+    E = (frames[4].w2c @ frames[0].c2w).astype(np.float32)
+    vol.set_state(3, 6)
+    probs_g, box_g = vol.assoc_probs(E)
+    probs_o, box_o = oracle.march_probs(g, list(p.Kinv), E, 640, 480, ost.sdf, ost.hist, p.box_thresh)
+    assert np.array_equal(probs_g.reshape(-1).view(np.uint32), probs_o.view(np.uint32))
+    vol.close()
+
+
 def test_integrate_general_intrinsics(S, oracle, stream):
     """A K with skew and a non-unit last row (not the pinhole fast path): the general
     screen map s = M p + m with a separate camera depth row, bit-exact."""
