@@ -72,7 +72,9 @@ typedef struct semtsdf_params {
     float duplicate_thresh;  /* Configuration::duplicate_thresh = 0.5 (configuration.h:9; unused upstream) */
     uint32_t flags;          /* SEMTSDF_F_* */
     /* Z-slab sharding.  The global z axis is cut into chunks of z_chunk
-     * planes; chunk c is owned by shard c % z_nshards.  z_nshards == 1 -> whole volume
+     * planes, dealt round by round in boustrophedon order: with n = z_nshards, chunk c of
+     * round r = c / n, position k = c % n, is owned by shard k (r even) or n - 1 - k (r odd).
+     * z_nshards == 1 -> whole volume
      * (z_chunk is then ignored).  Sharded handles store one extra halo plane per chunk. */
     int32_t z_shard, z_nshards, z_chunk;
 } semtsdf_params;

@@ -488,7 +488,8 @@ void oracle_render(const int32_t* dims, const float* geo, const float* s2w, cons
 /* ---------------------------------------------------------------- Z-sharded render
  * Restatement of the sharded raycast protocol (k_shard_ray_step / k_shard_render_final /
  * k_shard_render_finish in semtsdf_kernels.hip) for the tests: virtual shard `shard` of
- * `nshards` (chunks of `chunk` planes dealt round-robin) evaluates only the samples whose
+ * `nshards` (chunks of `chunk` planes dealt round by round in boustrophedon order: shard s
+ * owns position s of even rounds, n - 1 - s of odd ones) evaluates only the samples whose
  * base plane it owns; sampling reads the full volume, which equals the shard's local copy
  * (halo planes are integrated identically).  Records are int32 pairs {key, value bits};
  * the combine is the minimum key over shards.  state: 6 x npx words (k, fk, j, fj, fp, t).
@@ -496,7 +497,8 @@ void oracle_render(const int32_t* dims, const float* geo, const float* s2w, cons
 static int o_owner(const ogeom* g, float pz, int chunk, int nshards) {
     const float iz = (pz - g->start[2]) / g->voxel[2];
     const int zc = o_clamp(o_f2i_rd(iz), 0, g->dz - 1);
-    return (zc / chunk) % nshards;
+    const int c = zc / chunk, r = c / nshards, k = c - r * nshards;
+    return (r & 1) ? nshards - 1 - k : k;
 }
 
 static void o_gmin(const int32_t* gth, int n, size_t npx, size_t px, int32_t* key, int32_t* val) {

@@ -186,7 +186,11 @@ int local_planes(const semtsdf_params* p, int* chunk, int* halo) {
     *halo = 1;
     const int nchunks = (p->dim[2] + p->z_chunk - 1) / p->z_chunk;
     int mine = 0;
-    for (int c = p->z_shard; c < nchunks; c += p->z_nshards) ++mine;
+    // one chunk per round (boustrophedon order, chunk_pos in semtsdf_kernels.hip); the last
+    // round may lack this shard's position
+    const int n = p->z_nshards;
+    for (int r = 0; r * n < nchunks; ++r)
+        if (r * n + ((r & 1) ? n - 1 - p->z_shard : p->z_shard) < nchunks) ++mine;
     return mine * (p->z_chunk + 1);
 }
 

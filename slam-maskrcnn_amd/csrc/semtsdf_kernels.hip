@@ -88,12 +88,24 @@ __device__ __forceinline__ float vox_coord(float p, float start, float voxel, fl
     return q;
 }
 
+// Chunks are dealt to the shards round by round, in boustrophedon order: round r holds chunks
+// r n .. r n + n - 1, and shard s owns position s of even rounds and n - 1 - s of odd ones, so
+// a work density that drifts along z evens out over pairs of rounds.  Local chunk r of a
+// shard is its chunk of round r (only the last round may lack it).
+__host__ __device__ __forceinline__ int chunk_pos(int round, int shard, int n) {
+    return (round & 1) ? n - 1 - shard : shard;
+}
+__host__ __device__ __forceinline__ int chunk_owner(int c, int n) {
+    const int r = c / n;
+    return chunk_pos(r, c - r * n, n);  // the position map is its own inverse
+}
+
 __device__ __forceinline__ int local_to_global_z(const VolGeom& g, int l) {
     if (g.nshards == 1) return l;
     const int per = g.chunk + g.halo;
     const int c = l / per;
     const int w = l - c * per;
-    return (c * g.nshards + g.shard) * g.chunk + w;
+    return (c * g.nshards + chunk_pos(c, g.shard, g.nshards)) * g.chunk + w;
 }
 
 // Local plane of a global plane owned by this shard (inverse of local_to_global_z).
@@ -107,7 +119,7 @@ __device__ __forceinline__ int global_to_local_z(const VolGeom& g, int z) {
 __device__ __forceinline__ int sample_owner(const VolGeom& g, float pz) {
     const float iz = vox_coord(pz, g.start[2], g.voxel[2], g.rvox[2]);
     const int zc = min(max(f2i_rd(iz), 0), g.dimz - 1);
-    return (zc / g.chunk) % g.nshards;
+    return chunk_owner(zc / g.chunk, g.nshards);
 }
 
 // Project one voxel (reference tsdf.cu:30-44).  Returns camera-space z in *qz and the
@@ -882,13 +894,27 @@ __device__ __forceinline__ void stage_project(const IntegrateArgs& a, const Unit
     // the scalar IEEE operation, so the values are those of the scalar contract)
     const f32x2 bsxy = {bsx, bsy}, Mxy = {a.M[2], a.M[5]};
     const float fl0 = (float)l0;  // (float)(l0 + k) == fl0 + k: integers far below 2^24
+    // sharded: the chunk block of l0 once per lane (local_to_global_z without a division per
+    // voxel; l0 + k lies in that block or the next)
+    int cblk = 0, w0 = 0;
+    const int per = g.chunk + g.halo;
+    if (SHARD) {
+        cblk = l0 / per;
+        w0 = l0 - cblk * per;
+    }
     unsigned slow = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         int gz = l0 + k;
         bool zok = row_ok & (l0 + k < g.lz);
         if (SHARD) {
-            gz = local_to_global_z(g, l0 + k);
+            if (per >= 4) {  // 4 consecutive planes span at most two blocks
+                const bool nxt = w0 + k >= per;
+                const int cb = cblk + (nxt ? 1 : 0);
+                gz = (cb * g.nshards + chunk_pos(cb, g.shard, g.nshards)) * g.chunk + (w0 + k - (nxt ? per : 0));
+            } else {
+                gz = local_to_global_z(g, l0 + k);
+            }
             zok = zok & (gz < g.dimz);
         }
         const float pz = fmaf(SHARD ? (float)gz : fl0 + (float)k, g.voxel[2], g.start[2]);
@@ -2547,13 +2573,16 @@ __device__ __forceinline__ bool next_owned_t(const ShardRayArgs& a, const RayGeo
     const float iz = ((fmaf(t, r.dz, r.oz)) - g.start[2]) * g.rvox[2];
     const int zc = min(max((int)floorf(fminf(fmaxf(iz, -1.0f), (float)g.dimz)), 0), g.dimz - 1);
     const int c = zc / g.chunk, n = g.nshards, nch = (g.dimz + g.chunk - 1) / g.chunk;
+    const int rc = c / n, k = c - rc * n;
     float zb;  // voxel coordinate of the boundary the samples cross into the owned chunk
-    if (r.dz > 0.0f) {
-        const int cn = c + ((g.shard - c % n + n) % n);
+    if (r.dz > 0.0f) {  // the first owned chunk at or after c
+        const int pr = chunk_pos(rc, g.shard, n);
+        const int cn = pr >= k ? rc * n + pr : (rc + 1) * n + chunk_pos(rc + 1, g.shard, n);
         if (cn <= c || cn >= nch) return false;
         zb = (float)(cn * g.chunk);
-    } else {
-        const int cp = c - ((c % n - g.shard + n) % n);
+    } else {  // the last owned chunk at or before c
+        const int pr = chunk_pos(rc, g.shard, n);
+        const int cp = pr <= k ? rc * n + pr : (rc > 0 ? (rc - 1) * n + chunk_pos(rc - 1, g.shard, n) : -1);
         if (cp >= c || cp < 0) return false;
         zb = (float)((cp + 1) * g.chunk);
     }

@@ -1,8 +1,10 @@
 """Z-slab sharding of the volume across GPUs.
 
-The global z axis (camera depth at frame 0) is cut into chunks of `chunk` planes; chunk c
-belongs to shard c % nshards (interleaving balances the work: near chunks see more of the
-frustum than far ones).  Each shard stores its chunks back to back, each followed by one
+The global z axis (camera depth at frame 0) is cut into chunks of `chunk` planes, dealt to
+the shards round by round in boustrophedon order: round r holds chunks r n .. r n + n - 1
+and shard s owns position s of even rounds and n - 1 - s of odd ones (interleaving balances
+the work: near chunks see more of the frustum than far ones; the alternation evens out a
+density that drifts along z).  Each shard stores its chunks back to back, each followed by one
 halo plane (the first plane of the next chunk), integrated redundantly so that trilinear
 samples at a chunk face need no exchange.  Integrate is pointwise, so the gathered owned
 planes of all shards equal the single-device volume bit for bit.
@@ -36,10 +38,16 @@ class ShardLayout:
     def nchunks(self) -> int:
         return (self.dimz + self.chunk - 1) // self.chunk if self.nshards > 1 else 1
 
+    def pos(self, rnd: int, shard: int) -> int:
+        """Position of `shard`'s chunk within round `rnd` (chunk_pos of the kernels)."""
+        return self.nshards - 1 - shard if rnd & 1 else shard
+
     def chunks_of(self, shard: int) -> list[int]:
         if self.nshards == 1:
             return [0]
-        return list(range(shard, self.nchunks, self.nshards))
+        n = self.nshards
+        rounds = (self.nchunks + n - 1) // n
+        return [r * n + self.pos(r, shard) for r in range(rounds) if r * n + self.pos(r, shard) < self.nchunks]
 
     def local_planes(self, shard: int) -> int:
         if self.nshards == 1:
@@ -53,7 +61,8 @@ class ShardLayout:
         per = self.chunk + 1
         l = np.arange(self.local_planes(shard))
         c, w = l // per, l % per
-        return (c * self.nshards + shard) * self.chunk + w
+        pos = np.where(c & 1, self.nshards - 1 - shard, shard)
+        return (c * self.nshards + pos) * self.chunk + w
 
     def owned_local(self, shard: int) -> np.ndarray:
         """Boolean mask over local planes: True for planes this shard owns (not halo)."""
@@ -64,7 +73,10 @@ class ShardLayout:
         return (w < self.chunk) & (g < self.dimz)
 
     def owner(self, z: int) -> int:
-        return 0 if self.nshards == 1 else (z // self.chunk) % self.nshards
+        if self.nshards == 1:
+            return 0
+        c = z // self.chunk
+        return self.pos(c // self.nshards, c % self.nshards)
 
     def gather(self, locals_: list[np.ndarray], dimx: int, dimy: int) -> np.ndarray:
         """Assemble per-shard arrays [dimx, dimy, local_planes(s), ...] into the global

@@ -475,7 +475,7 @@ def test_error_paths(S, stream):
     vol.close()
 
 
-@pytest.mark.parametrize("nshards,chunk", [(2, 8), (3, 5), (4, 16)])
+@pytest.mark.parametrize("nshards,chunk", [(2, 8), (3, 5), (4, 16), (3, 2), (8, 15)])
 def test_sharded_handles_equal_single_volume(S, oracle, stream, nshards, chunk):
     """Z-slab shards on one device: the gathered owned planes equal the
     single-handle volume bit for bit, halo planes equal their owners, and each shard
@@ -538,7 +538,7 @@ def _shard_handles(S, p, nshards, chunk):
 
 @pytest.mark.parametrize("nshards,chunk,dimz,exchange", [(2, 8, 64, "allgather"), (3, 5, 64, "min"),
                                                          (4, 16, 64, "allgather"), (1, 64, 64, "min"),
-                                                         (8, 63, 512, "min")])
+                                                         (8, 63, 512, "min"), (4, 15, 128, "min")])
 def test_sharded_pipeline_equals_single_volume(S, oracle, stream, nshards, chunk, dimz, exchange):
     """The Z-sharded association + integrate + raycast protocol (k_shard_*, host
     LocalShardGroup) reproduces the single-volume pipeline bit for bit: relabelled masks,

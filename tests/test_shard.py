@@ -25,7 +25,9 @@ def test_layout_covers_every_plane_once():
         assert np.array_equal(np.sort(owned), np.arange(dimz))
         for s in range(n):
             g = lay.local_to_global(s)
-            assert np.all(np.diff(g) > 0)  # monotone: brick/segment bounds stay conservative
+            # monotone (brick/segment bounds stay conservative); a chunk's halo plane may be the
+            # shard's own next chunk's first plane (boustrophedon rounds), integrated identically
+            assert np.all(np.diff(g) >= 0)
             assert all(lay.owner(int(z)) == s for z in g[lay.owned_local(s)])
 
 
