@@ -1570,6 +1570,9 @@ struct TriCoord {
     float fx, fy, fz;
 };
 
+// SH = false: an unsharded volume (local z == global z) known at compile time (the
+// single-volume marches), so the sharded plane mapping is not compiled in.
+template <bool SH = true>
 __device__ __forceinline__ TriCoord tri_coord(const VolGeom& g, float px, float py, float pz) {
     const float ix = vox_coord(px, g.start[0], g.voxel[0], g.rvox[0]);
     const float iy = vox_coord(py, g.start[1], g.voxel[1], g.rvox[1]);
@@ -1592,7 +1595,7 @@ __device__ __forceinline__ TriCoord tri_coord(const VolGeom& g, float px, float 
     c.dzv = ((flz >= 0.0f) & (flz < hz)) ? 1 : 0;
     // global plane -> local plane of this shard (the caller only samples planes it owns;
     // zc + 1 is then the chunk's next plane or its halo plane)
-    c.zl = g.nshards == 1 ? c.zc : global_to_local_z(g, c.zc);
+    c.zl = (!SH || g.nshards == 1) ? c.zc : global_to_local_z(g, c.zc);
     return c;
 }
 
@@ -1609,8 +1612,9 @@ __device__ __forceinline__ Tri tri_from(const VolGeom& g, const TriCoord& c) {
     return t;
 }
 
+template <bool SH = true>
 __device__ __forceinline__ Tri tri_setup(const VolGeom& g, float px, float py, float pz) {
-    return tri_from(g, tri_coord(g, px, py, pz));
+    return tri_from(g, tri_coord<SH>(g, px, py, pz));
 }
 
 // Empty-space map: brick of 8^3 local voxels holding the sample's 8 corners.
@@ -1649,8 +1653,9 @@ __device__ __forceinline__ unsigned tri_hist(const VolGeom& g, const VolBufs& b,
     return bins;
 }
 
+template <bool SH = true>
 __device__ __forceinline__ float sample_sdf(const VolGeom& g, const float* sdf, float px, float py, float pz) {
-    return tri_eval(sdf, tri_setup(g, px, py, pz));
+    return tri_eval(sdf, tri_setup<SH>(g, px, py, pz));
 }
 
 // Slab test of the march (tsdf.cu:90-100): returns false when the ray misses the volume,
@@ -1778,10 +1783,11 @@ __device__ __forceinline__ void skip_box(const VolGeom& g, SkipCursor& cur, int 
     cur.hi[2] = hz ? 1e30f : (float)(z0 + n) - m;
 }
 
+template <bool SH = true>
 __device__ __forceinline__ bool sample_or_skip(const VolGeom& g, const VolBufs& b, float thr, SkipCursor& cur,
                                                float px, float py, float pz, float* f, bool box = false,
                                                int oct = -1) {
-    const TriCoord c = tri_coord(g, px, py, pz);
+    const TriCoord c = tri_coord<SH>(g, px, py, pz);
     if (SEMTSDF_BRICK_DIST && box && b.bdist) {
         // the brick's distance r to the nearest non-skippable brick of the ray's octant: the
         // r^3 bricks from it on towards the ray's direction are skippable, one box for the
@@ -1863,14 +1869,14 @@ __device__ bool march_ray(const VolGeom& g, const VolBufs& b, float ox, float oy
     const float thr = skip_threshold(g);
     SkipCursor cur;
     const RayVox rv = ray_vox(g, ox, oy, oz, dx, dy, dz);
-    const bool box = g.nshards == 1 && b.bmin;  // local z == global z only unsharded
+    const bool box = b.bmin != nullptr;  // single-volume marches only (the host rejects sharded handles)
     const int oct = SEMTSDF_BRICK_OCT && b.boct ? (dx < 0.0f ? 1 : 0) | (dy < 0.0f ? 2 : 0) | (dz < 0.0f ? 4 : 0) : -1;
     float f_t = 1.0f, f_tt = 0.0f;
     bool prev_skipped = false;  // f_t not evaluated: re-evaluate it at t_prev if needed
     float t_prev = t;
     {
         float f;
-        if (sample_or_skip(g, b, thr, cur, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz), &f, box, oct)) {
+        if (sample_or_skip<false>(g, b, thr, cur, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz), &f, box, oct)) {
             if (!(f > 0.0f)) return false;
             f_t = f;
         } else {
@@ -1900,7 +1906,7 @@ __device__ bool march_ray(const VolGeom& g, const VolBufs& b, float ox, float oy
         float f;
         const int brick_before = cur.brick;
         const bool evaluated =
-            sample_or_skip(g, b, thr, cur, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz), &f, box, oct);
+            sample_or_skip<false>(g, b, thr, cur, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz), &f, box, oct);
         if (st) {
             st->lookups += cur.brick != brick_before;
             st->evals += evaluated;
@@ -1931,7 +1937,7 @@ __device__ bool march_ray(const VolGeom& g, const VolBufs& b, float ox, float oy
             float tn = t;
 #pragma unroll
             for (int j = 0; j < kMarchSpec; ++j) {
-                fs[j] = sample_sdf(g, b.sdf, fmaf(tn, dx, ox), fmaf(tn, dy, oy), fmaf(tn, dz, oz));
+                fs[j] = sample_sdf<false>(g, b.sdf, fmaf(tn, dx, ox), fmaf(tn, dy, oy), fmaf(tn, dz, oz));
                 tn += step;
             }
             if (st) st->evals += kMarchSpec;
@@ -1956,7 +1962,7 @@ __device__ bool march_ray(const VolGeom& g, const VolBufs& b, float ox, float oy
         }
     }
     if (!(f_tt < 0.0f)) return false;
-    if (prev_skipped) f_t = sample_sdf(g, b.sdf, fmaf(t_prev, dx, ox), fmaf(t_prev, dy, oy), fmaf(t_prev, dz, oz));
+    if (prev_skipped) f_t = sample_sdf<false>(g, b.sdf, fmaf(t_prev, dx, ox), fmaf(t_prev, dy, oy), fmaf(t_prev, dz, oz));
     t += step * f_tt / (f_t - f_tt);
     *t_hit = t;
     return true;
@@ -2150,7 +2156,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_MAR
         for (int k = 0; k < kMaxObjects; ++k) p[k] = 0.0f;
         unsigned bins = 0;
         if (a.debug != 2 && march_ray(a.g, a.b, ox, oy, oz, dx, dy, dz, &t)) {
-            const Tri tr = tri_setup(a.g, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
+            const Tri tr = tri_setup<false>(a.g, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
             bins = tri_hist(a.g, a.b, tr, p);
         }
         const int px = y * a.width + x;
@@ -2358,7 +2364,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_MAR
     const uint64_t t_start = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
     if (march_ray(a.g, a.b, ox, oy, oz, dx, dy, dz, &t, STATS ? &ms : nullptr)) {
         th = t;
-        const Tri tr = tri_setup(a.g, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
+        const Tri tr = tri_setup<false>(a.g, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
         shade_hit(a.g, a.b, tr, a.mode, a.color_i32, a.palette, &b, &gch, &r);
     }
     a.out_bgr[(size_t)px * 3 + 0] = b;
