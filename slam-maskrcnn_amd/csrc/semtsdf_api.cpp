@@ -100,8 +100,11 @@ struct semtsdf_vol {
     uint32_t n_obs = 0;
     bool bmin_dirty = false;       // integrated since the last map update: update marked bricks
     bool bmin_stale = true;        // reset/upload: rebuild the whole map
-    hipEvent_t bmin_ev = nullptr;  // recorded after the last map update, on the stream that ran it
-    bool bmin_ev_set = false;
+    hipEvent_t bmin_ev = nullptr;  // marks the last map update on map_stream (recorded when needed)
+    bool bmin_ev_set = false;      // bmin_ev covers the last map update
+    hipStream_t map_stream = nullptr;
+    bool map_set = false;          // a map update has run (on map_stream)
+    bool multi_stream = false;     // the volume has been used from more than one stream
     // instrumentation
     int instr = 0;
     std::vector<EventPair> ev_integrate, ev_assoc, ev_render, ev_prep;
@@ -336,20 +339,35 @@ MarchCamera assoc_camera(const semtsdf_vol* v, const float E[16]) {
     return c;
 }
 
+// Orders stream s after the last empty-space map update.  On the stream that ran it nothing
+// is needed; the event is recorded on that stream only once another stream shows up (then
+// eagerly after every update), so single-stream use carries no event barriers.
+int order_after_map(semtsdf_vol* v, hipStream_t s) {
+    if (!v->map_set || v->map_stream == s) return SEMTSDF_OK;
+    v->multi_stream = true;
+    if (!v->bmin_ev_set) {
+        if (!v->bmin_ev) HIPC(hipEventCreateWithFlags(&v->bmin_ev, hipEventDisableTiming));
+        HIPC(hipEventRecord(v->bmin_ev, v->map_stream));  // everything queued there so far
+        v->bmin_ev_set = true;
+    }
+    HIPC(hipStreamWaitEvent(s, v->bmin_ev, 0));
+    return SEMTSDF_OK;
+}
+
 // Rebuild the empty-space map after the volume changed (integrate, upload, reset).  The
 // update runs on the stream of the first march that needs it; marches on other streams (a
-// render overlapping the next frame's association) and the next writer of the volume wait
-// for it through bmin_ev.
+// render overlapping the next frame's association) and the next writer of the volume are
+// ordered after it (order_after_map).
 int ensure_bmin(semtsdf_vol* v, hipStream_t s) {
-    if (!v->bmin_dirty && !v->bmin_stale) {
-        if (v->bmin_ev_set) HIPC(hipStreamWaitEvent(s, v->bmin_ev, 0));
-        return SEMTSDF_OK;
-    }
+    if (int rc = order_after_map(v, s)) return rc;
+    if (!v->bmin_dirty && !v->bmin_stale) return SEMTSDF_OK;
     // stale (reset/upload): every brick; dirty (integrate): the bricks the cull marked
-    if (v->bmin_ev_set) HIPC(hipStreamWaitEvent(s, v->bmin_ev, 0));
     HIPC(launch_brick_min(v->g, v->b, v->bmin_stale, s));
-    if (!v->bmin_ev && hipEventCreateWithFlags(&v->bmin_ev, hipEventDisableTiming) != hipSuccess) v->bmin_ev = nullptr;
-    if (v->bmin_ev) {
+    v->map_stream = s;
+    v->map_set = true;
+    v->bmin_ev_set = false;
+    if (v->multi_stream) {
+        if (!v->bmin_ev) HIPC(hipEventCreateWithFlags(&v->bmin_ev, hipEventDisableTiming));
         HIPC(hipEventRecord(v->bmin_ev, s));
         v->bmin_ev_set = true;
     }
@@ -359,10 +377,7 @@ int ensure_bmin(semtsdf_vol* v, hipStream_t s) {
 }
 
 // A writer of the volume (integrate, upload, reset) orders itself after the last map update.
-int after_bmin(semtsdf_vol* v, hipStream_t s) {
-    if (v->bmin_ev_set) HIPC(hipStreamWaitEvent(s, v->bmin_ev, 0));
-    return SEMTSDF_OK;
-}
+int after_bmin(semtsdf_vol* v, hipStream_t s) { return order_after_map(v, s); }
 
 int associate_impl(semtsdf_vol* v, uint8_t* mask_d, const float E[16], hipStream_t s, bool want_decision) {
     if (v->p.z_nshards != 1) return fail(SEMTSDF_ERR_UNSUPPORTED, "association on a Z-sharded handle is not supported yet");
