@@ -967,6 +967,10 @@ int semtsdf_parse_frame_dev_after(semtsdf_vol* v, const uint16_t* depth_d, const
     int rc = integrate_impl(v, depth_d, rgb_d, sem ? mask_d : nullptr, nullptr, E, s);
     if (rc) return rc;
     v->n_obs++;
+    // the next frame's association (and a live view) march this state: refresh the
+    // empty-space map now, on this stream, so a view on another stream ordered after this
+    // call and the next association on this stream both find it current
+    if (sem) return ensure_bmin(v, s);
     return SEMTSDF_OK;
 }
 
