@@ -289,24 +289,51 @@ __global__ __launch_bounds__(256) void k_brick_dilate(VolGeom g, const float* __
 // brick of that octant, capped: the box of the d bricks from b on along each of the octant's
 // directions is skippable.  The last pass also writes the symmetric distance (the min over
 // the octants: every brick lies in some octant of b) for the sharded march.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));  // v_pk_*_u16 operands
+
+// Octant bytes of a map word in four packed registers of two u16 lanes: R[0] = octants (0, 2),
+// R[1] = (1, 3) from the low dword, R[2] = (4, 6), R[3] = (5, 7) from the high dword.  For a
+// pass along AXIS, octant o takes its neighbour word from wn (negative side) when bit AXIS of
+// o is set, else from wp.
+template <int AXIS>
+__device__ __forceinline__ void oct_unpack(uint64_t wp, uint64_t wn, u16x2 R[4]) {
+    const uint32_t pl = (uint32_t)wp, ph = (uint32_t)(wp >> 32), nl = (uint32_t)wn, nh = (uint32_t)(wn >> 32);
+    uint32_t r0, r1, r2, r3;
+    if (AXIS == 0) {  // odd octants negative
+        r0 = pl & 0x00FF00FFu; r1 = (nl >> 8) & 0x00FF00FFu;
+        r2 = ph & 0x00FF00FFu; r3 = (nh >> 8) & 0x00FF00FFu;
+    } else if (AXIS == 1) {  // octants 2, 3, 6, 7 negative: the high lane of every register
+        r0 = (pl & 0x000000FFu) | (nl & 0x00FF0000u); r1 = ((pl >> 8) & 0x000000FFu) | ((nl >> 8) & 0x00FF0000u);
+        r2 = (ph & 0x000000FFu) | (nh & 0x00FF0000u); r3 = ((ph >> 8) & 0x000000FFu) | ((nh >> 8) & 0x00FF0000u);
+    } else {  // octants 4..7 negative: the high dword
+        r0 = pl & 0x00FF00FFu; r1 = (pl >> 8) & 0x00FF00FFu;
+        r2 = nh & 0x00FF00FFu; r3 = (nh >> 8) & 0x00FF00FFu;
+    }
+    R[0] = __builtin_bit_cast(u16x2, r0); R[1] = __builtin_bit_cast(u16x2, r1);
+    R[2] = __builtin_bit_cast(u16x2, r2); R[3] = __builtin_bit_cast(u16x2, r3);
+}
+
+// One axis pass of the octant distance maps (see above), the 8 octants as packed u16 lanes
+// (v_pk_max_u16 / v_pk_min_u16: 2 octants per operation).
+template <int AXIS>
 __global__ __launch_bounds__(256) void k_brick_oct_axis(VolGeom g, const uint64_t* __restrict__ in,
-                                                        uint64_t* __restrict__ out, uint8_t* __restrict__ sym,
-                                                        int axis) {
+                                                        uint64_t* __restrict__ out, uint8_t* __restrict__ sym) {
     const unsigned nb = (unsigned)g.nbx * g.nby * g.nbz;
     const unsigned br = blockIdx.x * blockDim.x + threadIdx.x;
     if (br >= nb) return;
     const int bz = br % g.nbz, by = (br / g.nbz) % g.nby, bx = br / (g.nbz * g.nby);
-    const int pos = axis == 0 ? bx : axis == 1 ? by : bz;
-    const int n = axis == 0 ? g.nbx : axis == 1 ? g.nby : g.nbz;
-    const int stride = axis == 0 ? g.nby * g.nbz : axis == 1 ? g.nbz : 1;
+    const int pos = AXIS == 0 ? bx : AXIS == 1 ? by : bz;
+    const int n = AXIS == 0 ? g.nbx : AXIS == 1 ? g.nby : g.nbz;
+    const int stride = AXIS == 0 ? g.nby * g.nbz : AXIS == 1 ? g.nbz : 1;
     const uint64_t v = in[br];
-    int d[8];
-    int dmax = 0;
-#pragma unroll
-    for (int o = 0; o < 8; ++o) {
-        d[o] = (int)((v >> (8 * o)) & 0xFFu);
-        dmax = max(dmax, d[o]);
-    }
+    u16x2 d[4];
+    oct_unpack<0>(v, v, d);  // the brick's own word (both sides the same): plain unpack
+    auto hmax = [](const u16x2* x) {
+        const u16x2 m = __builtin_elementwise_max(__builtin_elementwise_max(x[0], x[1]),
+                                                  __builtin_elementwise_max(x[2], x[3]));
+        return (int)max(m.x, m.y);
+    };
+    int dmax = hmax(d);
     // neighbours in chunks of 4 (loads in flight together; a k >= every d[o] changes nothing,
     // so the chunk may run past dmax)
     for (int k0 = 1; k0 < kBrickDistCap && k0 < dmax; k0 += 4) {
@@ -317,26 +344,25 @@ __global__ __launch_bounds__(256) void k_brick_oct_axis(VolGeom g, const uint64_
             wp[i] = (k < kBrickDistCap && pos + k < n) ? in[(int)br + k * stride] : ~0ull;   // octants positive on axis
             wn[i] = (k < kBrickDistCap && pos - k >= 0) ? in[(int)br - k * stride] : ~0ull;  // octants negative on axis
         }
-        dmax = 0;
 #pragma unroll
-        for (int o = 0; o < 8; ++o) {
+        for (int i = 0; i < 4; ++i) {
+            u16x2 w[4];
+            oct_unpack<AXIS>(wp[i], wn[i], w);
+            const u16x2 kk = {(unsigned short)(k0 + i), (unsigned short)(k0 + i)};
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const uint64_t w = ((o >> axis) & 1) ? wn[i] : wp[i];
-                d[o] = min(d[o], max(k0 + i, (int)((w >> (8 * o)) & 0xFFu)));
-            }
-            dmax = max(dmax, d[o]);
+            for (int j = 0; j < 4; ++j) d[j] = __builtin_elementwise_min(d[j], __builtin_elementwise_max(w[j], kk));
         }
+        dmax = hmax(d);
     }
-    uint64_t r = 0;
-    int dmin = kBrickDistCap;
-#pragma unroll
-    for (int o = 0; o < 8; ++o) {
-        r |= (uint64_t)d[o] << (8 * o);
-        dmin = min(dmin, d[o]);
+    // repack: byte o of the word = octant o
+    const uint32_t lo = (uint32_t)d[0].x | ((uint32_t)d[1].x << 8) | ((uint32_t)d[0].y << 16) | ((uint32_t)d[1].y << 24);
+    const uint32_t hi = (uint32_t)d[2].x | ((uint32_t)d[3].x << 8) | ((uint32_t)d[2].y << 16) | ((uint32_t)d[3].y << 24);
+    out[br] = (uint64_t)lo | ((uint64_t)hi << 32);
+    if (sym) {
+        const u16x2 m = __builtin_elementwise_min(__builtin_elementwise_min(d[0], d[1]),
+                                                  __builtin_elementwise_min(d[2], d[3]));
+        sym[br] = (uint8_t)min(min((int)m.x, (int)m.y), kBrickDistCap);
     }
-    out[br] = r;
-    if (sym) sym[br] = (uint8_t)dmin;
 }
 
 // Super-brick level: sbmin[s] = min of bmin over the (up to) 8^3 bricks of super-brick s,
@@ -367,9 +393,9 @@ hipError_t launch_brick_min(const VolGeom& g, const VolBufs& b, bool all, hipStr
     hipLaunchKernelGGL(k_brick_dilate, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.bplain, b.bmin,
                        dist ? b.botmp : nullptr, b.dlist);
     if (dist) {  // d0 in botmp -> x -> boct -> y -> botmp -> z -> boct (+ bdist)
-        hipLaunchKernelGGL(k_brick_oct_axis, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.botmp, b.boct, nullptr, 0);
-        hipLaunchKernelGGL(k_brick_oct_axis, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.boct, b.botmp, nullptr, 1);
-        hipLaunchKernelGGL(k_brick_oct_axis, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.botmp, b.boct, b.bdist, 2);
+        hipLaunchKernelGGL(k_brick_oct_axis<0>, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.botmp, b.boct, nullptr);
+        hipLaunchKernelGGL(k_brick_oct_axis<1>, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.boct, b.botmp, nullptr);
+        hipLaunchKernelGGL(k_brick_oct_axis<2>, dim3((nb + 255) / 256), dim3(256), 0, s, g, b.botmp, b.boct, b.bdist);
     } else {
         const unsigned ns = (unsigned)g.nsx * g.nsy * g.nsz;
         if (b.sbmin && ns) hipLaunchKernelGGL(k_brick_super, dim3((ns + 3) / 4), dim3(256), 0, s, g, b.bmin, b.sbmin);
