@@ -105,6 +105,7 @@ struct semtsdf_vol {
     hipStream_t map_stream = nullptr;
     bool map_set = false;          // a map update has run (on map_stream)
     bool multi_stream = false;     // the volume has been used from more than one stream
+    const uint8_t* pending_lut = nullptr;  // relabel table the next integrate's prepass applies
     // instrumentation
     int instr = 0;
     std::vector<EventPair> ev_integrate, ev_assoc, ev_render, ev_prep;
@@ -303,8 +304,11 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
     if (int rc = after_bmin(v, s)) return rc;
     EventPair epp;
     timing_begin(v, v->ev_prep, s, &epp);
-    HIPC(launch_depth_pyramid(depth_d, rgb_d, mask_d, v->p.width, v->p.height, v->p.depth_scale, v->pyr,
-                              v->list_count_d, s));
+    // a deferred relabel of this frame's association is applied by the prepass (in place)
+    const uint8_t* lut = mask_d ? v->pending_lut : nullptr;
+    v->pending_lut = nullptr;
+    HIPC(launch_depth_pyramid(depth_d, rgb_d, const_cast<uint8_t*>(mask_d), v->p.width, v->p.height, v->p.depth_scale,
+                              v->pyr, v->list_count_d, s, lut));
     HIPC(launch_cull(a, s));
     timing_end(v, v->ev_prep, s, &epp);
     v->n_prep++;
@@ -379,7 +383,10 @@ int ensure_bmin(semtsdf_vol* v, hipStream_t s) {
 // A writer of the volume (integrate, upload, reset) orders itself after the last map update.
 int after_bmin(semtsdf_vol* v, hipStream_t s) { return order_after_map(v, s); }
 
-int associate_impl(semtsdf_vol* v, uint8_t* mask_d, const float E[16], hipStream_t s, bool want_decision) {
+// defer_relabel: the caller integrates this mask next; the relabel is left to that
+// integrate's prepass (v->pending_lut), saving a launch.
+int associate_impl(semtsdf_vol* v, uint8_t* mask_d, const float E[16], hipStream_t s, bool want_decision,
+                   bool defer_relabel = false) {
     if (v->p.z_nshards != 1) return fail(SEMTSDF_ERR_UNSUPPORTED, "association on a Z-sharded handle is not supported yet");
     if (!(v->p.flags & SEMTSDF_F_SEMANTIC)) return fail(SEMTSDF_ERR_STATE, "association needs a SEMANTIC volume");
     if (v->n_obs == 0) return fail(SEMTSDF_ERR_STATE, "association needs n_obs > 0 (tsdf.cu:426)");
@@ -405,7 +412,10 @@ int associate_impl(semtsdf_vol* v, uint8_t* mask_d, const float E[16], hipStream
     }
     HIPC(launch_assoc_march(a, s));
     HIPC(launch_assoc_decide(v->tables_d, v->decision_d, 0, v->p.prior_mrcnn_err_rate, v->num_objs_d, s));
-    HIPC(launch_relabel(mask_d, (int)npx(v), v->decision_d, s));
+    if (defer_relabel)
+        v->pending_lut = &v->decision_d->lut[0];
+    else
+        HIPC(launch_relabel(mask_d, (int)npx(v), v->decision_d, s));
     timing_end(v, v->ev_assoc, s, &ep);
     v->n_assoc++;
     if (want_decision) HIPC(hipMemcpyAsync(v->decision_h, v->decision_d, sizeof(AssocDecision), hipMemcpyDeviceToHost, s));
@@ -909,7 +919,7 @@ int semtsdf_parse_frame(semtsdf_vol* v, const uint16_t* depth, const uint8_t* rg
     if (sem) {
         HIPC(hipMemcpyAsync(v->mask_d, mask_inout, n, hipMemcpyHostToDevice, s));
         if (v->n_obs > 0) {
-            int rc = associate_impl(v, v->mask_d, E, s, true);
+            int rc = associate_impl(v, v->mask_d, E, s, true, true);
             if (rc) return rc;
         } else {
             HIPC(launch_tables_init(v->tables_d, s));
@@ -918,6 +928,7 @@ int semtsdf_parse_frame(semtsdf_vol* v, const uint16_t* depth, const uint8_t* rg
         }
     }
     int rc = integrate_impl(v, v->depth_d, v->rgb_d, sem ? v->mask_d : nullptr, nullptr, E, s);
+    v->pending_lut = nullptr;  // consumed by the prepass (or dropped on an error)
     if (rc) return rc;
     v->n_obs++;
     if (sem) HIPC(hipMemcpyAsync(mask_inout, v->mask_d, n, hipMemcpyDeviceToHost, s));
@@ -953,7 +964,7 @@ int semtsdf_parse_frame_dev_after(semtsdf_vol* v, const uint16_t* depth_d, const
     if (sem) {
         if (!mask_d) return fail(SEMTSDF_ERR_INVALID, "semantic volume needs a mask");
         if (v->n_obs > 0) {
-            int rc = associate_impl(v, mask_d, E, s, false);
+            int rc = associate_impl(v, mask_d, E, s, false, true);
             if (rc) return rc;
         } else {
             HIPC(launch_tables_init(v->tables_d, s));
@@ -965,6 +976,7 @@ int semtsdf_parse_frame_dev_after(semtsdf_vol* v, const uint16_t* depth_d, const
     // other streams (a live render) finish first; the association above, a read, may overlap them
     if (integrate_after_event) HIPC(hipStreamWaitEvent(s, (hipEvent_t)integrate_after_event, 0));
     int rc = integrate_impl(v, depth_d, rgb_d, sem ? mask_d : nullptr, nullptr, E, s);
+    v->pending_lut = nullptr;  // consumed by the prepass (or dropped on an error)
     if (rc) return rc;
     v->n_obs++;
     // the next frame's association (and a live view) march this state: refresh the

@@ -238,8 +238,9 @@ size_t mask_scratch_bytes();
 size_t mask_scratch_kept_offset();
 hipError_t launch_brick_min(const VolGeom& g, const VolBufs& b, bool all, hipStream_t s);
 hipError_t launch_fill_volume(const VolGeom& g, const VolBufs& b, uint32_t flags, hipStream_t s);
-hipError_t launch_depth_pyramid(const uint16_t* depth, const uint8_t* rgb, const uint8_t* mask, int w, int h,
-                                float scale, const DepthPyramid& p, unsigned* list_count, hipStream_t s);
+hipError_t launch_depth_pyramid(const uint16_t* depth, const uint8_t* rgb, uint8_t* mask, int w, int h,
+                                float scale, const DepthPyramid& p, unsigned* list_count, hipStream_t s,
+                                const uint8_t* lut = nullptr);  // lut: relabel the mask in place (k_relabel folded in)
 hipError_t launch_vox_chunk(const void* src, void* dst, bool to_ref, const VolGeom& g, uint64_t v0, uint64_t nv,
                             hipStream_t s);
 hipError_t launch_color_chunk(const void* src, void* dst, bool to_ref, bool i32, const VolGeom& g, uint64_t v0,

@@ -419,11 +419,20 @@ hipError_t launch_fill_volume(const VolGeom& g, const VolBufs& b, uint32_t flags
 // 4 columns), loaded as one 8-B depth vector, one 4-B mask word and three 4-B rgb words
 // when the rows are 4-pixel aligned (vec), else pixel by pixel.
 // ------------------------------------------------------------------------------------
+// lut (optional): the association's relabel table (k_relabel folded in): labels are mapped
+// through it and the relabelled mask is written back in place.
 __global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restrict__ depth, const uint8_t* __restrict__ rgb,
-                                                       const uint8_t* __restrict__ mask, int w, int h, float scale,
-                                                       int vec, DepthPyramid p, unsigned* list_count) {
+                                                       uint8_t* mask, int w, int h, float scale,
+                                                       int vec, DepthPyramid p, unsigned* list_count,
+                                                       const uint8_t* __restrict__ lut) {
     const int tx = blockIdx.x, ty = blockIdx.y;
     const int t = threadIdx.x;
+    __shared__ uint32_t s_lut[64];
+    if (lut) {  // uniform
+        if (t < 64) s_lut[t] = reinterpret_cast<const uint32_t*>(lut)[t];
+        __syncthreads();
+    }
+    auto relab = [&](unsigned m) { return (s_lut[m >> 2] >> (8 * (m & 3))) & 0xFFu; };
     if (list_count && tx == 0 && ty == 0 && t < kLists * kListSegs)  // this frame's lists (general, free, full)
         list_count[(t & (kListSegs - 1)) * kListCountStride + (t >> 6) * kListSegs * kListCountStride] = 0u;
     const int r = t >> 3;          // row in tile
@@ -446,7 +455,12 @@ __global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restric
             if (rgb) {
                 const uint32_t* c = reinterpret_cast<const uint32_t*>(rgb + px0 * 3);
                 const uint32_t c0 = c[0], c1 = c[1], c2 = c[2];  // r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3
-                const uint32_t lab = mask ? *reinterpret_cast<const uint32_t*>(mask + px0) : 0u;
+                uint32_t lab = mask ? *reinterpret_cast<const uint32_t*>(mask + px0) : 0u;
+                if (lut && mask) {
+                    lab = relab(lab & 0xFFu) | (relab((lab >> 8) & 0xFFu) << 8) | (relab((lab >> 16) & 0xFFu) << 16) |
+                          (relab(lab >> 24) << 24);
+                    *reinterpret_cast<uint32_t*>(mask + px0) = lab;
+                }
                 o.x = (c0 & 0xFFFFFFu) | ((lab & 0xFFu) << 24);
                 o.y = (c0 >> 24) | ((c1 & 0xFFFFu) << 8) | (((lab >> 8) & 0xFFu) << 24);
                 o.z = (c1 >> 16) | ((c2 & 0xFFu) << 16) | (((lab >> 16) & 0xFFu) << 24);
@@ -465,7 +479,11 @@ __global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restric
                 z |= d == 0u ? 1u : 0u;
                 unsigned c = 0;
                 if (rgb) {
-                    const unsigned lab = mask ? (unsigned)mask[px] : 0u;
+                    unsigned lab = mask ? (unsigned)mask[px] : 0u;
+                    if (lut && mask) {
+                        lab = relab(lab);
+                        mask[px] = (uint8_t)lab;
+                    }
                     c = (unsigned)rgb[px * 3] | ((unsigned)rgb[px * 3 + 1] << 8) | ((unsigned)rgb[px * 3 + 2] << 16) |
                         (lab << 24);
                 }
@@ -501,12 +519,13 @@ __global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restric
                                           max(max(s_z[0], s_z[1]), max(s_z[2], s_z[3])));
 }
 
-hipError_t launch_depth_pyramid(const uint16_t* depth, const uint8_t* rgb, const uint8_t* mask, int w, int h,
-                                float scale, const DepthPyramid& p, unsigned* list_count, hipStream_t s) {
+hipError_t launch_depth_pyramid(const uint16_t* depth, const uint8_t* rgb, uint8_t* mask, int w, int h,
+                                float scale, const DepthPyramid& p, unsigned* list_count, hipStream_t s,
+                                const uint8_t* lut) {
     const bool vec = (w % 4 == 0) && ((uintptr_t)depth % 8 == 0) && ((uintptr_t)p.px % 16 == 0) && (!rgb || (uintptr_t)rgb % 4 == 0) &&
                      (!mask || (uintptr_t)mask % 4 == 0);
     hipLaunchKernelGGL(k_depth_pyramid, dim3(p.w1, p.h1), dim3(256), 0, s, depth, rgb, mask, w, h, scale,
-                       vec ? 1 : 0, p, list_count);
+                       vec ? 1 : 0, p, list_count, lut);
     return hipGetLastError();
 }
 
