@@ -106,6 +106,7 @@ struct semtsdf_vol {
     bool map_set = false;          // a map update has run (on map_stream)
     bool multi_stream = false;     // the volume has been used from more than one stream
     const uint8_t* pending_lut = nullptr;  // relabel table the next integrate's prepass applies
+    bool tables_clean = false;     // tables_d holds the cleared state (left by k_assoc_decide)
     // instrumentation
     int instr = 0;
     std::vector<EventPair> ev_integrate, ev_assoc, ev_render, ev_prep;
@@ -383,6 +384,14 @@ int ensure_bmin(semtsdf_vol* v, hipStream_t s) {
 // A writer of the volume (integrate, upload, reset) orders itself after the last map update.
 int after_bmin(semtsdf_vol* v, hipStream_t s) { return order_after_map(v, s); }
 
+// The association tables in their cleared state before a frame's statistics: one init
+// launch unless the last decide left them cleared.
+int tables_ready(semtsdf_vol* v, hipStream_t s) {
+    if (!v->tables_clean) HIPC(launch_tables_init(v->tables_d, s));
+    v->tables_clean = false;  // the caller's kernels fill them next
+    return SEMTSDF_OK;
+}
+
 // defer_relabel: the caller integrates this mask next; the relabel is left to that
 // integrate's prepass (v->pending_lut), saving a launch.
 int associate_impl(semtsdf_vol* v, uint8_t* mask_d, const float E[16], hipStream_t s, bool want_decision,
@@ -393,7 +402,7 @@ int associate_impl(semtsdf_vol* v, uint8_t* mask_d, const float E[16], hipStream
     EventPair ep;
     timing_begin(v, v->ev_assoc, s, &ep);
     if (int rc = ensure_bmin(v, s)) return rc;
-    HIPC(launch_tables_init(v->tables_d, s));
+    if (int rc = tables_ready(v, s)) return rc;
     HIPC(launch_mask_stats(mask_d, (int)npx(v), v->tables_d, s));
     AssocArgs a{};
     a.g = v->g;
@@ -412,6 +421,7 @@ int associate_impl(semtsdf_vol* v, uint8_t* mask_d, const float E[16], hipStream
     }
     HIPC(launch_assoc_march(a, s));
     HIPC(launch_assoc_decide(v->tables_d, v->decision_d, 0, v->p.prior_mrcnn_err_rate, v->num_objs_d, s));
+    v->tables_clean = true;  // the decide kernel clears them
     if (defer_relabel)
         v->pending_lut = &v->decision_d->lut[0];
     else
@@ -881,6 +891,7 @@ int semtsdf_assoc_probs(semtsdf_vol* v, const float E[16], float* probs, uint8_t
     // tables scratch is reused; the mask is all-zero so no log terms are needed
     HIPC(hipMemsetAsync(v->mask_d, 0, npx(v), s));
     HIPC(hipMemsetAsync(v->tables_d, 0, sizeof(AssocTables), s));
+    v->tables_clean = false;
     AssocArgs a{};
     a.g = v->g;
     a.b = v->b;
@@ -922,7 +933,7 @@ int semtsdf_parse_frame(semtsdf_vol* v, const uint16_t* depth, const uint8_t* rg
             int rc = associate_impl(v, v->mask_d, E, s, true, true);
             if (rc) return rc;
         } else {
-            HIPC(launch_tables_init(v->tables_d, s));
+            if (int rc = tables_ready(v, s)) return rc;
             HIPC(launch_mask_stats(v->mask_d, (int)n, v->tables_d, s));
             HIPC(launch_first_frame_objs(v->tables_d, v->num_objs_d, s));
         }
@@ -967,7 +978,7 @@ int semtsdf_parse_frame_dev_after(semtsdf_vol* v, const uint16_t* depth_d, const
             int rc = associate_impl(v, mask_d, E, s, false, true);
             if (rc) return rc;
         } else {
-            HIPC(launch_tables_init(v->tables_d, s));
+            if (int rc = tables_ready(v, s)) return rc;
             HIPC(launch_mask_stats(mask_d, (int)npx(v), v->tables_d, s));
             HIPC(launch_first_frame_objs(v->tables_d, v->num_objs_d, s));
         }
@@ -1115,10 +1126,11 @@ int semtsdf_shard_assoc_apply(semtsdf_vol* v, const int64_t* reduced_d, uint8_t*
     hipStream_t s = pick(v, stream);
     EventPair ep;
     timing_begin(v, v->ev_assoc, s, &ep);
-    HIPC(launch_tables_init(v->tables_d, s));
+    if (int rc = tables_ready(v, s)) return rc;
     HIPC(launch_mask_stats(mask_d, (int)npx(v), v->tables_d, s));
     HIPC(launch_tables_from_partial((const long long*)reduced_d, v->tables_d, s));
     HIPC(launch_assoc_decide(v->tables_d, v->decision_d, 0, v->p.prior_mrcnn_err_rate, v->num_objs_d, s));
+    v->tables_clean = true;  // the decide kernel clears them
     HIPC(launch_relabel(mask_d, (int)npx(v), v->decision_d, s));
     timing_end(v, v->ev_assoc, s, &ep);
     v->n_assoc++;
@@ -1136,7 +1148,7 @@ int semtsdf_shard_note_integrated(semtsdf_vol* v, const uint8_t* mask_d, void* s
     hipStream_t s = pick(v, stream);
     if (v->n_obs == 0 && (v->p.flags & SEMTSDF_F_SEMANTIC)) {
         if (!mask_d) return fail(SEMTSDF_ERR_INVALID, "semantic volume needs a mask");
-        HIPC(launch_tables_init(v->tables_d, s));
+        if (int rc = tables_ready(v, s)) return rc;
         HIPC(launch_mask_stats(mask_d, (int)npx(v), v->tables_d, s));
         HIPC(launch_first_frame_objs(v->tables_d, v->num_objs_d, s));
     }

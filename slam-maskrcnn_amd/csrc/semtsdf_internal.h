@@ -253,7 +253,7 @@ hipError_t launch_cull(const IntegrateArgs& a, hipStream_t s);       // per-unit
 hipError_t launch_tables_init(AssocTables* t, hipStream_t s);  // zero sums, first_px = UINT_MAX
 hipError_t launch_mask_stats(const uint8_t* mask, int npx, AssocTables* t, hipStream_t s);
 hipError_t launch_assoc_march(const AssocArgs& a, hipStream_t s);
-hipError_t launch_assoc_decide(const AssocTables* t, AssocDecision* d, int num_objs, float eps,
+hipError_t launch_assoc_decide(AssocTables* t, AssocDecision* d, int num_objs, float eps,
                                int* num_objs_dev, hipStream_t s);
 hipError_t launch_first_frame_objs(const AssocTables* t, int* num_objs_dev, hipStream_t s);
 hipError_t launch_relabel(uint8_t* mask, int npx, const AssocDecision* d, hipStream_t s);

@@ -2247,8 +2247,9 @@ hipError_t launch_assoc_march(const AssocArgs& a, hipStream_t s) {
 // maximum, as the reference's strict '>'); per previous id j the winning label i (scanning
 // i in order with a strict '<', i.e. the reference's greedy overwrite); unmatched labels get
 // new ids in the order of their first pixel (tsdf.cu:378-387) by ranking first_px.
-__global__ __launch_bounds__(256) void k_assoc_decide(const AssocTables* __restrict__ T, AssocDecision* D,
-                                                      int* num_objs_dev, float eps) {
+// Leaves the tables cleared for the next frame (k_tables_init's state), so the host can skip
+// that launch.
+__global__ __launch_bounds__(256) void k_assoc_decide(AssocTables* T, AssocDecision* D, int* num_objs_dev, float eps) {
     __shared__ double s_prob[kMaxObjects][kMaxObjects];
     __shared__ int s_bestj[kMaxObjects];
     __shared__ double s_bestp[kMaxObjects];
@@ -2324,9 +2325,14 @@ __global__ __launch_bounds__(256) void k_assoc_decide(const AssocTables* __restr
         D->bad_label = (after > kMaxObjects || max_now > kMaxObjects) ? 1 : 0;
         *num_objs_dev = after;
     }
+    // every read of T is above (the last barrier orders them): clear it for the next frame
+    uint2* w = reinterpret_cast<uint2*>(T);
+    for (unsigned i = tid; i < sizeof(AssocTables) / 8; i += 256) w[i] = make_uint2(0u, 0u);
+    __syncthreads();
+    T->first_px[tid] = 0xFFFFFFFFu;
 }
 
-hipError_t launch_assoc_decide(const AssocTables* t, AssocDecision* d, int num_objs, float eps,
+hipError_t launch_assoc_decide(AssocTables* t, AssocDecision* d, int num_objs, float eps,
                                int* num_objs_dev, hipStream_t s) {
     (void)num_objs;
     hipLaunchKernelGGL(k_assoc_decide, dim3(1), dim3(256), 0, s, t, d, num_objs_dev, eps);
