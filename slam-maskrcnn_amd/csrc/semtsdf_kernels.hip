@@ -1828,19 +1828,22 @@ __device__ __forceinline__ void skip_box(const VolGeom& g, SkipCursor& cur, int 
     cur.hi[2] = hz ? 1e30f : (float)(z0 + n) - m;
 }
 
-template <bool SH = true>
+// OCT: the volume has its octant distance maps (a single volume's marches, known on the
+// host), so the other map modes are not compiled in.
+template <bool SH = true, bool OCT = false>
 __device__ __forceinline__ bool sample_or_skip(const VolGeom& g, const VolBufs& b, float thr, SkipCursor& cur,
                                                float px, float py, float pz, float* f, bool box = false,
                                                int oct = -1) {
     const TriCoord c = tri_coord<SH>(g, px, py, pz);
-    if (SEMTSDF_BRICK_DIST && box && b.bdist) {
+    if (OCT || (SEMTSDF_BRICK_DIST && box && b.bdist)) {
         // the brick's distance r to the nearest non-skippable brick of the ray's octant: the
         // r^3 bricks from it on towards the ray's direction are skippable, one box for the
         // march to step through (without an octant: the (2r-1)^3 bricks around it)
         const int br = brick_of(g, c);
         if (br != cur.brick) {
             cur.brick = br;
-            const int r = oct >= 0 ? (int)reinterpret_cast<const uint8_t*>(b.boct)[(size_t)br * 8 + oct] : b.bdist[br];
+            const int r = (OCT || oct >= 0) ? (int)reinterpret_cast<const uint8_t*>(b.boct)[(size_t)br * 8 + oct]
+                                            : b.bdist[br];
             cur.skip = r > 0;
             if (cur.skip) {
                 const int bx = c.xc >> 3, by = c.yc >> 3, bz = c.zl >> 3;
@@ -1906,6 +1909,7 @@ struct MarchStats {
 #endif
 constexpr int kMarchSpec = SEMTSDF_MARCH_SPEC;  // speculative samples per evaluated sample
 
+template <bool OCT>
 __device__ bool march_ray(const VolGeom& g, const VolBufs& b, float ox, float oy, float oz, float dx, float dy,
                           float dz, float* t_hit, MarchStats* st = nullptr) {
     float t, tfar;
@@ -1914,14 +1918,15 @@ __device__ bool march_ray(const VolGeom& g, const VolBufs& b, float ox, float oy
     const float thr = skip_threshold(g);
     SkipCursor cur;
     const RayVox rv = ray_vox(g, ox, oy, oz, dx, dy, dz);
-    const bool box = b.bmin != nullptr;  // single-volume marches only (the host rejects sharded handles)
-    const int oct = SEMTSDF_BRICK_OCT && b.boct ? (dx < 0.0f ? 1 : 0) | (dy < 0.0f ? 2 : 0) | (dz < 0.0f ? 4 : 0) : -1;
+    const bool box = OCT || b.bmin != nullptr;  // single-volume marches only (the host rejects sharded handles)
+    const int oct = OCT || (SEMTSDF_BRICK_OCT && b.boct) ? (dx < 0.0f ? 1 : 0) | (dy < 0.0f ? 2 : 0) | (dz < 0.0f ? 4 : 0)
+                                                         : -1;
     float f_t = 1.0f, f_tt = 0.0f;
     bool prev_skipped = false;  // f_t not evaluated: re-evaluate it at t_prev if needed
     float t_prev = t;
     {
         float f;
-        if (sample_or_skip<false>(g, b, thr, cur, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz), &f, box, oct)) {
+        if (sample_or_skip<false, OCT>(g, b, thr, cur, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz), &f, box, oct)) {
             if (!(f > 0.0f)) return false;
             f_t = f;
         } else {
@@ -1951,7 +1956,7 @@ __device__ bool march_ray(const VolGeom& g, const VolBufs& b, float ox, float oy
         float f;
         const int brick_before = cur.brick;
         const bool evaluated =
-            sample_or_skip<false>(g, b, thr, cur, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz), &f, box, oct);
+            sample_or_skip<false, OCT>(g, b, thr, cur, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz), &f, box, oct);
         if (st) {
             st->lookups += cur.brick != brick_before;
             st->evals += evaluated;
@@ -2183,6 +2188,12 @@ __device__ __forceinline__ void assoc_accumulate_sparse(AssocLds& s, const float
 #define SEMTSDF_MARCH_WPE 1  // no occupancy request (register-limited: 3 waves per SIMD)
 #endif
 
+// The single-volume marches take the octant-map specialisation when the volume has the maps.
+inline bool oct_maps(const VolBufs& b) {
+    return SEMTSDF_BRICK_DIST && SEMTSDF_BRICK_OCT && b.bmin && b.bdist && b.boct;
+}
+
+template <bool OCT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_MARCH_WPE))) void k_assoc_march(AssocArgs a) {
     __shared__ AssocLds s;
     const int tid = threadIdx.x;
@@ -2200,7 +2211,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_MAR
 #pragma unroll
         for (int k = 0; k < kMaxObjects; ++k) p[k] = 0.0f;
         unsigned bins = 0;
-        if (a.debug != 2 && march_ray(a.g, a.b, ox, oy, oz, dx, dy, dz, &t)) {
+        if (a.debug != 2 && march_ray<OCT>(a.g, a.b, ox, oy, oz, dx, dy, dz, &t)) {
             const Tri tr = tri_setup<false>(a.g, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
             bins = tri_hist(a.g, a.b, tr, p);
         }
@@ -2238,7 +2249,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_MAR
 }
 
 hipError_t launch_assoc_march(const AssocArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_assoc_march, dim3((a.width + 15) / 16, (a.height + 15) / 16), dim3(256), 0, s, a);
+    const dim3 grid((a.width + 15) / 16, (a.height + 15) / 16);
+    if (oct_maps(a.b))
+        hipLaunchKernelGGL(k_assoc_march<true>, grid, dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_assoc_march<false>, grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
@@ -2400,7 +2415,7 @@ __device__ __forceinline__ void shade_hit(const VolGeom& g, const VolBufs& vb, c
 
 // STATS: instrumentation build of the kernel (a run-time select of the stats pointer would
 // keep MarchStats in scratch memory)
-template <bool STATS>
+template <bool STATS, bool OCT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_MARCH_WPE))) void k_render(RenderArgs a) {
     const int x = blockIdx.x * 16 + (threadIdx.x & 15);
     const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
@@ -2413,7 +2428,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_MAR
     float th = -1.0f;
     MarchStats ms;
     const uint64_t t_start = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
-    if (march_ray(a.g, a.b, ox, oy, oz, dx, dy, dz, &t, STATS ? &ms : nullptr)) {
+    if (march_ray<OCT>(a.g, a.b, ox, oy, oz, dx, dy, dz, &t, STATS ? &ms : nullptr)) {
         th = t;
         const Tri tr = tri_setup<false>(a.g, fmaf(t, dx, ox), fmaf(t, dy, oy), fmaf(t, dz, oz));
         shade_hit(a.g, a.b, tr, a.mode, a.color_i32, a.palette, &b, &gch, &r);
@@ -2439,9 +2454,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_MAR
 hipError_t launch_render(const RenderArgs& a, hipStream_t s) {
     const dim3 grid((a.width + 15) / 16, (a.height + 15) / 16);
     if (a.ray_stats)
-        hipLaunchKernelGGL(k_render<true>, grid, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((k_render<true, false>), grid, dim3(256), 0, s, a);
     else
-        hipLaunchKernelGGL(k_render<false>, grid, dim3(256), 0, s, a);
+        if (oct_maps(a.b))
+            hipLaunchKernelGGL((k_render<false, true>), grid, dim3(256), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_render<false, false>), grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -10,4 +10,4 @@ BENCH_ARGS="--only pipeline" bash $R/tools/pmc_groups.sh $OUT \
   "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_INST_CYCLES_VMEM_RD SQ_INSTS_BRANCH" \
   "TCC_HIT_sum TCC_MISS_sum TA_TA_BUSY_sum TD_TD_BUSY_sum" \
   "FETCH_SIZE TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum" > $R/$OUT.log 2>&1 || exit $?
-for k in "k_render<false>" k_assoc_march; do echo "== $k"; python3 $R/tools/pmc_summary.py $R/$OUT "$k"; done
+for k in "k_render<false, true>" "k_assoc_march<true>"; do echo "== $k"; python3 $R/tools/pmc_summary.py $R/$OUT "$k"; done
