@@ -316,7 +316,7 @@ def run_pipeline(semtsdf, L, p, local, n_frames=100, n_warm=5):
     mean_m = tum.mean_depth_m(frames[0].depth)
     ext0_inv = np.linalg.inv(P.parse_pos(traj[0, 1:]))  # frame 0 places the volume (tsdf.cu:173-214)
 
-    def run(overlap):
+    def run(overlap, instr=False):
         vol = semtsdf.Volume(p, local)
         vstream = torch.cuda.ExternalStream(vol.stream, device=dev)
         cstream = torch.cuda.Stream(device=dev)
@@ -366,34 +366,26 @@ def run_pipeline(semtsdf, L, p, local, n_frames=100, n_warm=5):
         vol.sync()
         torch.cuda.synchronize()
         # the timed frames carry no timing events (each event pair adds a barrier on the stream)
+        if instr:  # per-kernel breakdown run: timing events around the kernels
+            vol.reset_timing()
+            vol.set_instrumentation(events=True, count=False)
         t0 = time.perf_counter()
         for k in range(1 + n_warm, n_all):
             frame(k, False)
         vol.sync()
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        img = outs[(n_all - 1) % 2].clone()
-        # per-kernel breakdown: a second pass over the first 20 timed frames, with events
-        vol.reset_timing()
-        vol.set_instrumentation(events=True, count=False)
-        nb = min(20, n_frames)
-        for k in range(ring):
-            upload(1 + n_warm + k)
-        for k in range(1 + n_warm, 1 + n_warm + nb):
-            frame(k, False)
-        vol.sync()
-        torch.cuda.synchronize()
-        tm = vol.timing()
-        vol.set_instrumentation(events=False, count=False)
-        return vol, t1 - t0, tm, img
+        tm = vol.timing() if instr else None
+        return vol, t1 - t0, tm, outs[(n_all - 1) % 2].clone(), int(vol.state().num_objs)
 
-    vol_s, t_ser, tm, img_s = run(False)
+
+    vol_s, t_ser, _, img_s, objs_s = run(False)  # the reported rate: no timing events
     ref_img = img_s.cpu()
-    objs_s = int(vol_s.state().num_objs)
     vol_s.close()
-    vol, t_ovl, _, img_o = run(True)
-    same = bool(torch.equal(img_o.cpu(), ref_img)) and int(vol.state().num_objs) == objs_s
-    st_ = vol.state()
+    vol_b, _, tm, _, _ = run(False, instr=True)  # the same frames again, with events
+    vol_b.close()
+    vol, t_ovl, _, img_o, objs_o = run(True)
+    same = bool(torch.equal(img_o.cpu(), ref_img)) and objs_o == objs_s
     # live orbit (kernel.cpp:101-107): angle += 0.01 per view, distance = mean depth
     out = torch.empty(NPX * 3, dtype=torch.uint8, device=dev)
     n_views = 60
@@ -425,7 +417,7 @@ def run_pipeline(semtsdf, L, p, local, n_frames=100, n_warm=5):
         "integrate_ms_per_frame": tm.integrate_ms / max(tm.n_integrate, 1),
         "prep_ms_per_frame": tm.prep_ms / max(tm.n_prep, 1),
         "render_ms_per_view": tm.render_ms / max(tm.n_render, 1),
-        "num_objs": int(st_.num_objs),
+        "num_objs": objs_s,
     }, {
         "views_per_s": n_views / (tv1 - tv0),
         "render_ms_per_view": tr.render_ms / max(tr.n_render, 1),
