@@ -719,8 +719,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--dim", type=int, default=512)
     ap.add_argument("--frames", type=int, default=16, help="distinct synthetic frames cycled through")
-    ap.add_argument("--c4-chunk", type=int, default=15,
-                    help="Z-slab chunk of the C4 shards (planes; chunk + halo = one 16-plane unit)")
+    ap.add_argument("--c4-chunk", type=int, default=47,
+                    help="Z-slab chunk of the C4 shards (planes; chunk + halo = three 16-plane units)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true", help="skip pipeline, orbit, C2 and C4-single")
     ap.add_argument("--no-c4", action="store_true", help="skip the 1024^3 single-GPU C4 measurement")
