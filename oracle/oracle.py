@@ -60,7 +60,7 @@ def lib():
         _lib.oracle_integrate_slab.restype = None
         _lib.oracle_march_probs.argtypes = [P, P, P, P, C.c_int, C.c_int, P, P, C.c_float, P, P, C.c_int, C.c_int]
         _lib.oracle_march_probs.restype = None
-        _lib.oracle_filter_overlaps.argtypes = [P, P, P, C.c_int, C.c_int, C.c_uint32, C.c_float, C.c_int, P, P, P]
+        _lib.oracle_filter_overlaps.argtypes = [P, P, P, C.c_int, C.c_int, C.c_uint32, C.c_float, C.c_int, P, P, P, P]
         _lib.oracle_filter_overlaps.restype = C.c_int
         _lib.oracle_render.argtypes = [P, P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P, P, C.c_int,
                                        C.c_int]
@@ -194,16 +194,21 @@ def march_probs(g: OGeom, Kinv16, E16, W, H, sdf, hist, box_thresh=0.3):
     return probs, box
 
 
-def filter_overlaps(probs, box, mask, n_obs, num_objs, eps=0.05, precision=1):
-    """Relabels a copy of mask; returns (mask, num_objs, max_obj_now, assigned_prev, assigned_prob)."""
+def filter_overlaps(probs, box, mask, n_obs, num_objs, eps=0.05, precision=1, table=None):
+    """Relabels a copy of mask; returns (mask, num_objs, max_obj_now, assigned_prev, assigned_prob).
+    table: optional float64 [32, 32] that receives every candidate probability (row = current
+    label, column = previous id)."""
     H, W = mask.shape
     m = np.ascontiguousarray(mask, np.uint8).copy()
     no = C.c_int(int(num_objs))
     prev = np.zeros(OMAX, np.int32)
     prob = np.zeros(OMAX, np.float32)
+    if table is not None:
+        assert table.dtype == np.float64 and table.shape == (OMAX, OMAX) and table.flags["C_CONTIGUOUS"]
+        table[:] = 0.0
     mx = lib().oracle_filter_overlaps(_p(np.ascontiguousarray(probs, np.float32)),
                                       _p(np.ascontiguousarray(box, np.uint8)), _p(m), W, H, int(n_obs), eps,
-                                      int(precision), C.byref(no), _p(prev), _p(prob))
+                                      int(precision), C.byref(no), _p(prev), _p(prob), _p(table))
     return m, no.value, mx, prev, prob
 
 

@@ -344,7 +344,7 @@ void oracle_march_probs(const int32_t* dims, const float* geo, const float* Kinv
  * Returns max_obj_now. */
 int oracle_filter_overlaps(const float* probs, const uint8_t* box, uint8_t* mask, int width, int height,
                            uint32_t n_obs, float eps, int precision, int* num_objs, int32_t* assigned_prev,
-                           float* assigned_prob) {
+                           float* assigned_prob, double* prob_table) {
     const size_t n = (size_t)width * height;
     int maxv = 0;
     for (size_t i = 0; i < n; ++i)
@@ -396,6 +396,7 @@ int oracle_filter_overlaps(const float* probs, const uint8_t* box, uint8_t* mask
             else if (precision == 0) prob = (double)expf(af[i][j] / (float)cnts[i][j]);
             else prob = exp(ad[i][j] / (double)cnts[i][j]);
             if (precision == 0) prob = (double)(float)prob;
+            if (prob_table) prob_table[i * OMAX + j] = prob;  /* the candidates, for margins */
             if (prob > max_p) { max_j = j; max_p = prob; }
         }
         if (max_p > (double)thr) {

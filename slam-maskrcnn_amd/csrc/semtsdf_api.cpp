@@ -174,12 +174,13 @@ int check_params(const semtsdf_params* p) {
         return fail(SEMTSDF_ERR_INVALID, "bad shard %d of %d", p->z_shard, p->z_nshards);
     if (p->z_nshards > 1 && (p->z_chunk < 1 || p->z_chunk > p->dim[2]))
         return fail(SEMTSDF_ERR_INVALID, "bad z_chunk %d", p->z_chunk);
-    {  // integrate list entries pack a unit's (x, y/8, z/16) into 12 + 10 + 10 bits (pack_unit)
+    {  // integrate list entries pack a unit's coordinates into 12 + 10 + 10 bits (pack_unit)
         int chunk, halo;
         const int lz = local_planes(p, &chunk, &halo);
-        if (p->dim[0] > 4096 || (p->dim[1] + 7) / 8 > 1024 || (lz + 15) / 16 > 1024)
+        if (!unit_grid_fits(p->dim[0], p->dim[1], lz))
             return fail(SEMTSDF_ERR_INVALID, "volume %d x %d x %d (%d local planes) outside the unit grid limits "
-                        "(x <= 4096, y <= 8192, local z <= 16384)", p->dim[0], p->dim[1], p->dim[2], lz);
+                        "of the list entries (default units: x <= 4096, y <= 8192, local z <= 16384)", p->dim[0],
+                        p->dim[1], p->dim[2], lz);
     }
     return SEMTSDF_OK;
 }
@@ -371,7 +372,9 @@ int ensure_bmin(semtsdf_vol* v, hipStream_t s) {
     v->map_stream = s;
     v->map_set = true;
     v->bmin_ev_set = false;
-    if (v->multi_stream) {
+    // on a stream other than the volume's own, record now: that stream may be gone (a
+    // caller's temporary render stream) by the time another stream needs the ordering
+    if (v->multi_stream || s != v->stream) {
         if (!v->bmin_ev) HIPC(hipEventCreateWithFlags(&v->bmin_ev, hipEventDisableTiming));
         HIPC(hipEventRecord(v->bmin_ev, s));
         v->bmin_ev_set = true;
@@ -913,6 +916,17 @@ int semtsdf_assoc_probs(semtsdf_vol* v, const float E[16], float* probs, uint8_t
     return SEMTSDF_OK;
 }
 
+// An integrate that failed before its prepass leaves the association's deferred relabel
+// unapplied: apply it here, so the mask matches the object count the decide kernel already
+// advanced (the state an immediate relabel would have left), then report the error.
+static int relabel_unconsumed(semtsdf_vol* v, uint8_t* mask_d, hipStream_t s, int rc) {
+    if (v->pending_lut) {
+        v->pending_lut = nullptr;
+        (void)launch_relabel(mask_d, (int)npx(v), v->decision_d, s);
+    }
+    return rc;
+}
+
 int semtsdf_parse_frame(semtsdf_vol* v, const uint16_t* depth, const uint8_t* rgb, uint8_t* mask_inout,
                         const float E[16], semtsdf_assoc_stats* stats, void* stream) {
     if (!v || !depth || !rgb || !E) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
@@ -939,8 +953,7 @@ int semtsdf_parse_frame(semtsdf_vol* v, const uint16_t* depth, const uint8_t* rg
         }
     }
     int rc = integrate_impl(v, v->depth_d, v->rgb_d, sem ? v->mask_d : nullptr, nullptr, E, s);
-    v->pending_lut = nullptr;  // consumed by the prepass (or dropped on an error)
-    if (rc) return rc;
+    if (rc) return relabel_unconsumed(v, v->mask_d, s, rc);
     v->n_obs++;
     if (sem) HIPC(hipMemcpyAsync(mask_inout, v->mask_d, n, hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
@@ -969,7 +982,7 @@ int semtsdf_parse_frame_dev(semtsdf_vol* v, const uint16_t* depth_d, const uint8
 
 int semtsdf_parse_frame_dev_after(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d, uint8_t* mask_d,
                                   const float E[16], void* integrate_after_event, void* stream) {
-    if (!v || !E) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    if (!v || !E || !depth_d || !rgb_d) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
     hipStream_t s = pick(v, stream);
     const bool sem = v->p.flags & SEMTSDF_F_SEMANTIC;
     if (sem) {
@@ -987,8 +1000,7 @@ int semtsdf_parse_frame_dev_after(semtsdf_vol* v, const uint16_t* depth_d, const
     // other streams (a live render) finish first; the association above, a read, may overlap them
     if (integrate_after_event) HIPC(hipStreamWaitEvent(s, (hipEvent_t)integrate_after_event, 0));
     int rc = integrate_impl(v, depth_d, rgb_d, sem ? mask_d : nullptr, nullptr, E, s);
-    v->pending_lut = nullptr;  // consumed by the prepass (or dropped on an error)
-    if (rc) return rc;
+    if (rc) return relabel_unconsumed(v, mask_d, s, rc);
     v->n_obs++;
     // the next frame's association (and a live view) march this state: refresh the
     // empty-space map now, on this stream, so a view on another stream ordered after this

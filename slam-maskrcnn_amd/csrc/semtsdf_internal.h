@@ -249,6 +249,7 @@ hipError_t launch_integrate(const IntegrateArgs& a, hipStream_t s, hipEvent_t e0
                             hipEvent_t e1 = nullptr);  // e0/e1: kernel start/end events (timing)
 uint64_t unit_count(const VolGeom& g);
 uint64_t unit_list_capacity(const VolGeom& g);
+int unit_grid_fits(int dimx, int dimy, int local_z);  // list entries (pack_unit) hold the unit grid
 hipError_t launch_cull(const IntegrateArgs& a, hipStream_t s);       // per-unit cull flags
 hipError_t launch_tables_init(AssocTables* t, hipStream_t s);  // zero sums, first_px = UINT_MAX
 hipError_t launch_mask_stats(const uint8_t* mask, int npx, AssocTables* t, hipStream_t s);

@@ -734,6 +734,12 @@ struct UnitGrid {
 // unit counts; the host rejects volumes whose unit grid does not fit (check_params).
 constexpr int kEntryXBits = 12, kEntryYBits = 10, kEntryZBits = 10;
 static_assert(kEntryXBits + kEntryYBits + kEntryZBits == 32, "one word per entry");
+// Host side of that guard, from the same unit shape and field widths as the kernels.
+int unit_grid_fits(int dimx, int dimy, int local_z) {
+    const long long ux = ((long long)dimx + UX - 1) / UX, uy = ((long long)dimy + UY - 1) / UY,
+                    uz = ((long long)local_z + UZ - 1) / UZ;
+    return ux <= (1ll << kEntryXBits) && uy <= (1ll << kEntryYBits) && uz <= (1ll << kEntryZBits);
+}
 __device__ __forceinline__ unsigned pack_unit(unsigned ux, unsigned uy, unsigned uz) {
     return ux | (uy << kEntryXBits) | (uz << (kEntryXBits + kEntryYBits));
 }

@@ -32,7 +32,7 @@ def _c2w_from_pos(pos) -> np.ndarray:
     axis = pos[3:6]
     n = float(np.linalg.norm(axis))
     theta = 2.0 * math.atan2(n, pos[6])
-    rot = rodrigues(theta * axis / n) if n > 0 else np.eye(3)
+    rot = rodrigues(theta * (axis / n)) if n > 0 else np.eye(3)  # normalised first (tsdf_utils.py:68-70)
     m = np.eye(4)
     m[:3, :3] = rot
     m[:3, 3] = pos[:3]

@@ -15,6 +15,7 @@ by tests and checkpoint export.
 """
 from __future__ import annotations
 
+import contextlib
 from dataclasses import dataclass
 
 import numpy as np
@@ -318,10 +319,21 @@ class DistShardGroup:
 
         return C.c_void_p(self.vol.stream)
 
+    @contextlib.contextmanager
     def _on_stream(self):
+        """Run a call on the volume's stream, ordered both ways against the caller's current
+        torch stream: inputs the caller wrote on its stream are ready before the library reads
+        them, and the caller's stream waits for the call's outputs (tensors allocated here are
+        also recorded as used on the caller's stream)."""
         import torch
 
-        return torch.cuda.stream(self.tstream)
+        caller = torch.cuda.current_stream(self.device)
+        if caller.cuda_stream != self.tstream.cuda_stream:
+            self.tstream.wait_stream(caller)
+        with torch.cuda.stream(self.tstream):
+            yield caller
+        if caller.cuda_stream != self.tstream.cuda_stream:
+            caller.wait_stream(self.tstream)
 
     def _exchange_step(self, step):
         from . import _lib as L
@@ -353,10 +365,11 @@ class DistShardGroup:
     def raycast(self, s2w, c, mode, want_t=False):
         import torch
 
-        with self._on_stream():
-            out = torch.empty((self.H, self.W, 3), dtype=torch.uint8, device=self.device)
-            t = torch.empty((self.H, self.W), dtype=torch.float32, device=self.device) if want_t else None
-            self.raycast_dev(s2w, c, mode, out.data_ptr(), t.data_ptr() if t is not None else None)
+        # allocated on the caller's stream (the caching allocator then keeps them alive for
+        # that stream's consumers); the call orders the volume's stream around itself
+        out = torch.empty((self.H, self.W, 3), dtype=torch.uint8, device=self.device)
+        t = torch.empty((self.H, self.W), dtype=torch.float32, device=self.device) if want_t else None
+        self.raycast_dev(s2w, c, mode, out.data_ptr(), t.data_ptr() if t is not None else None)
         return (out, t) if want_t else out
 
     def associate_dev(self, mask_ptr: int, E, want_stats=False):
@@ -382,7 +395,8 @@ class DistShardGroup:
 
         from . import _lib as L
 
-        if self.vol.state().n_obs > 0:
-            self.associate_dev(mask_ptr, E)
-        self.vol.integrate_dev(depth_ptr, rgb_ptr, mask_ptr, E, self._stream())
-        L.check(L.load().semtsdf_shard_note_integrated(self.vol.handle, C.c_void_p(mask_ptr), self._stream()))
+        with self._on_stream():
+            if self.vol.state().n_obs > 0:
+                self.associate_dev(mask_ptr, E)
+            self.vol.integrate_dev(depth_ptr, rgb_ptr, mask_ptr, E, self._stream())
+            L.check(L.load().semtsdf_shard_note_integrated(self.vol.handle, C.c_void_p(mask_ptr), self._stream()))

@@ -222,6 +222,15 @@ class TSDF:
         s2w, c = orbit_camera(self.intrinsic_inv, angle, self.mean_depth if dist is None else dist)
         return self.vol.raycast(s2w, c, L.RENDER_LABEL if mode == "label" else L.RENDER_COLOR)
 
+    def orbit(self, n: int, out_dir: str | None = None, mode: str = "label", step: float = 0.01, callback=None):
+        """The reference's view loop (kernel.cpp:101-107: angle += 0.01 per view at the mean
+        depth) headless: n views written as PNG files to out_dir, or handed to callback(k,
+        angle, bgr), or returned (semtsdf.orbit.orbit_views)."""
+        from .orbit import orbit_views
+
+        return orbit_views(self.vol, self.intrinsic_inv, self.mean_depth, n, mode, step, out_dir=out_dir,
+                           callback=callback)
+
     # ------------------------------------------------------------------ checkpoint (§8f rank 3)
     def save(self, path: str):
         v = self.vol

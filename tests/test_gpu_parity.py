@@ -170,8 +170,8 @@ def test_render_matches_oracle(S, oracle, stream, mode):
         assert np.array_equal(s2w, s2w_o) and np.array_equal(c, c_o)
         img, t = vol.raycast(s2w, c, mode, want_t=True)
         ref, t_ref = oracle.render(g, s2w, c, 640, 480, mode, ost.sdf, ost.hist, ost.color)
-        agree = (img == ref).all(axis=-1).mean()
-        assert agree >= 0.995, agree
+        diff = (img != ref).any(axis=-1)
+        assert not diff.any(), (angle, int(diff.sum()))
         assert (t >= 0).mean() > 0.2  # the scene is actually hit
         assert np.array_equal(t.view(np.uint32), t_ref.view(np.uint32))
     vol.close()
@@ -197,7 +197,7 @@ def test_render_and_association_256_match_oracle(S, oracle, stream):
     ref, t_ref = oracle.render(g, s2w, c, 640, 480, L.RENDER_LABEL, ost.sdf, ost.hist, ost.color)
     assert (t >= 0).mean() > 0.2
     assert np.array_equal(t.view(np.uint32), t_ref.view(np.uint32))
-    assert (img == ref).all(axis=-1).mean() >= 0.995
+    assert np.array_equal(img, ref), int((img != ref).any(axis=-1).sum())
     E = (frames[4].w2c @ frames[0].c2w).astype(np.float32)
     vol.set_state(3, 6)
     probs_g, box_g = vol.assoc_probs(E)
@@ -246,7 +246,7 @@ def test_uploaded_volume_raycasts_and_associates(S, oracle, stream):
     s2w, c = semtsdf.orbit_camera(list(p.Kinv), 0.1, dist)
     img, t = vol.raycast(s2w, c, L.RENDER_LABEL, want_t=True)
     ref, t_ref = oracle.render(g, s2w, c, 640, 480, 0, ost.sdf, ost.hist, ost.color)
-    assert (img == ref).all(axis=-1).mean() >= 0.995
+    assert np.array_equal(img, ref), int((img != ref).any(axis=-1).sum())
     assert np.array_equal(t.view(np.uint32), t_ref.view(np.uint32))
     fr = frames[4]
     E = (fr.w2c @ frames[0].c2w).astype(np.float32)
@@ -778,3 +778,148 @@ def test_render_stream_beside_association_equals_serial(S, stream):
         assert torch.equal(x, y)
     for key in ("sdf", "wt", "color", "hist"):
         assert np.array_equal(sa[key], sb[key]), key
+
+
+@pytest.mark.parametrize("D", [64, 128])
+def test_gpu_histogram_matches_reference_class_count(S, oracle, D):
+    """The HIP label path pinned to the reference's own code: a semantic, ungated volume
+    (flags SEMANTIC only, so every touched voxel counts its label) after the first real frame
+    equals the class count of src/TSDF_Python/tsdf.py:122-130 executed after the integrate
+    block (tests/golden/hist_golden.npz) on every touched voxel whose pixel choice agrees."""
+    from test_oracle_golden import hist_golden_check
+
+    semtsdf, L = S
+    g = np.load(os.path.join(GOLDEN, "hist_golden.npz"))
+    f = np.load(os.path.join(GOLDEN, "frames_tum_fr2.npz"))
+    p = semtsdf.default_params(D, KI, 640, 480)
+    for i in range(3):
+        p.vol_start[i] = g[f"d{D}_vol_start"][i]
+        p.vol_end[i] = g[f"d{D}_vol_start"][i] + (D - 1) * g[f"d{D}_voxel"][i]
+        p.voxel[i] = g[f"d{D}_voxel"][i]
+    p.mu = float(g[f"d{D}_mu"])
+    p.flags = L.F_SEMANTIC
+    vol = semtsdf.Volume(p, 0)
+    vol.integrate(f["depth_a"], f["rgb_a"], np.ascontiguousarray(g["labels"]), g[f"d{D}_E"].astype(np.float32))
+    out = vol.download(hist=True)
+    assert hist_golden_check(D, out["hist"], out["wt"], oracle) > 10_000
+    vol.close()
+
+
+def test_headless_orbit_views_deterministic(S, oracle, stream, tmp_path):
+    """f4: the reference's endless orbit loop (kernel.cpp:101-107, viewer.cu:137-179) headless:
+    TSDF.orbit writes the views as PNG files; the sequence is deterministic (two runs give
+    identical files), view k is the raycast at angle 0.01 (k + 1), the first view equals the
+    oracle's render, and the checkpoint CLI (python -m semtsdf.orbit) writes the same files."""
+    from PIL import Image
+
+    from semtsdf import TSDF, FusionConfig
+    from semtsdf.orbit import main as orbit_main
+
+    semtsdf, L = S
+    st, frames = stream
+    t = TSDF(KI, 64, FusionConfig(vol_dim=64))
+    for k in range(0, 4):
+        fr = frames[k]
+        t.parse_frame(fr.depth, fr.rgb, fr.w2c, float(np.mean(fr.depth[fr.depth > 0]) / 5000.0), fr.mask.copy())
+    a = t.orbit(5, str(tmp_path / "a"))
+    b = t.orbit(5, str(tmp_path / "b"))
+    assert [os.path.basename(x) for x in a] == [f"view_{k:05d}.png" for k in range(5)]
+    for x, y in zip(a, b):
+        assert open(x, "rb").read() == open(y, "rb").read()
+    imgs = t.orbit(5)
+    for k, (x, img) in enumerate(zip(a, imgs)):
+        assert np.array_equal(np.array(Image.open(x))[:, :, ::-1], img)
+        assert np.array_equal(img, t.render(0.01 * (k + 1)))
+    assert any(int(img.any(axis=-1).sum()) > 1000 for img in imgs)
+    p = t.vol.get_params()
+    out = t.vol.download(hist=True)
+    g = oracle.OGeom.from_params(p)
+    s2w, c = semtsdf.orbit_camera(list(p.Kinv), 0.01, t.mean_depth)
+    ref, _ = oracle.render(g, s2w, c, 640, 480, 0, out["sdf"], out["hist"], out["color"])
+    assert np.array_equal(imgs[0], ref)
+    ck = str(tmp_path / "vol.npz")
+    t.save(ck)
+    t.close()
+    orbit_main([ck, str(tmp_path / "cli"), "--views", "5"])
+    for k, x in enumerate(a):
+        assert open(x, "rb").read() == open(str(tmp_path / "cli" / f"view_{k:05d}.png"), "rb").read()
+
+
+def assoc_margins(table, n_labels, thr):
+    """Per current label (rows 1..n_labels-1 of the candidate table): the gap between its best
+    and second-best candidate, and between its best and the acceptance threshold 3 eps."""
+    gaps, thr_gaps = [], []
+    for i in range(1, n_labels):
+        row = np.sort(table[i, 1:])[::-1]
+        if row[0] <= 0.0:
+            continue
+        if row[0] > thr:  # an accepted candidate: the runner-up must not overtake it
+            gaps.append(float(row[0] - row[1]))
+        thr_gaps.append(float(abs(row[0] - thr)))
+    return gaps, thr_gaps
+
+
+def test_association_30_frames_f32_pixel_order_rule(S, oracle):
+    """a6 over a long stream: 30 frames at 128^3.  Every frame the GPU's decisions (2^-28
+    fixed-point sums) equal the reference's own rule, f32 logf sums in pixel order and expf of
+    the f32 mean (tsdf.cu:312-349, oracle precision 0), on the same volume state, and so do the
+    relabelled masks and object counts.  The smallest best-vs-second and best-vs-3 eps margins
+    of the stream are reported (the distance by which f32 rounding would have to move a
+    decision)."""
+    import json
+    from concurrent.futures import ThreadPoolExecutor
+
+    from semtsdf.synth import SyntheticStream
+
+    semtsdf, L = S
+    st = SyntheticStream(seed=2, noise=True)
+    frames = [st.frame(k) for k in range(31)]
+    p, vol, g, ost = make(S, oracle, (128, 128, 128), frames[0], 0x3)
+    eps = float(p.prior_mrcnn_err_rate)
+    bands = [(y, min(y + 60, 480)) for y in range(0, 480, 60)]
+    gaps, thr_gaps, decided = [], [], 0
+    num = 0
+    for k in range(1, 31):
+        fr = frames[k]
+        E = (fr.w2c @ frames[0].c2w).astype(np.float32)
+        m_gpu = np.ascontiguousarray(fr.mask.copy())
+        stats = vol.parse_frame(fr.depth, fr.rgb, m_gpu, E)
+        m_ref = fr.mask.copy()
+        if k == 1:
+            num = int(m_ref.max()) + 1
+        else:
+            probs = np.zeros(640 * 480 * 32, np.float32)
+            box = np.zeros(640 * 480 * 32, np.uint8)
+            Ki = np.ascontiguousarray(np.array(list(p.Kinv), np.float32))
+            E16 = np.ascontiguousarray(E.reshape(16))
+
+            def band(r):
+                oracle.lib().oracle_march_probs(oracle._p(g.dims), oracle._p(g.geo), oracle._p(oracle.k9(Ki)),
+                                                oracle._p(E16), 640, 480, oracle._p(ost.sdf), oracle._p(ost.hist),
+                                                float(p.box_thresh), oracle._p(probs), oracle._p(box), r[0], r[1])
+
+            with ThreadPoolExecutor(8) as ex:
+                list(ex.map(band, bands))
+            table = np.zeros((32, 32), np.float64)
+            m_ref, num, mx, prev, _ = oracle.filter_overlaps(probs, box, m_ref, k - 1, num, eps, precision=0,
+                                                             table=table)
+            assert np.array_equal(np.array(stats.assigned_prev[:]), prev), k
+            assert stats.num_objs == num, k
+            a, b = assoc_margins(table, mx, 3.0 * eps)
+            gaps += a
+            thr_gaps += b
+            decided += int((prev >= 0).sum())
+        assert np.array_equal(m_gpu, m_ref), f"frame {k}"
+        oracle.integrate(g, ost, list(p.K), E, fr.depth, fr.rgb, m_ref, flags=0x3)
+    assert decided > 50  # most instances are matched to earlier ids
+    rep = {"frames": 30, "dim": 128, "matched_decisions": decided, "candidate_rows": len(gaps),
+           "min_best_vs_second": min(gaps), "min_best_vs_3eps": min(thr_gaps),
+           "rule": "f32 logf sums in pixel order, expf of the f32 mean (tsdf.cu:312-349)"}
+    print("association margins", json.dumps(rep))
+    out = os.environ.get("SEMTSDF_REPORT_DIR")
+    if out:
+        os.makedirs(out, exist_ok=True)
+        with open(os.path.join(out, "assoc_margins.json"), "w") as f:
+            json.dump(rep, f)
+    assert min(gaps) > 1e-6 and min(thr_gaps) > 1e-6
+    vol.close()

@@ -236,3 +236,41 @@ def test_library_placement_matches_reference_and_oracle(frames, oracle, fname, D
         for key in ("vol_start", "vol_end", "voxel"):
             assert np.array_equal(np.array(getattr(q, key)[:], np.float32), o[key]), (mode, key)
         assert np.float32(q.mu) == np.float32(o["mu"])
+
+
+def hist_golden_check(D, hist, wt, oracle):
+    """The label path against the reference's own first-frame class count (tsdf.py:122-130,
+    executed by tests/golden/gen_label_tum.py after the integrate block on a real frame with
+    synthetic non-overlapping instance masks).  `hist` [D^3, 32] is a semantic, UNGATED state
+    after that one frame (label k + 1 where mask channel k is set, 0 elsewhere).  On the touched
+    voxels whose f32 pixel choice equals the float64 block's: bin k + 1 == the reference count
+    of channel k for every channel, and bin 0 (background, tsdf.cu:61) counts the rest.
+    Returns the number of compared voxels."""
+    g = _load("hist_golden.npz")
+    n_cls = int(g["n_cls"])
+    vs, vx, mu = g[f"d{D}_vol_start"], g[f"d{D}_voxel"], float(g[f"d{D}_mu"])
+    n_flat = int(g[f"d{D}_nflat"])
+    idx, cnt = g[f"d{D}_idx"], g[f"d{D}_cls_cnt"].astype(np.uint32)
+    f = _load("frames_tum_fr2.npz")
+    agree, edge = agreeing_voxels(oracle, D, n_flat, vs, vx, mu, [g[f"d{D}_E"]], [(f["depth_a"], f["rgb_a"])])
+    hist = hist.reshape(-1, 32)
+    sel = agree[idx]
+    assert sel.mean() > 0.999  # only pixel-border voxels differ in their pixel
+    v = idx[sel]
+    assert np.array_equal(wt[v] > 0, np.ones(v.size, bool))
+    assert np.array_equal(hist[v, 1:n_cls + 1], cnt[sel])
+    assert np.array_equal(hist[v, 0], 1 - cnt[sel].sum(axis=1))
+    assert not hist[v, n_cls + 1:].any()
+    assert int(cnt[sel].sum()) > 1000  # the instances are actually seen
+    return int(v.size)
+
+
+@pytest.mark.parametrize("D", [64, 128])
+def test_c_oracle_histogram_matches_reference_class_count(D, oracle):
+    g = _load("hist_golden.npz")
+    f = _load("frames_tum_fr2.npz")
+    og = oracle.OGeom([D] * 3, g[f"d{D}_vol_start"], g[f"d{D}_voxel"], float(g[f"d{D}_mu"]))
+    st = oracle.OState([D] * 3, np.float32(g[f"d{D}_mu"]), semantic=True)
+    oracle.integrate(og, st, K, g[f"d{D}_E"].astype(np.float32), f["depth_a"], f["rgb_a"], mask=g["labels"],
+                     flags=0x1)
+    assert hist_golden_check(D, st.hist, st.wt, oracle) > 10_000

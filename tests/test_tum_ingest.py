@@ -151,3 +151,21 @@ def test_synthetic_tum_lines_roundtrip_poses():
     for k in range(8):
         assert abs(traj[k, 0] - math.fmod(st.stamp(k), 1e5)) < 1e-4
         assert np.allclose(P.parse_pos(traj[k, 1:]), st.frame(k).w2c, atol=1e-8)
+
+
+def test_associate_python_matches_executed_reference(tmp_path):
+    """tum.associate(mode="python") against the reference's own main.py:63-140 loop, executed
+    on the same file lists and groundtruth by tests/golden/gen_label_tum.py: identical (i, j)
+    pairs (repeats and skips included) and identical interpolated extrinsics."""
+    from conftest import GOLDEN
+
+    g = np.load(os.path.join(GOLDEN, "tum_assoc_golden.npz"), allow_pickle=False)
+    for case in ("jitter", "half_rate_rgb"):
+        root = tmp_path / case
+        _write_dir(str(root), [str(s) for s in g[f"{case}_depth"]], [str(s) for s in g[f"{case}_rgb"]],
+                   [str(s) for s in g["gt_lines"]], shape=(2, 2))
+        py = tum.associate(str(root), "python")
+        assert [(f.i, f.j) for f in py] == [tuple(int(x) for x in p) for p in g[f"{case}_pairs"]], case
+        assert len(py) > 5
+        for f, ext in zip(py, g[f"{case}_extrinsic"]):
+            assert np.array_equal(P.parse_pos(f.pose), ext), case
