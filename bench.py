@@ -25,8 +25,10 @@ N > 1 (torch.distributed.run, one process per GPU, RCCL): configuration C4, stro
 of the fixed 1024^3 semantic volume: rank r integrates its interleaved Z-slab shard
 (no collective) and every step composites one raycast view across the shards (the
 DistShardGroup protocol: an RCCL all-reduce MIN of 8-byte per-pixel records between
-its steps); value = 1024^3 x K / max-over-ranks wall time, so value_N / c4_single_gpu.value
-is the speed-up.
+its steps); value = 1024^3 x K / max-over-ranks wall time.  Rank 0 first runs the same
+workload on the whole volume on its GPU (before any shard exists), so the line carries its
+own speedup_vs_1gpu; roofline = the slowest rank's algorithmic bytes / its kernel time.
+The N = 1 line measures C3 (512^3), so value_N / value_1 is not a speed-up.
 """
 from __future__ import annotations
 
@@ -106,6 +108,20 @@ def max_over_ranks(pg, device, x: float) -> float:
 
 def sum_over_ranks(pg, device, x: float) -> float:
     return x if pg is None else _reduce(pg, device, x, pg.ReduceOp.SUM)
+
+
+def gather_over_ranks(pg, device, x: float) -> list:
+    """Every rank's value of x (an all-reduce SUM of a one-hot vector)."""
+    if pg is None:
+        return [x]
+    import torch
+
+    n, r = pg.get_world_size(), pg.get_rank()
+    on_gpu = pg.get_backend() == "nccl"
+    t = torch.zeros(n, dtype=torch.float64, device=f"cuda:{device}" if on_gpu else "cpu")
+    t[r] = x
+    pg.all_reduce(t, op=pg.ReduceOp.SUM)
+    return [float(v) for v in t.cpu()]
 
 
 # ----------------------------------------------------------------------------- CPU baseline
@@ -695,13 +711,20 @@ def run_c4_dist(semtsdf, L, rank, world, local, pg, frames, f0, K, warmup, chunk
     comp = max_over_ranks(pg, local, time.perf_counter() - tc0)
     Kf = max(4, K // 3)
     elapsed_f, _, _ = timed_integrate(vol, lambda k: (integ(k), view(k)), Kf, 1, pg, local)
+    touched, gated = tc.touched / K, tc.gated / K
+    rank_bytes = 16.0 * touched + 14.0 * gated + 6.0 * NPX  # SURVEY §8d rule, this rank's voxels
+    kerns = gather_over_ranks(pg, local, kern)
+    bytes_all = gather_over_ranks(pg, local, rank_bytes)
     res = {
         "elapsed": t_max,
-        "integrate_kernel_ms_max": max_over_ranks(pg, local, kern),
+        "integrate_kernel_ms_max": max(kerns),
+        "integrate_kernel_ms_ranks": kerns,
+        "algorithmic_bytes_ranks": bytes_all,
         "prep_ms_max": max_over_ranks(pg, local, prep),
         "composite_ms": comp * 1e3,
         "per_frame_elapsed": max_over_ranks(pg, local, elapsed_f), "per_frame_steps": Kf,
-        "touched_per_frame": sum_over_ranks(pg, local, tc.touched / K),
+        "touched_per_frame": sum_over_ranks(pg, local, touched),
+        "gated_per_frame": sum_over_ranks(pg, local, gated),
         "local_planes": int(vol.state().local_dim[2]),
         "device_gib": round(vol.state().device_bytes / 2 ** 30, 1),
     }
@@ -751,28 +774,53 @@ def main():
     log(f"[bench rank {rank}] generated {len(frames) + 1} frames in {time.perf_counter() - t_gen:.1f}s")
 
     if world > 1:
+        # the same workload on one GPU, timed in this run before any shard is allocated (rank
+        # 0, whole 1024^3 volume; the other ranks wait): the base of speedup_vs_1gpu
+        base = None
+        if rank == 0 and not args.no_c4:
+            base = run_c4_single(semtsdf, L, local, frames, f0, args.steps, args.warmup)
+            log(f"[bench rank 0] C4 on one GPU: {base['ms_per_step']:.4f} ms per step")
+        barrier(pg, local)
         r = run_c4_dist(semtsdf, L, rank, world, local, pg, frames, f0, args.steps, args.warmup, args.c4_chunk)
         if rank == 0:
             value = 1024 ** 3 * args.steps / r["elapsed"] / 1e6
             kf = r["per_frame_steps"]
+            slow = int(np.argmax(r["integrate_kernel_ms_ranks"]))
+            kms = r["integrate_kernel_ms_ranks"][slow]
+            sb = r["algorithmic_bytes_ranks"][slow]
+            ach = sb / (kms * 1e-3) / 1e9
+            pf_value = 1024 ** 3 * kf / r["per_frame_elapsed"] / 1e6
             rec = {
                 "metric": METRIC, "value": round(value, 2), "unit": "Mvoxel-updates/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(r["elapsed"] * 1e3 / args.steps, 4),
                 "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
                 "data": "synthetic",
-                "config": {"workload": C4_SPEC + "; Z-slab sharded over the ranks (interleaved chunks), composite by "
-                                       "RCCL all-reduce MIN between protocol steps; speed-up = value / the N=1 "
-                                       "line's c4_single_gpu.value",
+                "config": {"workload": "C4 (not C3: the N=1 line's value is the 512^3 C3 workload, so value_N / "
+                                       "value_1 is no speed-up; use speedup_vs_1gpu) -- " + C4_SPEC +
+                                       "; Z-slab sharded over the ranks (interleaved chunks), composite by RCCL "
+                                       "all-reduce MIN between protocol steps",
                            "volume": [1024, 1024, 1024], "z_chunk": args.c4_chunk, "frames_cycled": len(frames),
                            "parallelism": f"zslab{world}"},
+                "speedup_vs_1gpu": round(value / base["value"], 3) if base else None,
+                "c4_1gpu_in_run": base,
+                "frames_per_s": round(args.steps / r["elapsed"], 1),
+                "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                             "rank": slow, "algorithmic_bytes_per_launch": int(sb),
+                             "bytes_rule": "16 N_touch + 14 N_gate + 6 W H of the slowest rank's voxels (SURVEY "
+                                           "§8d) / that rank's integrate kernel time, against one GPU's peak"},
+                "integrate_kernel_ms_ranks": [round(x, 4) for x in r["integrate_kernel_ms_ranks"]],
                 "integrate_kernel_ms_max_rank": round(r["integrate_kernel_ms_max"], 4),
                 "prep_ms_max_rank": round(r["prep_ms_max"], 4),
                 "final_composite_ms": round(r["composite_ms"], 4),
-                "per_frame_composite": {"value": round(1024 ** 3 * kf / r["per_frame_elapsed"] / 1e6, 2),
-                                        "unit": "Mvoxel-updates/s",
+                "per_frame_composite": {"value": round(pf_value, 2), "unit": "Mvoxel-updates/s",
+                                        "frames_per_s": round(kf / r["per_frame_elapsed"], 1),
                                         "ms_per_step": round(r["per_frame_elapsed"] * 1e3 / kf, 4), "steps": kf,
-                                        "step": "integrate + one composited label view per frame"},
+                                        "step": "integrate + one composited label view per frame",
+                                        "speedup_vs_1gpu": round(pf_value / base["per_frame_view"]["value"], 3)
+                                        if base else None},
                 "touched_per_frame": int(r["touched_per_frame"]),
+                "gated_per_frame": int(r["gated_per_frame"]),
                 "local_planes_rank0": r["local_planes"], "device_gib_rank0": r["device_gib"],
             }
             print(json.dumps(rec), flush=True)
