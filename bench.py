@@ -651,6 +651,18 @@ def run_c4_single(semtsdf, L, local, frames, f0, K, warmup):
     vol.set_instrumentation(events=False, count=False)
     Kf = max(4, K // 3)
     elapsed_f, _, _ = timed_integrate(vol, lambda k: (integ(k), view(k)), Kf, 1)
+    # the semantic frame: association raycast + relabel of the frame's own (permuted) labels,
+    # then the integrate; the masks are relabelled in place, so each step copies its frame's
+    # mask into a working buffer first
+    _, _, msem = resident_frames(frames, ids=False)
+    wm = DeviceBuffer(NPX)
+
+    def sem(k):
+        i = k % len(frames)
+        wm.copy_from(msem.ptr + i * NPX, NPX, stream=vol.stream)
+        vol.parse_frame_dev(dbuf.ptr + i * NPX * 2, rbuf.ptr + i * NPX * 3, wm.ptr, Es[i])
+
+    elapsed_s, _, _ = timed_integrate(vol, sem, Kf, 2)
     res = {
         "workload": "C4 on one GPU: " + C4_SPEC + " (144 GiB)",
         "value": round(1024 ** 3 * K / elapsed / 1e6, 2), "unit": "Mvoxel-updates/s",
@@ -661,11 +673,15 @@ def run_c4_single(semtsdf, L, local, frames, f0, K, warmup):
         "per_frame_view": {"value": round(1024 ** 3 * Kf / elapsed_f / 1e6, 2), "unit": "Mvoxel-updates/s",
                            "ms_per_step": round(elapsed_f * 1e3 / Kf, 4), "steps": Kf,
                            "step": "integrate + one label raycast view per frame"},
+        "per_frame_semantic": {"value": round(1024 ** 3 * Kf / elapsed_s / 1e6, 2), "unit": "Mvoxel-updates/s",
+                               "frames_per_s": round(Kf / elapsed_s, 1),
+                               "ms_per_step": round(elapsed_s * 1e3 / Kf, 4), "steps": Kf,
+                               "step": "association raycast + relabel + integrate per frame"},
         "touched_per_frame": int(tc.touched / K),
         "device_gib": round(vol.state().device_bytes / 2 ** 30, 1),
     }
     out.free()
-    for b in (dbuf, rbuf, mbuf):
+    for b in (dbuf, rbuf, mbuf, msem, wm):
         b.free()
     vol.close()
     return res
@@ -711,6 +727,17 @@ def run_c4_dist(semtsdf, L, rank, world, local, pg, frames, f0, K, warmup, chunk
     comp = max_over_ranks(pg, local, time.perf_counter() - tc0)
     Kf = max(4, K // 3)
     elapsed_f, _, _ = timed_integrate(vol, lambda k: (integ(k), view(k)), Kf, 1, pg, local)
+    # the semantic frame across the shards: the association ray protocol (RCCL all-reduce MIN
+    # between its steps) + all-reduce SUM of the partial tables + relabel, then the integrate
+    msem = torch.from_numpy(np.stack([fr.mask.reshape(-1) for fr in frames])).to(out.device)
+    wm = torch.empty(NPX, dtype=torch.uint8, device=out.device)
+
+    def sem(k):
+        i = k % len(frames)
+        wm.copy_(msem[i])
+        grp.parse_frame_dev(dbuf.ptr + i * NPX * 2, rbuf.ptr + i * NPX * 3, wm.data_ptr(), Es[i])
+
+    elapsed_s, _, _ = timed_integrate(vol, sem, Kf, 2, pg, local)
     touched, gated = tc.touched / K, tc.gated / K
     rank_bytes = 16.0 * touched + 14.0 * gated + 6.0 * NPX  # SURVEY §8d rule, this rank's voxels
     kerns = gather_over_ranks(pg, local, kern)
@@ -723,6 +750,7 @@ def run_c4_dist(semtsdf, L, rank, world, local, pg, frames, f0, K, warmup, chunk
         "prep_ms_max": max_over_ranks(pg, local, prep),
         "composite_ms": comp * 1e3,
         "per_frame_elapsed": max_over_ranks(pg, local, elapsed_f), "per_frame_steps": Kf,
+        "semantic_elapsed": max_over_ranks(pg, local, elapsed_s),
         "touched_per_frame": sum_over_ranks(pg, local, touched),
         "gated_per_frame": sum_over_ranks(pg, local, gated),
         "local_planes": int(vol.state().local_dim[2]),
@@ -819,6 +847,13 @@ def main():
                                         "step": "integrate + one composited label view per frame",
                                         "speedup_vs_1gpu": round(pf_value / base["per_frame_view"]["value"], 3)
                                         if base else None},
+                "per_frame_semantic": {"value": round(1024 ** 3 * kf / r["semantic_elapsed"] / 1e6, 2),
+                                       "unit": "Mvoxel-updates/s", "frames_per_s": round(kf / r["semantic_elapsed"], 1),
+                                       "ms_per_step": round(r["semantic_elapsed"] * 1e3 / kf, 4), "steps": kf,
+                                       "step": "sharded association protocol + relabel + integrate per frame",
+                                       "speedup_vs_1gpu": round((1024 ** 3 * kf / r["semantic_elapsed"] / 1e6) /
+                                                                base["per_frame_semantic"]["value"], 3)
+                                       if base else None},
                 "touched_per_frame": int(r["touched_per_frame"]),
                 "gated_per_frame": int(r["gated_per_frame"]),
                 "local_planes_rank0": r["local_planes"], "device_gib_rank0": r["device_gib"],
@@ -878,6 +913,7 @@ def main():
     live_units = tc.bricks / args.steps
     free_units = tc.free_units / args.steps
     full_units = tc.full_units / args.steps
+    lazy = tc.lazy_voxels / args.steps
     vol.close()
     for b in (dbuf, rbuf, mbuf):
         b.free()
@@ -921,6 +957,7 @@ def main():
         "live_units_per_frame": int(live_units),
         "free_units_per_frame": int(free_units),
         "full_free_units_per_frame": int(full_units),
+        "lazy_weight_voxels_per_frame": int(lazy),
         "touched_mvox_per_s": round(touched / (kern_ms * 1e-3) / 1e6, 1),
         "roofline": {
             "bound": "hbm",

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SEMTSDF_ABI_VERSION 5
+#define SEMTSDF_ABI_VERSION 6
 #define SEMTSDF_MAX_OBJECTS 32 /* tsdf.cuh:4 */
 
 /* ---- status codes ------------------------------------------------------------ */
@@ -111,6 +111,8 @@ typedef struct semtsdf_timing {
     uint64_t n_prep;
     uint64_t free_units;  /* of those, units whose touched voxels all have f == 1 (count mode only) */
     uint64_t full_units;  /* of those, free units whose every voxel is touched (no projection; count mode only) */
+    uint64_t lazy_voxels; /* touched voxels of steady lines whose +1 weight went to the line's pending count
+                             instead of a weight store (count mode only) */
 } semtsdf_timing;
 
 /* ---- library ------------------------------------------------------------------------ */

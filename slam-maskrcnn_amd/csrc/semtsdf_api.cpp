@@ -105,6 +105,13 @@ struct semtsdf_vol {
     hipStream_t map_stream = nullptr;
     bool map_set = false;          // a map update has run (on map_stream)
     bool multi_stream = false;     // the volume has been used from more than one stream
+    // Colour storage of a COLOR_I32 volume (the NumPy rule's int32 colours): u8 x 4 while every
+    // value fits a byte -- the running means of byte inputs never leave [0, 255] -- and int32 x 4
+    // once an upload brings values outside that range.  Integrate, render and the transfers
+    // follow the storage; the int32 boundary is unchanged.
+    bool color_wide = false;
+    int64_t wmax_bound = 0;        // upper bound of every weight (uploads, +1 per integrate): byte storage
+                                   // is left before a colour mean could take the int32 wrap (w >= 2^23)
     const uint8_t* pending_lut = nullptr;  // relabel table the next integrate's prepass applies
     bool tables_clean = false;     // tables_d holds the cleared state (left by k_assoc_decide)
     // instrumentation
@@ -258,12 +265,33 @@ void screen_map(IntegrateArgs& a) {
     a.ftol = 0.5f - ldexpf((float)b, -21);
 }
 
+// A COLOR_I32 volume leaves byte colour storage for int32 x 4 (values converted on the device).
+int widen_color(semtsdf_vol* v, hipStream_t s) {
+    if (v->color_wide) return SEMTSDF_OK;
+    void* wide = nullptr;
+    if (int rc = dev_alloc(v, &wide, v->g.nvox * 16)) return rc;
+    HIPC(launch_color_widen(static_cast<const uint8_t*>(v->b.color), static_cast<int32_t*>(wide), v->g.nvox, s));
+    HIPC(hipStreamSynchronize(s));
+    HIPC(hipFree(v->b.color));
+    v->device_bytes -= v->g.nvox * 4;
+    v->b.color = wide;
+    v->color_wide = true;
+    return SEMTSDF_OK;
+}
+
+
 int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d, const uint8_t* mask_d,
                    const int32_t* cls_d, const float E[16], hipStream_t s) {
     if (!E) return fail(SEMTSDF_ERR_INVALID, "E is NULL");
     if (!depth_d || !rgb_d) return fail(SEMTSDF_ERR_INVALID, "depth/rgb is NULL");
     if ((v->p.flags & SEMTSDF_F_SEMANTIC) && !mask_d) return fail(SEMTSDF_ERR_INVALID, "semantic volume needs a mask");
     if ((v->p.flags & SEMTSDF_F_VOTE) && !cls_d) return fail(SEMTSDF_ERR_INVALID, "vote volume needs cls");
+    // byte colour storage holds the integer means exactly until a weight could reach 2^23,
+    // where the int32 arithmetic of the reference wraps (then the means need int32 storage);
+    // before the kernel arguments are built, which copy the buffer pointers
+    if ((v->p.flags & SEMTSDF_F_COLOR_I32) && !v->color_wide && v->wmax_bound + 1 >= (1ll << 23)) {
+        if (int rc = widen_color(v, s)) return rc;
+    }
     IntegrateArgs a{};
     a.g = v->g;
     a.b = v->b;
@@ -277,6 +305,7 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
     a.depth_scale = v->p.depth_scale;
     a.gate = v->p.gate;
     a.flags = v->p.flags | ((v->instr & 2) ? 0x80000000u : 0u);
+    a.color_wide = v->color_wide ? 1 : 0;
     a.cull = (v->p.flags & SEMTSDF_F_NO_CULL) ? 0 : 1;
     {
         static const char* dbg = getenv("SEMTSDF_DEBUG_INTEGRATE");  // timing probes only
@@ -304,6 +333,7 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
                     : 0;
     if (a.debug == 2) return SEMTSDF_OK;
     if (int rc = after_bmin(v, s)) return rc;
+    v->wmax_bound += 1;
     EventPair epp;
     timing_begin(v, v->ev_prep, s, &epp);
     // a deferred relabel of this frame's association is applied by the prepass (in place)
@@ -705,7 +735,8 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     if ((rc = dev_alloc(v, (void**)&v->b.dlist, (nquads + 1) * 4))) return bail(rc);
     if (nquads && (hipMemset(v->b.bdirty, 0, nquads * 4) != hipSuccess || hipMemset(v->b.dlist, 0, 4) != hipSuccess))
         return bail(fail(SEMTSDF_ERR_HIP, "memset failed"));
-    if ((rc = dev_alloc(v, &v->b.color, g.nvox * 4 * (ci32 ? 4 : 1)))) return bail(rc);
+    (void)ci32;  // COLOR_I32 volumes start with byte storage (color_wide)
+    if ((rc = dev_alloc(v, &v->b.color, g.nvox * 4))) return bail(rc);
     if (p->flags & SEMTSDF_F_SEMANTIC)
     {
         if ((rc = dev_alloc(v, (void**)&v->b.hist, g.nvox * kMaxObjects * 4))) return bail(rc);
@@ -800,7 +831,7 @@ int semtsdf_reset(semtsdf_vol* v, void* stream) {
     HIPC(launch_fill_volume(v->g, v->b, v->p.flags, s));
     HIPC(hipMemsetAsync(v->b.wt, 0, n * 4, s));
     HIPC(hipMemsetAsync(v->b.sflag, 0, n / 32 + 1, s));  // steady flags: unknown
-    HIPC(hipMemsetAsync(v->b.color, 0, v->g.nvox * 4 * ((v->p.flags & SEMTSDF_F_COLOR_I32) ? 4 : 1), s));
+    HIPC(hipMemsetAsync(v->b.color, 0, v->g.nvox * 4 * (v->color_wide ? 4 : 1), s));
     if (v->b.hist) HIPC(hipMemsetAsync(v->b.hist, 0, v->g.nvox * kMaxObjects * 4, s));
     if (v->b.hmask) HIPC(hipMemsetAsync(v->b.hmask, 0, n * 4, s));
     if (v->b.cls) HIPC(hipMemsetAsync(v->b.cls, 0, n * 4, s));
@@ -808,6 +839,7 @@ int semtsdf_reset(semtsdf_vol* v, void* stream) {
     HIPC(hipMemsetAsync(v->num_objs_d, 0, 16, s));
     HIPC(hipMemsetAsync(v->counters_d, 0, kCounters * sizeof(unsigned long long), s));
     v->n_obs = 0;
+    v->wmax_bound = 0;
     v->bmin_stale = true;
     return SEMTSDF_OK;
 }
@@ -1027,7 +1059,7 @@ static ShardRayArgs shard_args(semtsdf_vol* v) {
     a.st.fj = (float*)(base + 12 * n);
     a.st.fp = (float*)(base + 16 * n);
     a.st.t = (float*)(base + 20 * n);
-    a.color_i32 = (v->p.flags & SEMTSDF_F_COLOR_I32) ? 1 : 0;
+    a.color_i32 = v->color_wide ? 1 : 0;
     a.palette = v->palette_d;
     a.n_obs = (float)v->n_obs;
     a.eps = v->p.prior_mrcnn_err_rate;
@@ -1262,7 +1294,7 @@ static int raycast_impl(semtsdf_vol* v, const float s2w[16], const float c[3], i
     a.width = v->p.width;
     a.height = v->p.height;
     a.mode = mode;
-    a.color_i32 = (v->p.flags & SEMTSDF_F_COLOR_I32) ? 1 : 0;
+    a.color_i32 = v->color_wide ? 1 : 0;
     a.palette = v->palette_d;
     a.out_bgr = out_bgr_d;
     a.out_t = out_t_d;
@@ -1354,7 +1386,7 @@ static int vox_xfer(semtsdf_vol* v, void* host, void* dev, bool to_host, const c
 
 // colour between the padded device layout and the reference [N][3] layout, chunked
 static int color_xfer(semtsdf_vol* v, void* host, bool to_host, hipStream_t s, uint64_t vb, uint64_t ve) {
-    const bool i32 = v->p.flags & SEMTSDF_F_COLOR_I32;
+    const bool i32 = v->p.flags & SEMTSDF_F_COLOR_I32;  // the boundary's element type
     const size_t es = i32 ? 4 : 1;
     if (ve <= vb) return SEMTSDF_OK;
     const uint64_t chunk = std::min<uint64_t>(ve - vb, 1ull << 24);
@@ -1365,11 +1397,11 @@ static int color_xfer(semtsdf_vol* v, void* host, bool to_host, hipStream_t s, u
         char* h = static_cast<char*>(host) + (v0 - vb) * 3 * es;
         hipError_t e;
         if (to_host) {
-            e = launch_color_chunk(v->b.color, stage, true, i32, v->g, v0, nv, s);
+            e = launch_color_chunk(v->b.color, stage, true, i32, v->color_wide, v->g, v0, nv, s);
             if (e == hipSuccess) e = hipMemcpyAsync(h, stage, nv * 3 * es, hipMemcpyDeviceToHost, s);
         } else {
             e = hipMemcpyAsync(stage, h, nv * 3 * es, hipMemcpyHostToDevice, s);
-            if (e == hipSuccess) e = launch_color_chunk(stage, v->b.color, false, i32, v->g, v0, nv, s);
+            if (e == hipSuccess) e = launch_color_chunk(stage, v->b.color, false, i32, v->color_wide, v->g, v0, nv, s);
         }
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) {
@@ -1391,6 +1423,7 @@ int semtsdf_download_slab(semtsdf_vol* v, int x0, int x1, float* sdf, int32_t* w
     const uint64_t vb = (uint64_t)x0 * plane, ve = (uint64_t)x1 * plane;
     int rc;
     if (sdf && (rc = vox_xfer(v, sdf, v->b.sdf, true, "sdf", s, vb, ve))) return rc;
+    if (wt) HIPC(launch_flush_lazy(v->g, v->b, s));  // pending increments of steady lines into the weights
     if (wt && (rc = vox_xfer(v, wt, v->b.wt, true, "weight", s, vb, ve))) return rc;
     if (color) {
         rc = color_xfer(v, color, true, s, vb, ve);
@@ -1442,10 +1475,26 @@ int semtsdf_upload(semtsdf_vol* v, const float* sdf, const int32_t* wt, const vo
     // derived maps first: a transfer that fails half-way must not leave steady flags or an
     // empty-space map that describe the old contents (0 = unknown is always safe)
     v->bmin_stale = true;
+    // the weights a flag byte's pending increments apply to stay: fold them in before the
+    // flags are dropped (an upload of the weights replaces them, pending counts included)
+    if (sdf && !wt) HIPC(launch_flush_lazy(v->g, v->b, s));
     if (sdf || wt) HIPC(hipMemsetAsync(v->b.sflag, 0, v->g.nvox / 32 + 1, s));  // steady flags: unknown
     if (sdf && (rc = vox_xfer(v, const_cast<float*>(sdf), v->b.sdf, false, "sdf", s, 0, nref(v)))) return rc;
     if (wt && (rc = vox_xfer(v, const_cast<int32_t*>(wt), v->b.wt, false, "weight", s, 0, nref(v)))) return rc;
+    if (wt) {
+        int64_t m = 0;
+        for (uint64_t i = 0, n = nref(v); i < n; ++i) m = std::max<int64_t>(m, wt[i]);
+        v->wmax_bound = m;
+    }
     if (color) {
+        if ((v->p.flags & SEMTSDF_F_COLOR_I32) && !v->color_wide) {
+            // int32 colours outside [0, 255] need the wide storage (a one-way switch)
+            const int32_t* c = static_cast<const int32_t*>(color);
+            const uint64_t nc = nref(v) * 3;
+            bool fits = true;
+            for (uint64_t i = 0; i < nc && fits; ++i) fits = (uint32_t)c[i] <= 255u;
+            if (!fits && (rc = widen_color(v, s))) return rc;
+        }
         rc = color_xfer(v, const_cast<void*>(color), false, s, 0, nref(v));
         if (rc) return rc;
     }
@@ -1524,6 +1573,7 @@ int semtsdf_get_timing(semtsdf_vol* v, semtsdf_timing* out) {
     out->bricks = c[3];
     out->free_units = c[4];
     out->full_units = c[5];
+    out->lazy_voxels = c[6];
     out->prep_ms = v->t_prep;
     out->n_prep = v->n_prep;
     return SEMTSDF_OK;

@@ -76,8 +76,9 @@ struct VolBufs {
     uint32_t* bdirty;  // per quad of 4 z-consecutive 8^3 bricks ((bx, by, bz/4), z fastest): bit j set when
                        // a voxel of brick 4q + j crossed the skip threshold since the last map update
     uint32_t* dlist;   // [1 + quads]: count, then the quads whose dirty word is nonzero
-    uint8_t* sflag;    // per 128-B sdf line (32 voxels): 1 = every sdf is 1.0f and every weight
-                       // < 2^23 (k_integrate skips the sdf traffic of such lines); 0 = unknown
+    uint8_t* sflag;    // per 128-B sdf line (32 voxels): s >= 1 = every sdf is 1.0f and every weight
+                       // < 2^23 (k_integrate skips the sdf traffic of such lines), and s - 1 increments
+                       // of every weight of the line are pending (lazy weights); 0 = unknown
 };
 
 // Per-frame images of the integrate: depth in metres and rgb+label per pixel (row-major,
@@ -124,6 +125,7 @@ struct IntegrateArgs {
     unsigned* unit_list;           // live units: three lists (general, free, full free) of kListSegs segments (k_cull_units)
     unsigned* list_count;          // [3][kListSegs * kListCountStride] entries per segment (zeroed by the frame prepass)
     int free_ok;                   // free units allowed: gated colour with gate <= 1 (f == 1 updates sdf/weight only)
+    int color_wide;                // colour stored as int32 x 4 (else u8 x 4; see semtsdf_vol::color_wide)
 };
 
 // Association accumulators (fixed point, scale 2^28, deterministic).
@@ -238,13 +240,15 @@ size_t mask_scratch_bytes();
 size_t mask_scratch_kept_offset();
 hipError_t launch_brick_min(const VolGeom& g, const VolBufs& b, bool all, hipStream_t s);
 hipError_t launch_fill_volume(const VolGeom& g, const VolBufs& b, uint32_t flags, hipStream_t s);
+hipError_t launch_flush_lazy(const VolGeom& g, const VolBufs& b, hipStream_t s);  // lazy weights -> weights
 hipError_t launch_depth_pyramid(const uint16_t* depth, const uint8_t* rgb, uint8_t* mask, int w, int h,
                                 float scale, const DepthPyramid& p, unsigned* list_count, hipStream_t s,
                                 const uint8_t* lut = nullptr);  // lut: relabel the mask in place (k_relabel folded in)
 hipError_t launch_vox_chunk(const void* src, void* dst, bool to_ref, const VolGeom& g, uint64_t v0, uint64_t nv,
                             hipStream_t s);
-hipError_t launch_color_chunk(const void* src, void* dst, bool to_ref, bool i32, const VolGeom& g, uint64_t v0,
-                              uint64_t nv, hipStream_t s);
+hipError_t launch_color_widen(const uint8_t* narrow, int32_t* wide, uint64_t nvox, hipStream_t s);  // u8x4 -> i32x4
+hipError_t launch_color_chunk(const void* src, void* dst, bool to_ref, bool ref_i32, bool dev_i32, const VolGeom& g,
+                              uint64_t v0, uint64_t nv, hipStream_t s);
 hipError_t launch_integrate(const IntegrateArgs& a, hipStream_t s, hipEvent_t e0 = nullptr,
                             hipEvent_t e1 = nullptr);  // e0/e1: kernel start/end events (timing)
 uint64_t unit_count(const VolGeom& g);

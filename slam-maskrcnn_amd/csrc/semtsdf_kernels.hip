@@ -403,6 +403,27 @@ hipError_t launch_brick_min(const VolGeom& g, const VolBufs& b, bool all, hipStr
     return hipGetLastError();
 }
 
+// Folds the pending weight increments of steady lines into the weights (k_integrate's lazy
+// weights): one lane per voxel, the 32 voxels of a line in one half-wave, which reads the flag
+// byte before its first lane resets it (loads of one wave-instruction precede its stores).
+__global__ __launch_bounds__(256) void k_flush_lazy(int32_t* __restrict__ wt, uint8_t* __restrict__ sflag, uint64_t nvox) {
+    for (uint64_t v = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; v < nvox; v += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned f = sflag[v >> 5];
+        if (f > 1u) {
+            wt[v] += (int)f - 1;
+            if ((v & 31u) == 0u) sflag[v >> 5] = 1u;
+        }
+    }
+}
+
+hipError_t launch_flush_lazy(const VolGeom& g, const VolBufs& b, hipStream_t s) {
+    const uint64_t n = g.nvox;
+    if (n == 0) return hipSuccess;  // a shard that owns no chunk
+    const unsigned grid = (unsigned)((n + 255) / 256 < 65536 ? (n + 255) / 256 : 65536);
+    hipLaunchKernelGGL(k_flush_lazy, dim3(grid), dim3(256), 0, s, b.wt, b.sflag, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_fill_volume(const VolGeom& g, const VolBufs& b, uint32_t flags, hipStream_t s) {
     (void)flags;
     const uint64_t n = g.nvox;
@@ -579,9 +600,10 @@ __device__ __forceinline__ int floor_div(float a, float b) {
 
 // (c*w + x) / (w+1) for 0 <= c, x <= 255 via the float reciprocal plus one exact integer
 // correction (quotient <= 255, so the float estimate is within one of it); integer
-// division above w = 65535 where the numerator would leave the exact f32 range.
+// division (truncating, as the reference's int arithmetic) above w = 65535, where the
+// numerator would leave the exact f32 range, and for negative (uploaded) colours.
 __device__ __forceinline__ int avg_div(int num, int den) {
-    if (den > 65536) return num / den;
+    if (num < 0 || den > 65536) return num / den;  // the reference's truncating int quotient
     int q = (int)((float)num * __builtin_amdgcn_rcpf((float)den));
     if ((q + 1) * den <= num) ++q;
     else if (q * den > num) --q;
@@ -757,8 +779,12 @@ __host__ __device__ inline UnitGrid unit_grid(const VolGeom& g) {
 // b % kListSegs == c (one counter per segment, 256 B apart, keeps the same-address atomics
 // per counter to 1/64 of the workgroups).  Capacity of a segment: all units of its
 // workgroups.
+#ifndef SEMTSDF_CULL_ZRUN
+#define SEMTSDF_CULL_ZRUN 0  // cull (and list) order: 0 x runs, 1 memory order (z fastest)
+#endif
 __host__ __device__ inline unsigned list_seg_cap(const UnitGrid& ug) {
-    const unsigned groups = (ug.nux + 255u) / 256u * ug.nuy * ug.nuz;  // k_cull_units workgroups
+    const unsigned groups = SEMTSDF_CULL_ZRUN ? (ug.n + 255u) / 256u
+                                              : (ug.nux + 255u) / 256u * ug.nuy * ug.nuz;  // k_cull_units workgroups
     return (groups + kListSegs - 1u) / kListSegs * 256u;
 }
 
@@ -769,12 +795,22 @@ __host__ __device__ inline unsigned list_seg_cap(const UnitGrid& ug) {
 __global__ __launch_bounds__(256) void k_cull_units(IntegrateArgs a, UnitGrid ug, unsigned seg_cap) {
     __shared__ unsigned s_cnt[kLists][4];
     __shared__ unsigned s_base[kLists];
+#if SEMTSDF_CULL_ZRUN
+    // units in memory order (z fastest, then y, then x): consecutive list entries are adjacent
+    // half tiles, so an integrate wave's two units are one contiguous 1-KB tile per array
+    const unsigned lin = blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned uz = lin % ug.nuz, t = lin / ug.nuz, uy = t % ug.nuy, ux = t / ug.nuy;
+    const unsigned bid = blockIdx.x;
+    const bool inside = lin < ug.n;
+#else
     // grid (x runs of 256 units, uy, uz): no integer division by the runtime unit counts
     const unsigned ux = blockIdx.x * blockDim.x + threadIdx.x, uy = blockIdx.y, uz = blockIdx.z;
-    const unsigned u = pack_unit(ux, uy, uz);
     const unsigned bid = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    const bool inside = ux < ug.nux;
+#endif
+    const unsigned u = pack_unit(ux, uy, uz);
     int c = 1;  // dead
-    if (ux < ug.nux) c = a.cull ? unit_cull(a, (int)ux * UX, (int)uy * UY, (int)uz * UZ) : 0;
+    if (inside) c = a.cull ? unit_cull(a, (int)ux * UX, (int)uy * UY, (int)uz * UZ) : 0;
     const int lane = (int)(threadIdx.x & 63u), wv = (int)(threadIdx.x >> 6);
     // list of class c: 0 general (c == 0), 1 free (c == 2), 2 full free (c == 3)
     const unsigned long long bal0 = __ballot(c == 0), bal1 = __ballot(c == 2), bal2 = __ballot(c == 3);
@@ -802,8 +838,12 @@ __global__ __launch_bounds__(256) void k_cull_units(IntegrateArgs a, UnitGrid ug
 hipError_t launch_cull(const IntegrateArgs& a, hipStream_t s) {
     const UnitGrid ug = unit_grid(a.g);
     if (ug.n == 0) return hipSuccess;  // a shard that owns no chunk
+#if SEMTSDF_CULL_ZRUN
+    hipLaunchKernelGGL(k_cull_units, dim3((ug.n + 255) / 256), dim3(256), 0, s, a, ug, list_seg_cap(ug));
+#else
     hipLaunchKernelGGL(k_cull_units, dim3((ug.nux + 255) / 256, ug.nuy, ug.nuz), dim3(256), 0, s, a, ug,
                        list_seg_cap(ug));
+#endif
     return hipGetLastError();
 }
 
@@ -863,6 +903,18 @@ __device__ __forceinline__ uint64_t unit_tile(const VolGeom& g, const UnitPos& u
 #ifndef SEMTSDF_STEADY
 #define SEMTSDF_STEADY 1  // skip the sdf traffic of steady lines (Ld::skip)
 #endif
+// Lazy weights of steady lines.  A steady line (every sdf exactly 1.0f) whose 32 voxels are
+// all touched with f == 1 changes only its weights, each by +1, when the colour/histogram
+// gate rejects f == 1 (free_ok modes): the increment is kept as a per-line pending count in
+// the line's flag byte instead of a read-modify-write of the 128-B weight line (and the sdf
+// line is skipped as a steady line anyway).  Flag byte s: 0 = not steady; s >= 1 = steady with
+// s - 1 pending increments of every weight of the line.  Any other update of the line adds
+// the pending count first (stage_compute), and k_flush_lazy folds the counts into the weights
+// before they are read out (download, upload, checkpoint).
+#ifndef SEMTSDF_LAZY_WEIGHT
+#define SEMTSDF_LAZY_WEIGHT 1
+#endif
+constexpr unsigned kFlagMax = 255u;  // s - 1 <= 254 pending increments
 
 struct Proj {
     float qz[4];
@@ -896,6 +948,7 @@ __device__ __forceinline__ StoreMeta store_meta(const Cls& C) {
 
 struct Ld {
     bool skip;  // steady line: s4 not loaded, every value is 1.0f
+    bool lazy;  // steady line, all 32 voxels touched with f == 1: only the flag byte changes
     float4 s4;
     int4 w4;
     uint4 c8;
@@ -909,6 +962,7 @@ struct Out {
     float4 s4;
     int4 w4;
     bool skip;       // the line's sdf was neither loaded nor changes (steady line)
+    bool lazy;       // the line's weights take one more pending increment (flag byte + 1)
     unsigned oflag;  // the line's steady flag before this update
     bool cross;      // a voxel's sdf crossed the skip threshold (its brick's map entry may flip)
     uint4 c8;
@@ -1093,6 +1147,9 @@ __device__ __forceinline__ void stage_classify(const IntegrateArgs& a, const Pro
 #ifndef SEMTSDF_FULLROW
 #define SEMTSDF_FULLROW 1
 #endif
+#ifndef SEMTSDF_PIPE
+#define SEMTSDF_PIPE 1  // integrate_list software pipeline: 1 two-stage, 2 three-stage (one wait per iteration)
+#endif
 // Whole-line state traffic: a 128-B line of a per-voxel array is the 8 lanes of one
 // z-quad (lane % 8); when any of them updates, all 8 load and store it (unchanged values
 // included), so every line written back is fully dirty.
@@ -1172,9 +1229,13 @@ __device__ __forceinline__ void stage_load(const IntegrateArgs& a, const UnitPos
 #pragma unroll
     for (int k = 0; k < 4; ++k) fone &= (((C.tmask >> k) & 1u) == 0u) | (C.fv[k] == 1.0f);
     const bool skip = SEMTSDF_STEADY && tile_line_all((C.sflag != 0u) & fone);
+    // lazy: steady, every voxel of the line touched (f == 1), pending count below the cap
+    const bool lazy = SEMTSDF_STEADY && SEMTSDF_LAZY_WEIGHT && !VOTE && a.free_ok &&
+                      tile_line_all((C.sflag != 0u) & (C.sflag < kFlagMax) & fone & (C.tmask == 15u));
     L.skip = skip;
+    L.lazy = lazy;
     L.s4 = ld_state<float4>(skip ? reinterpret_cast<const float*>(dummy) : a.b.sdf + ub + lt);
-    L.w4 = ld_state<int4>(a.b.wt + ub + lt);
+    L.w4 = ld_state<int4>(lazy ? reinterpret_cast<const int*>(dummy) : a.b.wt + ub + lt);
     if (FREE) return;  // sdf and weight only
     if (CI32) {
 #pragma unroll
@@ -1201,8 +1262,11 @@ __device__ __forceinline__ void stage_compute(const IntegrateArgs& a, const floa
     const float so[4] = {L.skip ? 1.0f : L.s4.x, L.skip ? 1.0f : L.s4.y, L.skip ? 1.0f : L.s4.z,
                          L.skip ? 1.0f : L.s4.w};
     O.skip = L.skip;
+    O.lazy = L.lazy;
     O.oflag = C.sflag;
-    const int wo[4] = {L.w4.x, L.w4.y, L.w4.z, L.w4.w};
+    // the stored weights plus the line's pending increments (0 unless the line is steady)
+    const int pend = (SEMTSDF_STEADY && SEMTSDF_LAZY_WEIGHT && C.sflag) ? (int)C.sflag - 1 : 0;
+    const int wo[4] = {L.w4.x + pend, L.w4.y + pend, L.w4.z + pend, L.w4.w + pend};
     float sn[4];
     int wn[4];
     unsigned uslow = 0;
@@ -1305,9 +1369,9 @@ __device__ __forceinline__ void stage_compute(const IntegrateArgs& a, const floa
     }
 }
 
-template <bool SEM, bool CI32, bool VOTE, bool FREE>
+template <bool SEM, bool CI32, bool VOTE, bool FREE, bool COUNT>
 __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPos& up, unsigned coff,
-                                            const StoreMeta& M, const Out& O) {
+                                            const StoreMeta& M, const Out& O, unsigned& n_lazy) {
     const VolGeom& g = a.g;
     const unsigned tmask = M.meta & 15u, gmask = (M.meta >> 4) & 15u, hmode = (M.meta >> 8) & 3u,
                    hlab = M.meta >> 16;
@@ -1333,15 +1397,18 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
             }
         }
     }
-    if (!(kProbes && a.debug == 10)) {  // 10: timing probe, loads but no sdf/weight stores
+    if (COUNT && O.lazy) n_lazy += 4u;
+    if (!(kProbes && a.debug == 10) && !O.lazy) {  // 10: timing probe, loads but no sdf/weight stores
         if (!O.skip) st_state(a.b.sdf + v, O.s4);
         st_state(a.b.wt + v, O.w4);
     }
-    if (SEMTSDF_STEADY) {  // the line's steady flag after this update (one lane per line writes)
+    if (SEMTSDF_STEADY) {  // the line's flag byte after this update (one lane per line writes)
         const bool one = (O.s4.x == 1.0f) & (O.s4.y == 1.0f) & (O.s4.z == 1.0f) & (O.s4.w == 1.0f) &
                          (O.w4.x < (1 << 23)) & (O.w4.y < (1 << 23)) & (O.w4.z < (1 << 23)) & (O.w4.w < (1 << 23));
-        const bool nflag = tile_line_all(one);
-        if (lane_y((int)__lane_id()) == 0 && nflag != (O.oflag != 0u)) a.b.sflag[v >> 5] = nflag ? 1u : 0u;
+        // a lazy line counts one more pending increment; any other update stored the weights
+        // with the pending count folded in: steady (1) or not (0)
+        const unsigned nb = O.lazy ? O.oflag + 1u : (tile_line_all(one) ? 1u : 0u);
+        if (lane_y((int)__lane_id()) == 0 && nb != O.oflag) a.b.sflag[v >> 5] = (uint8_t)nb;
     }
     if (!FREE && grow) {
         if (CI32) {
@@ -1394,7 +1461,8 @@ template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT, bool SHARD, boo
 __device__ __forceinline__ unsigned integrate_list(const IntegrateArgs& a, const UnitGrid& ug, unsigned seg_cap,
                                                    const float* __restrict__ s_rcp, const unsigned* list,
                                                    const unsigned* list_count, unsigned wave, unsigned nwaves,
-                                                   unsigned rot, unsigned& n_touch, unsigned& n_gate) {
+                                                   unsigned rot, unsigned& n_touch, unsigned& n_gate,
+                                                   unsigned& n_lazy) {
     const int lane = threadIdx.x & 63;
     // the lane's offset from the unit origin (a volume has < 2^31 stored voxels per x-plane pair)
     const unsigned coff = (unsigned)lane_zq(lane) * 32u + (unsigned)lane_y(lane) * 4u;  // lane's offset in its unit
@@ -1441,7 +1509,46 @@ __device__ __forceinline__ unsigned integrate_list(const IntegrateArgs& a, const
         return p;
     };
     unsigned i = (wave + nwaves - rot % nwaves) % nwaves;
-    if (i < ngroups) {
+    if (SEMTSDF_PIPE == 2 && i < ngroups) {
+        // Deeper pipeline: at the top of iteration i one wait covers everything the previous
+        // iteration issued (the state loads of unit k issued a whole iteration earlier, the
+        // pixel gathers of unit k+1 half an iteration earlier, the stores of unit k-1), then
+        //   classify(k+1)  load(k+1)  project(k+2)  compute(k)  store(k)
+        // so the state loads of k+1 and the gathers of k+2 are in flight under the compute and
+        // store of k.  The last iteration classifies, loads and projects copies of the current
+        // units (not counted), so every iteration issues the same memory operations.
+        unsigned e[kSlots], en[kSlots];
+        group_entries(i, e);
+        UnitPos cur = lane_pos(e);
+        if (i + nwaves < ngroups) group_entries(i + nwaves, en);
+        Proj P;
+        Cls C, Cn;
+        Ld L, Ln;
+        Out O;
+        stage_project<SHARD, PIN, FREE, FULL>(a, cur, lane, P);
+        stage_classify<SEM, GATE, VOTE, COUNT, FREE>(a, P, C, true, n_touch, n_gate);
+        stage_load<SEM, CI32, VOTE, FREE>(a, cur, coff, C, L);
+        UnitPos n1 = (i + nwaves < ngroups) ? lane_pos(en) : cur;
+        if (i + 2u * nwaves < ngroups) group_entries(i + 2u * nwaves, en);
+        stage_project<SHARD, PIN, FREE, FULL>(a, n1, lane, P);
+        while (true) {
+            const bool has1 = i + nwaves < ngroups;
+            const UnitPos n2 = (i + 2u * nwaves < ngroups) ? lane_pos(en) : n1;
+            if (i + 3u * nwaves < ngroups) group_entries(i + 3u * nwaves, en);
+            stage_classify<SEM, GATE, VOTE, COUNT, FREE>(a, P, Cn, has1, n_touch, n_gate);
+            stage_load<SEM, CI32, VOTE, FREE>(a, n1, coff, Cn, Ln);
+            stage_project<SHARD, PIN, FREE, FULL>(a, n2, lane, P);
+            stage_compute<SEM, GATE, CI32, VOTE, FREE>(a, s_rcp, C, L, O);
+            const StoreMeta Mc = store_meta(C);
+            stage_store<SEM, CI32, VOTE, FREE, COUNT>(a, cur, coff, Mc, O, n_lazy);
+            if (!has1) break;
+            C = Cn;
+            L = Ln;
+            cur = n1;
+            n1 = n2;
+            i += nwaves;
+        }
+    } else if (i < ngroups) {
         unsigned e[kSlots], en[kSlots];
         group_entries(i, e);
         UnitPos cur = lane_pos(e);
@@ -1463,7 +1570,7 @@ __device__ __forceinline__ unsigned integrate_list(const IntegrateArgs& a, const
             if (SEMTSDF_FULLROW || C.tmask) stage_compute<SEM, GATE, CI32, VOTE, FREE>(a, s_rcp, C, L, O);
             const StoreMeta Mc = store_meta(C);
             stage_classify<SEM, GATE, VOTE, COUNT, FREE>(a, P, C, has, n_touch, n_gate);
-            stage_store<SEM, CI32, VOTE, FREE>(a, cur, coff, Mc, O);
+            stage_store<SEM, CI32, VOTE, FREE, COUNT>(a, cur, coff, Mc, O, n_lazy);
             if (!has) break;
             stage_load<SEM, CI32, VOTE, FREE>(a, nxt, coff, C, L);
             cur = nxt;
@@ -1487,16 +1594,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
     const int lane = threadIdx.x & 63;
     const unsigned wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     const unsigned nwaves = gridDim.x * (blockDim.x >> 6);
-    unsigned n_touch = 0, n_gate = 0;
+    unsigned n_touch = 0, n_gate = 0, n_lazy = 0;
     unsigned rot = 0, nlive = 0;
     if (GATE && !VOTE) {  // free units exist only in gated modes (free_ok)
         const unsigned n1 = integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, true, false>(
             a, ug, seg_cap, s_rcp, a.unit_list + (size_t)kListSegs * seg_cap, a.list_count + kListSegs * kListCountStride,
-            wave, nwaves, 0u, n_touch, n_gate);
+            wave, nwaves, 0u, n_touch, n_gate, n_lazy);
         const unsigned g1 = (n1 + kSlots - 1) / kSlots;
         const unsigned n2 = integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, true, true>(
             a, ug, seg_cap, s_rcp, a.unit_list + (size_t)2 * kListSegs * seg_cap,
-            a.list_count + 2 * kListSegs * kListCountStride, wave, nwaves, g1 % nwaves, n_touch, n_gate);
+            a.list_count + 2 * kListSegs * kListCountStride, wave, nwaves, g1 % nwaves, n_touch, n_gate, n_lazy);
         rot = (g1 + (n2 + kSlots - 1) / kSlots) % nwaves;
         if (COUNT && blockIdx.x == 0 && threadIdx.x == 0) {
             atomicAdd(a.counters + 4, (unsigned long long)(n1 + n2));
@@ -1505,17 +1612,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
         if (COUNT) nlive += n1 + n2;
     }
     const unsigned n0 = integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, false>(
-        a, ug, seg_cap, s_rcp, a.unit_list, a.list_count, wave, nwaves, rot, n_touch, n_gate);
+        a, ug, seg_cap, s_rcp, a.unit_list, a.list_count, wave, nwaves, rot, n_touch, n_gate, n_lazy);
     if (COUNT) {
         nlive += n0;
-        unsigned long long t = n_touch, gg = n_gate;
+        unsigned long long t = n_touch, gg = n_gate, lz = n_lazy;
         for (int off = 32; off > 0; off >>= 1) {
             t += __shfl_xor(t, off, 64);
             gg += __shfl_xor(gg, off, 64);
+            lz += __shfl_xor(lz, off, 64);
         }
         if (lane == 0) {
             if (t) atomicAdd(a.counters + 0, t);
             if (gg) atomicAdd(a.counters + 1, gg);
+            if (lz) atomicAdd(a.counters + 6, lz);
         }
         // live units of both lists
         if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.counters + 3, (unsigned long long)nlive);
@@ -1580,7 +1689,10 @@ static hipError_t launch_integrate_t(const IntegrateArgs& a, bool count, hipStre
 
 hipError_t launch_integrate(const IntegrateArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const bool count = a.counters != nullptr && (a.flags & 0x80000000u);
-    const bool sem = a.flags & 0x1u, gate = a.flags & 0x2u, ci32 = a.flags & 0x4u, vote = a.flags & 0x8u;
+    // ci32: the colour STORAGE is int32 x 4 (a COLOR_I32 volume holding values outside [0, 255]);
+    // a COLOR_I32 volume whose colours fit a byte stores them as u8 x 4 and integrates them
+    // with the same integer quotient (semtsdf_api.cpp: color_wide)
+    const bool sem = a.flags & 0x1u, gate = a.flags & 0x2u, ci32 = a.color_wide != 0, vote = a.flags & 0x8u;
     // Instantiated mode combinations: SfM semantic (u8 colour, gated), TSDF+colour (NumPy
     // rule: i32 colour, ungated), TSDF_Python vote, plus their neighbours.
     if (vote) {
@@ -3048,40 +3160,63 @@ hipError_t launch_vox_chunk(const void* src, void* dst, bool to_ref, const VolGe
 }
 
 // colour: device storage is padded to 4 channels (u8x4 / i32x4), the reference layout has 3
-template <typename T>
-__global__ __launch_bounds__(256) void k_color_to_ref(VolGeom g, const T* __restrict__ dev, T* __restrict__ ref,
+// TD: device storage element, TR: reference-layout element (int32 boundary of a COLOR_I32
+// volume stored as bytes: values in [0, 255], checked by the host before an upload)
+template <typename TD, typename TR>
+__global__ __launch_bounds__(256) void k_color_to_ref(VolGeom g, const TD* __restrict__ dev, TR* __restrict__ ref,
                                                       uint64_t v0, uint64_t nv) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv * 3; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t v = v0 + i / 3, c = i % 3;
-        ref[i] = dev[tile_of_ref(g, v) * 4 + c];
+        ref[i] = (TR)dev[tile_of_ref(g, v) * 4 + c];
     }
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void k_color_from_ref(VolGeom g, const T* __restrict__ ref, T* __restrict__ dev,
+template <typename TD, typename TR>
+__global__ __launch_bounds__(256) void k_color_from_ref(VolGeom g, const TR* __restrict__ ref, TD* __restrict__ dev,
                                                         uint64_t v0, uint64_t nv) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv * 3; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t v = v0 + i / 3, c = i % 3;
-        dev[tile_of_ref(g, v) * 4 + c] = ref[i];
+        dev[tile_of_ref(g, v) * 4 + c] = (TD)ref[i];
     }
 }
 
-hipError_t launch_color_chunk(const void* src, void* dst, bool to_ref, bool i32, const VolGeom& g, uint64_t v0,
-                              uint64_t nv, hipStream_t s) {
+__global__ __launch_bounds__(256) void k_color_widen(const uint32_t* __restrict__ narrow, int4* __restrict__ wide,
+                                                     uint64_t nvox) {
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvox; v += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t c = narrow[v];
+        wide[v] = make_int4((int)(c & 0xFFu), (int)((c >> 8) & 0xFFu), (int)((c >> 16) & 0xFFu), 0);
+    }
+}
+
+hipError_t launch_color_widen(const uint8_t* narrow, int32_t* wide, uint64_t nvox, hipStream_t s) {
+    if (nvox == 0) return hipSuccess;
+    uint64_t blocks = (nvox + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(k_color_widen, dim3((unsigned)blocks), dim3(256), 0, s, reinterpret_cast<const uint32_t*>(narrow),
+                       reinterpret_cast<int4*>(wide), nvox);
+    return hipGetLastError();
+}
+
+template <typename TD, typename TR>
+static void color_chunk_t(const void* src, void* dst, bool to_ref, const VolGeom& g, uint64_t v0, uint64_t nv,
+                          dim3 gr, hipStream_t s) {
+    if (to_ref)
+        hipLaunchKernelGGL((k_color_to_ref<TD, TR>), gr, dim3(256), 0, s, g, (const TD*)src, (TR*)dst, v0, nv);
+    else
+        hipLaunchKernelGGL((k_color_from_ref<TD, TR>), gr, dim3(256), 0, s, g, (const TR*)src, (TD*)dst, v0, nv);
+}
+
+hipError_t launch_color_chunk(const void* src, void* dst, bool to_ref, bool ref_i32, bool dev_i32, const VolGeom& g,
+                              uint64_t v0, uint64_t nv, hipStream_t s) {
     uint64_t blocks = (nv * 3 + 255) / 256;
     if (blocks > 16384) blocks = 16384;
-    const dim3 gr((unsigned)blocks), bl(256);
-    if (i32) {
-        if (to_ref)
-            hipLaunchKernelGGL(k_color_to_ref<int32_t>, gr, bl, 0, s, g, (const int32_t*)src, (int32_t*)dst, v0, nv);
-        else
-            hipLaunchKernelGGL(k_color_from_ref<int32_t>, gr, bl, 0, s, g, (const int32_t*)src, (int32_t*)dst, v0, nv);
-    } else {
-        if (to_ref)
-            hipLaunchKernelGGL(k_color_to_ref<uint8_t>, gr, bl, 0, s, g, (const uint8_t*)src, (uint8_t*)dst, v0, nv);
-        else
-            hipLaunchKernelGGL(k_color_from_ref<uint8_t>, gr, bl, 0, s, g, (const uint8_t*)src, (uint8_t*)dst, v0, nv);
-    }
+    const dim3 gr((unsigned)blocks);
+    if (dev_i32)
+        color_chunk_t<int32_t, int32_t>(src, dst, to_ref, g, v0, nv, gr, s);
+    else if (ref_i32)
+        color_chunk_t<uint8_t, int32_t>(src, dst, to_ref, g, v0, nv, gr, s);
+    else
+        color_chunk_t<uint8_t, uint8_t>(src, dst, to_ref, g, v0, nv, gr, s);
     return hipGetLastError();
 }
 

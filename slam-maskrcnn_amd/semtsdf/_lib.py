@@ -109,6 +109,7 @@ class Timing(C.Structure):
         ("n_prep", C.c_uint64),
         ("free_units", C.c_uint64),
         ("full_units", C.c_uint64),
+        ("lazy_voxels", C.c_uint64),
     ]
 
 

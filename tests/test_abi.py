@@ -27,7 +27,7 @@ def test_library_exports_every_symbol():
     lib = L.load()
     for n in declared():
         assert hasattr(lib, n), n
-    assert lib.semtsdf_abi_version() == 5
+    assert lib.semtsdf_abi_version() == 6
 
 
 def test_structs_match_header_sizes():
@@ -38,3 +38,5 @@ def test_structs_match_header_sizes():
     # semtsdf_params: 3 i32 + 13 f32 + 32 f32 + 2 i32 + 5 f32 + u32 + 3 i32
     assert C.sizeof(L.Params) == 4 * (3 + 9 + 1 + 32 + 2 + 5 + 1 + 3)
     assert C.sizeof(L.AssocStats) == 4 * (2 + 32 + 32) + 256
+    # semtsdf_timing: 5 doubles-or-u64 groups of 8 bytes each, 14 fields
+    assert C.sizeof(L.Timing) == 8 * 14

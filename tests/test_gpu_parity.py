@@ -923,3 +923,63 @@ def test_association_30_frames_f32_pixel_order_rule(S, oracle):
             json.dump(rep, f)
     assert min(gaps) > 1e-6 and min(thr_gaps) > 1e-6
     vol.close()
+
+
+def test_full_size_256_c2_mode(S, oracle, stream):
+    """C2 at its full size: 256^3 TSDF + colour with the NumPy rule (int32 colour, ungated,
+    flags 0x4), 4 frames of the synthetic stream, culling on: sdf bits, weights and colours
+    identical to the exhaustive C oracle (x-slabs in threads)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    st, frames = stream
+    p, vol, g, ost = make(S, oracle, (256, 256, 256), frames[0], 0x4)
+    slabs = [(x, x + 32) for x in range(0, 256, 32)]
+    touched = 0
+    with ThreadPoolExecutor(8) as ex:
+        for k in range(1, 5):
+            fr = frames[k]
+            E = (fr.w2c @ frames[0].c2w).astype(np.float32)
+            vol.integrate(fr.depth, fr.rgb, None, E)
+            counts = list(ex.map(lambda r: oracle.integrate(g, ost, list(p.K), E, fr.depth, fr.rgb, None, flags=0x4,
+                                                            x_range=r), slabs))
+            touched += sum(int(c[0]) for c in counts)
+    assert touched > 1_000_000
+    assert_same(vol, ost)
+    vol.close()
+
+
+def test_color_i32_storage_widening(S, oracle, stream):
+    """COLOR_I32 volumes (the NumPy rule's int32 colours) store bytes while every colour fits
+    [0, 255] and switch to int32 storage when an upload brings other values (negative, > 255)
+    or when a weight could reach 2^23 (where the reference's int32 mean wraps).  Integrating
+    across both switches stays bit-identical to the oracle's int32 arithmetic."""
+    st, frames = stream
+    semtsdf, L = S
+    dims = (64, 64, 64)
+    for case in ("values", "weights"):
+        p, vol, g, ost = make(S, oracle, dims, frames[0], 0x4)
+        for k in (1, 2):
+            fr = frames[k]
+            E = (fr.w2c @ frames[0].c2w).astype(np.float32)
+            vol.integrate(fr.depth, fr.rgb, None, E)
+            oracle.integrate(g, ost, list(p.K), E, fr.depth, fr.rgb, None, flags=0x4)
+        assert_same(vol, ost)
+        narrow_bytes = vol.state().device_bytes
+        rng = np.random.default_rng(17)
+        if case == "values":  # out-of-byte colours on a few voxels
+            c = ost.color.reshape(-1, 3)
+            idx = rng.choice(c.shape[0], 5000, replace=False)
+            c[idx] = rng.integers(-3000, 3000, (idx.size, 3), dtype=np.int32)
+            vol.upload(color=ost.color)
+        else:  # weights just below the wrap bound
+            ost.wt[:] = np.where(ost.wt > 0, (1 << 23) - 2 + rng.integers(0, 2, ost.wt.size), 0).astype(np.int32)
+            vol.upload(wt=ost.wt)
+        for k in (3, 4, 5):
+            fr = frames[k]
+            E = (fr.w2c @ frames[0].c2w).astype(np.float32)
+            vol.integrate(fr.depth, fr.rgb, None, E)
+            oracle.integrate(g, ost, list(p.K), E, fr.depth, fr.rgb, None, flags=0x4)
+        assert vol.state().device_bytes > narrow_bytes, case  # int32 storage now
+        assert_same(vol, ost)
+        assert (ost.color < 0).any() or (ost.wt >= (1 << 23)).any(), case
+        vol.close()
