@@ -776,6 +776,8 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true", help="skip pipeline, orbit, C2 and C4-single")
     ap.add_argument("--no-c4", action="store_true", help="skip the 1024^3 single-GPU C4 measurement")
     ap.add_argument("--no-cull", action="store_true", help="debug: disable unit culling")
+    ap.add_argument("--async-prepass", action="store_true",
+                    help="C3 step: frame prepass on the volume's prep stream (overlap probe; measured no faster)")
     ap.add_argument("--only", choices=["pipeline", "masks", "c2", "c4"], default=None,
                     help="debug: run one section alone and print its record")
     ap.add_argument("--cpu-planes", type=int, default=64)
@@ -898,7 +900,10 @@ def main():
 
     def step(k):
         i = k % len(frames)
-        vol.integrate_dev(dbuf.ptr + i * NPX * 2, rbuf.ptr + i * NPX * 3, mbuf.ptr + i * NPX, Es[i])
+        if args.async_prepass:  # the prepass on the volume's prep stream (semtsdf_integrate_dev_async)
+            vol.integrate_dev_async(dbuf.ptr + i * NPX * 2, rbuf.ptr + i * NPX * 3, mbuf.ptr + i * NPX, Es[i])
+        else:
+            vol.integrate_dev(dbuf.ptr + i * NPX * 2, rbuf.ptr + i * NPX * 3, mbuf.ptr + i * NPX, Es[i])
 
     elapsed, tm, tc = timed_integrate(vol, step, args.steps, args.warmup)
     kern_ms = tm.integrate_ms / max(tm.n_integrate, 1)

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SEMTSDF_ABI_VERSION 6
+#define SEMTSDF_ABI_VERSION 7
 #define SEMTSDF_MAX_OBJECTS 32 /* tsdf.cuh:4 */
 
 /* ---- status codes ------------------------------------------------------------ */
@@ -155,6 +155,14 @@ int semtsdf_integrate(semtsdf_vol* v, const uint16_t* depth, const uint8_t* rgb,
 /* Same with device pointers (inputs already resident in HBM). */
 int semtsdf_integrate_dev(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d,
                           const uint8_t* mask_d, const float E[16], void* stream);
+/* As semtsdf_integrate_dev, with the frame prepass (pixel records, depth pyramid, unit
+ * cull) on the volume's own prep stream, ordered only after inputs_ready (a hipEvent_t
+ * marking the inputs complete; NULL: the inputs are already complete) and after the
+ * integrate two frames back -- not after the earlier work of `stream` -- so it overlaps the
+ * previous frame's integrate.  The integrate itself is ordered on `stream` as usual.  The
+ * inputs must stay unchanged until this frame's integrate has run. */
+int semtsdf_integrate_dev_async(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d,
+                                const uint8_t* mask_d, const float E[16], void* inputs_ready, void* stream);
 /* Label-vote mode input (TSDF_Python/tsdf.cu:48-57): cls is int32 [H*W]. */
 int semtsdf_integrate_vote_dev(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d,
                                const int32_t* cls_d, const float E[16], void* stream);

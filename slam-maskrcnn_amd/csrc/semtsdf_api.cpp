@@ -76,7 +76,20 @@ struct semtsdf_vol {
     uint8_t* rgb_d = nullptr;
     uint8_t* mask_d = nullptr;
     int32_t* cls_d = nullptr;
-    DepthPyramid pyr{};
+    // Per-frame prepass outputs (pixel records + depth pyramid, live-unit lists), two sets
+    // used in turn: the prepass of frame k+1 may run on prep_stream while the integrate of
+    // frame k still reads the other set (semtsdf_integrate_dev_async).
+    struct FrameSet {
+        DepthPyramid pyr{};
+        unsigned* unit_list = nullptr;   // live units of the frame (cull pass)
+        unsigned* list_count = nullptr;  // [kLists][kListSegs * kListCountStride] (general, free, full free)
+        hipEvent_t prep_done = nullptr;  // the set's prepass finished (prep_stream)
+        hipEvent_t set_free = nullptr;   // the integrate reading the set finished (recorded once async is in use)
+        bool free_recorded = false;
+    } fs[2];
+    int next_set = 0;
+    hipStream_t prep_stream = nullptr;   // created on the first asynchronous integrate
+    bool async_used = false;
     // association state
     AssocTables* tables_d = nullptr;
     AssocDecision* decision_d = nullptr;
@@ -87,8 +100,6 @@ struct semtsdf_vol {
     uint8_t* render_d = nullptr;
     float* render_t_d = nullptr;
     unsigned long long* counters_d = nullptr;
-    unsigned* unit_list_d = nullptr;  // live units of the frame (cull pass)
-    unsigned* list_count_d = nullptr; // [kLists][kListSegs * kListCountStride] (general, free, full free)
     float* rcp_table_d = nullptr;    // RN(1/n), n = 1..kRcpTable
     AssocDecision* decision_h = nullptr;  // pinned
     // Z-sharded raycast protocol (allocated on first use)
@@ -139,15 +150,22 @@ int dev_alloc(semtsdf_vol* v, void** p, size_t bytes) {
 
 void free_all(semtsdf_vol* v) {
     void* ptrs[] = {v->b.sdf, v->b.wt, v->b.bmin, v->b.bplain, v->b.sbmin, v->b.bdist, v->b.boct, v->b.botmp, v->b.bdirty, v->b.dlist, v->b.sflag, v->b.color, v->b.hist, v->b.hmask, v->b.cls, v->b.cls_cnt, v->depth_d, v->rgb_d,
-                    v->mask_d, v->cls_d, v->pyr.px, v->pyr.l0, v->pyr.l1, v->tables_d, v->decision_d,
+                    v->mask_d, v->cls_d, v->fs[0].pyr.px, v->fs[0].pyr.l0, v->fs[0].pyr.l1, v->fs[1].pyr.px,
+                    v->fs[1].pyr.l0, v->fs[1].pyr.l1, v->tables_d, v->decision_d,
                     v->num_objs_d, v->probs_d, v->box_d, v->palette_d, v->render_d, v->render_t_d,
-                    v->counters_d, v->ray_state_d, v->unit_list_d, v->list_count_d, v->rcp_table_d};
+                    v->counters_d, v->ray_state_d, v->fs[0].unit_list, v->fs[0].list_count, v->fs[1].unit_list,
+                    v->fs[1].list_count, v->rcp_table_d};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (v->decision_h) (void)hipHostFree(v->decision_h);
     for (auto* vec : {&v->ev_integrate, &v->ev_assoc, &v->ev_render, &v->ev_prep})
         for (auto& e : *vec) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
     if (v->bmin_ev) (void)hipEventDestroy(v->bmin_ev);
+    for (auto& f : v->fs) {
+        if (f.prep_done) (void)hipEventDestroy(f.prep_done);
+        if (f.set_free) (void)hipEventDestroy(f.set_free);
+    }
+    if (v->prep_stream) (void)hipStreamDestroy(v->prep_stream);
     if (v->stream) (void)hipStreamDestroy(v->stream);
 }
 
@@ -280,8 +298,12 @@ int widen_color(semtsdf_vol* v, hipStream_t s) {
 }
 
 
+// async: the frame prepass runs on the volume's prep stream, ordered after inputs_ready (when
+// given) and after the integrate that last read its frame set -- not after the earlier work
+// of stream s -- so it may overlap the previous frame's integrate.
 int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d, const uint8_t* mask_d,
-                   const int32_t* cls_d, const float E[16], hipStream_t s) {
+                   const int32_t* cls_d, const float E[16], hipStream_t s, bool async = false,
+                   hipEvent_t inputs_ready = nullptr) {
     if (!E) return fail(SEMTSDF_ERR_INVALID, "E is NULL");
     if (!depth_d || !rgb_d) return fail(SEMTSDF_ERR_INVALID, "depth/rgb is NULL");
     if ((v->p.flags & SEMTSDF_F_SEMANTIC) && !mask_d) return fail(SEMTSDF_ERR_INVALID, "semantic volume needs a mask");
@@ -315,10 +337,12 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
     a.rgb = rgb_d;
     a.mask = mask_d;
     a.cls = cls_d;
-    a.pyr = v->pyr;
+    const int fset = v->next_set;
+    semtsdf_vol::FrameSet& F = v->fs[fset];
+    a.pyr = F.pyr;
     a.counters = v->counters_d;
-    a.unit_list = v->unit_list_d;
-    a.list_count = v->list_count_d;
+    a.unit_list = F.unit_list;
+    a.list_count = F.list_count;
     a.rcp_table = v->rcp_table_d;
     screen_map(a);
     a.pinhole = (a.K[1] == 0.0f && a.K[3] == 0.0f && a.K[6] == 0.0f && a.K[7] == 0.0f && a.K[8] == 1.0f) ? 1 : 0;
@@ -332,18 +356,46 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
                     ? 1
                     : 0;
     if (a.debug == 2) return SEMTSDF_OK;
-    if (int rc = after_bmin(v, s)) return rc;
-    v->wmax_bound += 1;
-    EventPair epp;
-    timing_begin(v, v->ev_prep, s, &epp);
-    // a deferred relabel of this frame's association is applied by the prepass (in place)
+    // a deferred relabel of this frame's association is applied by the prepass (in place):
+    // that prepass follows the association on s
     const uint8_t* lut = mask_d ? v->pending_lut : nullptr;
     v->pending_lut = nullptr;
+    if (lut) async = false;
+    if (async && !v->prep_stream) {
+        int lo = 0, hi = 0;
+        if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
+        HIPC(hipStreamCreateWithPriority(&v->prep_stream, hipStreamNonBlocking, hi));
+        for (auto& f : v->fs) {
+            HIPC(hipEventCreateWithFlags(&f.prep_done, hipEventDisableTiming));
+            HIPC(hipEventCreateWithFlags(&f.set_free, hipEventDisableTiming));
+        }
+    }
+    hipStream_t ps = s;
+    if (async) {
+        ps = v->prep_stream;
+        v->async_used = true;
+        if (inputs_ready) HIPC(hipStreamWaitEvent(ps, inputs_ready, 0));
+        if (!F.free_recorded) {  // the set's last reader is unknown (first asynchronous frame): all of s
+            HIPC(hipEventRecord(F.set_free, s));
+            F.free_recorded = true;
+        }
+        HIPC(hipStreamWaitEvent(ps, F.set_free, 0));
+    }
+    v->next_set ^= 1;
+    EventPair epp;
+    timing_begin(v, v->ev_prep, ps, &epp);
     HIPC(launch_depth_pyramid(depth_d, rgb_d, const_cast<uint8_t*>(mask_d), v->p.width, v->p.height, v->p.depth_scale,
-                              v->pyr, v->list_count_d, s, lut));
-    HIPC(launch_cull(a, s));
-    timing_end(v, v->ev_prep, s, &epp);
+                              F.pyr, F.list_count, ps, lut));
+    HIPC(launch_cull(a, ps));
+    timing_end(v, v->ev_prep, ps, &epp);
     v->n_prep++;
+    if (async) {
+        HIPC(hipEventRecord(F.prep_done, ps));
+        HIPC(hipStreamWaitEvent(s, F.prep_done, 0));
+    }
+    // the volume's writer: after the last empty-space map update
+    if (int rc = after_bmin(v, s)) return rc;
+    v->wmax_bound += 1;
     // timing: the integrate kernel's own start/end (events recorded by its dispatch, the
     // duration rocprofv3 reports for the same kernel)
     EventPair ep{nullptr, nullptr};
@@ -351,6 +403,10 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
         ep.a = ep.b = nullptr;
     HIPC(launch_integrate(a, s, ep.a, ep.b));
     if (ep.a) v->ev_integrate.push_back(ep);
+    if (v->async_used) {  // a later asynchronous prepass into this set waits for this integrate
+        HIPC(hipEventRecord(F.set_free, s));
+        F.free_recorded = true;
+    }
     v->bmin_dirty = true;
     v->n_integrate++;
     return SEMTSDF_OK;
@@ -750,16 +806,18 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     if ((rc = dev_alloc(v, (void**)&v->depth_d, px * 2))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->rgb_d, px * 3))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->mask_d, px))) return bail(rc);
-    DepthPyramid& pyr = v->pyr;
-    pyr.w0 = (p->width + 7) / 8; pyr.h0 = (p->height + 7) / 8;
-    pyr.w1 = (p->width + 31) / 32; pyr.h1 = (p->height + 31) / 32;
-    if ((rc = dev_alloc(v, (void**)&pyr.px, (px + 1) * 8))) return bail(rc);
-    if (hipMemset(pyr.px, 0, (px + 1) * 8) != hipSuccess) return bail(fail(SEMTSDF_ERR_HIP, "memset failed"));
-    if ((rc = dev_alloc(v, (void**)&pyr.l0, (size_t)pyr.w1 * 4 * pyr.h1 * 4 * sizeof(uint2)))) return bail(rc);
-    if ((rc = dev_alloc(v, (void**)&pyr.l1, (size_t)pyr.w1 * pyr.h1 * sizeof(uint2)))) return bail(rc);
-    if ((rc = dev_alloc(v, (void**)&v->unit_list_d, unit_list_capacity(g) * sizeof(unsigned)))) return bail(rc);
-    if ((rc = dev_alloc(v, (void**)&v->list_count_d, kLists * kListSegs * kListCountStride * sizeof(unsigned))))
-        return bail(rc);
+    for (auto& f : v->fs) {
+        DepthPyramid& pyr = f.pyr;
+        pyr.w0 = (p->width + 7) / 8; pyr.h0 = (p->height + 7) / 8;
+        pyr.w1 = (p->width + 31) / 32; pyr.h1 = (p->height + 31) / 32;
+        if ((rc = dev_alloc(v, (void**)&pyr.px, (px + 1) * 8))) return bail(rc);
+        if (hipMemset(pyr.px, 0, (px + 1) * 8) != hipSuccess) return bail(fail(SEMTSDF_ERR_HIP, "memset failed"));
+        if ((rc = dev_alloc(v, (void**)&pyr.l0, (size_t)pyr.w1 * 4 * pyr.h1 * 4 * sizeof(uint2)))) return bail(rc);
+        if ((rc = dev_alloc(v, (void**)&pyr.l1, (size_t)pyr.w1 * pyr.h1 * sizeof(uint2)))) return bail(rc);
+        if ((rc = dev_alloc(v, (void**)&f.unit_list, unit_list_capacity(g) * sizeof(unsigned)))) return bail(rc);
+        if ((rc = dev_alloc(v, (void**)&f.list_count, kLists * kListSegs * kListCountStride * sizeof(unsigned))))
+            return bail(rc);
+    }
     if ((rc = dev_alloc(v, (void**)&v->rcp_table_d, kRcpTable * sizeof(float)))) return bail(rc);
     {
         float t[kRcpTable];
@@ -869,6 +927,13 @@ int semtsdf_integrate_dev(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t
                           const float E[16], void* stream) {
     if (!v) return fail(SEMTSDF_ERR_INVALID, "NULL handle");
     return integrate_impl(v, depth_d, rgb_d, mask_d, nullptr, E, pick(v, stream));
+}
+
+int semtsdf_integrate_dev_async(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d, const uint8_t* mask_d,
+                                const float E[16], void* inputs_ready, void* stream) {
+    if (!v) return fail(SEMTSDF_ERR_INVALID, "NULL handle");
+    HIPC(hipSetDevice(v->device));
+    return integrate_impl(v, depth_d, rgb_d, mask_d, nullptr, E, pick(v, stream), true, (hipEvent_t)inputs_ready);
 }
 
 int semtsdf_integrate_vote_dev(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d, const int32_t* cls_d,

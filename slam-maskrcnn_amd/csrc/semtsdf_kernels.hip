@@ -779,12 +779,8 @@ __host__ __device__ inline UnitGrid unit_grid(const VolGeom& g) {
 // b % kListSegs == c (one counter per segment, 256 B apart, keeps the same-address atomics
 // per counter to 1/64 of the workgroups).  Capacity of a segment: all units of its
 // workgroups.
-#ifndef SEMTSDF_CULL_ZRUN
-#define SEMTSDF_CULL_ZRUN 0  // cull (and list) order: 0 x runs, 1 memory order (z fastest)
-#endif
 __host__ __device__ inline unsigned list_seg_cap(const UnitGrid& ug) {
-    const unsigned groups = SEMTSDF_CULL_ZRUN ? (ug.n + 255u) / 256u
-                                              : (ug.nux + 255u) / 256u * ug.nuy * ug.nuz;  // k_cull_units workgroups
+    const unsigned groups = (ug.nux + 255u) / 256u * ug.nuy * ug.nuz;  // k_cull_units workgroups
     return (groups + kListSegs - 1u) / kListSegs * 256u;
 }
 
@@ -795,19 +791,10 @@ __host__ __device__ inline unsigned list_seg_cap(const UnitGrid& ug) {
 __global__ __launch_bounds__(256) void k_cull_units(IntegrateArgs a, UnitGrid ug, unsigned seg_cap) {
     __shared__ unsigned s_cnt[kLists][4];
     __shared__ unsigned s_base[kLists];
-#if SEMTSDF_CULL_ZRUN
-    // units in memory order (z fastest, then y, then x): consecutive list entries are adjacent
-    // half tiles, so an integrate wave's two units are one contiguous 1-KB tile per array
-    const unsigned lin = blockIdx.x * blockDim.x + threadIdx.x;
-    const unsigned uz = lin % ug.nuz, t = lin / ug.nuz, uy = t % ug.nuy, ux = t / ug.nuy;
-    const unsigned bid = blockIdx.x;
-    const bool inside = lin < ug.n;
-#else
     // grid (x runs of 256 units, uy, uz): no integer division by the runtime unit counts
     const unsigned ux = blockIdx.x * blockDim.x + threadIdx.x, uy = blockIdx.y, uz = blockIdx.z;
     const unsigned bid = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
     const bool inside = ux < ug.nux;
-#endif
     const unsigned u = pack_unit(ux, uy, uz);
     int c = 1;  // dead
     if (inside) c = a.cull ? unit_cull(a, (int)ux * UX, (int)uy * UY, (int)uz * UZ) : 0;
@@ -838,12 +825,8 @@ __global__ __launch_bounds__(256) void k_cull_units(IntegrateArgs a, UnitGrid ug
 hipError_t launch_cull(const IntegrateArgs& a, hipStream_t s) {
     const UnitGrid ug = unit_grid(a.g);
     if (ug.n == 0) return hipSuccess;  // a shard that owns no chunk
-#if SEMTSDF_CULL_ZRUN
-    hipLaunchKernelGGL(k_cull_units, dim3((ug.n + 255) / 256), dim3(256), 0, s, a, ug, list_seg_cap(ug));
-#else
     hipLaunchKernelGGL(k_cull_units, dim3((ug.nux + 255) / 256, ug.nuy, ug.nuz), dim3(256), 0, s, a, ug,
                        list_seg_cap(ug));
-#endif
     return hipGetLastError();
 }
 
@@ -912,7 +895,7 @@ __device__ __forceinline__ uint64_t unit_tile(const VolGeom& g, const UnitPos& u
 // the pending count first (stage_compute), and k_flush_lazy folds the counts into the weights
 // before they are read out (download, upload, checkpoint).
 #ifndef SEMTSDF_LAZY_WEIGHT
-#define SEMTSDF_LAZY_WEIGHT 1
+#define SEMTSDF_LAZY_WEIGHT 0  // measured slower: the kernel is issue-bound, not traffic-bound
 #endif
 constexpr unsigned kFlagMax = 255u;  // s - 1 <= 254 pending increments
 
@@ -1146,9 +1129,6 @@ __device__ __forceinline__ void stage_classify(const IntegrateArgs& a, const Pro
 
 #ifndef SEMTSDF_FULLROW
 #define SEMTSDF_FULLROW 1
-#endif
-#ifndef SEMTSDF_PIPE
-#define SEMTSDF_PIPE 1  // integrate_list software pipeline: 1 two-stage, 2 three-stage (one wait per iteration)
 #endif
 // Whole-line state traffic: a 128-B line of a per-voxel array is the 8 lanes of one
 // z-quad (lane % 8); when any of them updates, all 8 load and store it (unchanged values
@@ -1509,46 +1489,7 @@ __device__ __forceinline__ unsigned integrate_list(const IntegrateArgs& a, const
         return p;
     };
     unsigned i = (wave + nwaves - rot % nwaves) % nwaves;
-    if (SEMTSDF_PIPE == 2 && i < ngroups) {
-        // Deeper pipeline: at the top of iteration i one wait covers everything the previous
-        // iteration issued (the state loads of unit k issued a whole iteration earlier, the
-        // pixel gathers of unit k+1 half an iteration earlier, the stores of unit k-1), then
-        //   classify(k+1)  load(k+1)  project(k+2)  compute(k)  store(k)
-        // so the state loads of k+1 and the gathers of k+2 are in flight under the compute and
-        // store of k.  The last iteration classifies, loads and projects copies of the current
-        // units (not counted), so every iteration issues the same memory operations.
-        unsigned e[kSlots], en[kSlots];
-        group_entries(i, e);
-        UnitPos cur = lane_pos(e);
-        if (i + nwaves < ngroups) group_entries(i + nwaves, en);
-        Proj P;
-        Cls C, Cn;
-        Ld L, Ln;
-        Out O;
-        stage_project<SHARD, PIN, FREE, FULL>(a, cur, lane, P);
-        stage_classify<SEM, GATE, VOTE, COUNT, FREE>(a, P, C, true, n_touch, n_gate);
-        stage_load<SEM, CI32, VOTE, FREE>(a, cur, coff, C, L);
-        UnitPos n1 = (i + nwaves < ngroups) ? lane_pos(en) : cur;
-        if (i + 2u * nwaves < ngroups) group_entries(i + 2u * nwaves, en);
-        stage_project<SHARD, PIN, FREE, FULL>(a, n1, lane, P);
-        while (true) {
-            const bool has1 = i + nwaves < ngroups;
-            const UnitPos n2 = (i + 2u * nwaves < ngroups) ? lane_pos(en) : n1;
-            if (i + 3u * nwaves < ngroups) group_entries(i + 3u * nwaves, en);
-            stage_classify<SEM, GATE, VOTE, COUNT, FREE>(a, P, Cn, has1, n_touch, n_gate);
-            stage_load<SEM, CI32, VOTE, FREE>(a, n1, coff, Cn, Ln);
-            stage_project<SHARD, PIN, FREE, FULL>(a, n2, lane, P);
-            stage_compute<SEM, GATE, CI32, VOTE, FREE>(a, s_rcp, C, L, O);
-            const StoreMeta Mc = store_meta(C);
-            stage_store<SEM, CI32, VOTE, FREE, COUNT>(a, cur, coff, Mc, O, n_lazy);
-            if (!has1) break;
-            C = Cn;
-            L = Ln;
-            cur = n1;
-            n1 = n2;
-            i += nwaves;
-        }
-    } else if (i < ngroups) {
+    if (i < ngroups) {
         unsigned e[kSlots], en[kSlots];
         group_entries(i, e);
         UnitPos cur = lane_pos(e);

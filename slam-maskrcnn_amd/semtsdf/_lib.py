@@ -142,6 +142,7 @@ SIGNATURES = {
     "semtsdf_reset": (_I, [_P, _P]),
     "semtsdf_integrate": (_I, [_P, _P, _P, _P, _P, _P]),
     "semtsdf_integrate_dev": (_I, [_P, _P, _P, _P, _P, _P]),
+    "semtsdf_integrate_dev_async": (_I, [_P, _P, _P, _P, _P, _P, _P]),
     "semtsdf_integrate_vote_dev": (_I, [_P, _P, _P, _P, _P, _P]),
     "semtsdf_associate": (_I, [_P, _P, _P, C.POINTER(AssocStats), _P]),
     "semtsdf_associate_dev": (_I, [_P, _P, _P, C.POINTER(AssocStats), _P]),

@@ -177,6 +177,16 @@ class Volume:
         L.check(L.load().semtsdf_integrate_dev(self._h, C.c_void_p(depth_ptr), C.c_void_p(rgb_ptr),
                                                C.c_void_p(mask_ptr) if mask_ptr else None, L.ptr(e), stream))
 
+    def integrate_dev_async(self, depth_ptr: int, rgb_ptr: int, mask_ptr: int | None, E, inputs_ready=None,
+                            stream=None):
+        """integrate_dev with the frame prepass on the volume's prep stream, overlapping the
+        previous frame's integrate; inputs_ready: a raw hipEvent_t marking the inputs complete
+        (None: they already are).  The inputs must not change until this frame has run."""
+        e = L.f32(E, 16)
+        L.check(L.load().semtsdf_integrate_dev_async(self._h, C.c_void_p(depth_ptr), C.c_void_p(rgb_ptr),
+                                                     C.c_void_p(mask_ptr) if mask_ptr else None, L.ptr(e),
+                                                     C.c_void_p(inputs_ready) if inputs_ready else None, stream))
+
     def integrate_vote_dev(self, depth_ptr: int, rgb_ptr: int, cls_ptr: int, E, stream=None):
         e = L.f32(E, 16)
         L.check(L.load().semtsdf_integrate_vote_dev(self._h, C.c_void_p(depth_ptr), C.c_void_p(rgb_ptr),

@@ -983,3 +983,40 @@ def test_color_i32_storage_widening(S, oracle, stream):
         assert_same(vol, ost)
         assert (ost.color < 0).any() or (ost.wt >= (1 << 23)).any(), case
         vol.close()
+
+
+def test_async_prepass_integrate_matches_oracle(S, oracle, stream):
+    """semtsdf_integrate_dev_async: the frame prepass of frame k+1 on the volume's prep stream
+    overlaps the integrate of frame k (two prepass buffer sets used in turn).  Resident frames
+    issued back to back, mixed with synchronous integrate_dev calls and a host-pointer
+    integrate, give every array bit-identical to the oracle."""
+    from semtsdf.volume import DeviceBuffer
+
+    st, frames = stream
+    semtsdf, L = S
+    p, vol, g, ost = make(S, oracle, (96, 96, 96), frames[0], 0x3)
+    npx = 640 * 480
+    F = len(frames) - 1
+    d, r, m = DeviceBuffer(F * npx * 2), DeviceBuffer(F * npx * 3), DeviceBuffer(F * npx)
+    for i, fr in enumerate(frames[1:]):
+        d.upload(fr.depth, None, i * npx * 2)
+        r.upload(fr.rgb, None, i * npx * 3)
+        m.upload(fr.gt_ids, None, i * npx)
+    order = [0, 1, 2, 3, 4, 0, 1, 2, 3, 4, 2, 2, 3]
+    mode = ["async", "async", "async", "sync", "async", "async", "host", "async", "async", "sync", "async", "async",
+            "async"]
+    for i, md in zip(order, mode):
+        fr = frames[1 + i]
+        E = (fr.w2c @ frames[0].c2w).astype(np.float32)
+        if md == "async":
+            vol.integrate_dev_async(d.ptr + i * npx * 2, r.ptr + i * npx * 3, m.ptr + i * npx, E)
+        elif md == "sync":
+            vol.integrate_dev(d.ptr + i * npx * 2, r.ptr + i * npx * 3, m.ptr + i * npx, E)
+        else:
+            vol.integrate(fr.depth, fr.rgb, fr.gt_ids, E)
+        oracle.integrate(g, ost, list(p.K), E, fr.depth, fr.rgb, fr.gt_ids, flags=0x3)
+    vol.sync()
+    assert_same(vol, ost, hist=True)
+    for b in (d, r, m):
+        b.free()
+    vol.close()
