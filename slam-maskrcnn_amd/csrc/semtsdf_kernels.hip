@@ -886,6 +886,7 @@ __device__ __forceinline__ uint64_t unit_tile(const VolGeom& g, const UnitPos& u
 #ifndef SEMTSDF_STEADY
 #define SEMTSDF_STEADY 1  // skip the sdf traffic of steady lines (Ld::skip)
 #endif
+
 // Lazy weights of steady lines.  A steady line (every sdf exactly 1.0f) whose 32 voxels are
 // all touched with f == 1 changes only its weights, each by +1, when the colour/histogram
 // gate rejects f == 1 (free_ok modes): the increment is kept as a per-line pending count in
