@@ -401,7 +401,28 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
     EventPair ep{nullptr, nullptr};
     if ((v->instr & 1) && (hipEventCreate(&ep.a) != hipSuccess || hipEventCreate(&ep.b) != hipSuccess))
         ep.a = ep.b = nullptr;
+    // instrumentation (a SEMTSDF_WAVE_TRACE=1 build): SEMTSDF_WAVE_TRACE=<file> appends the
+    // per-wave phase timestamps of the first 32 integrates (kWaveTraceWords u64 per wave slot)
+    static const char* wt_path = getenv("SEMTSDF_WAVE_TRACE");
+    static int wt_calls = 0;
+    constexpr size_t kWtSlots = 65536;
+    const bool wt = wt_path && wt_calls < 32;
+    if (wt) {
+        ++wt_calls;
+        HIPC(hipMalloc((void**)&a.wtrace, kWtSlots * kWaveTraceWords * 8));
+        HIPC(hipMemsetAsync(a.wtrace, 0, kWtSlots * kWaveTraceWords * 8, s));
+    }
     HIPC(launch_integrate(a, s, ep.a, ep.b));
+    if (wt) {
+        std::vector<unsigned long long> h(kWtSlots * kWaveTraceWords);
+        HIPC(hipMemcpyAsync(h.data(), a.wtrace, h.size() * 8, hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+        HIPC(hipFree(a.wtrace));
+        if (FILE* f = fopen(wt_path, "ab")) {
+            fwrite(h.data(), 8, h.size(), f);
+            fclose(f);
+        }
+    }
     if (ep.a) v->ev_integrate.push_back(ep);
     if (v->async_used) {  // a later asynchronous prepass into this set waits for this integrate
         HIPC(hipEventRecord(F.set_free, s));

@@ -126,7 +126,10 @@ struct IntegrateArgs {
     unsigned* list_count;          // [3][kListSegs * kListCountStride] entries per segment (zeroed by the frame prepass)
     int free_ok;                   // free units allowed: gated colour with gate <= 1 (f == 1 updates sdf/weight only)
     int color_wide;                // colour stored as int32 x 4 (else u8 x 4; see semtsdf_vol::color_wide)
+    unsigned long long* wtrace;    // instrumentation (build with SEMTSDF_WAVE_TRACE=1, run with
+                                   // SEMTSDF_WAVE_TRACE=<file>): per wave kWaveTraceWords timestamps
 };
+constexpr int kWaveTraceWords = 8;
 
 // Association accumulators (fixed point, scale 2^28, deterministic).
 constexpr double kFixScale = 268435456.0;  // 2^28

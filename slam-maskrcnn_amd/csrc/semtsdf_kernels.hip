@@ -898,6 +898,12 @@ __device__ __forceinline__ uint64_t unit_tile(const VolGeom& g, const UnitPos& u
 #ifndef SEMTSDF_LAZY_WEIGHT
 #define SEMTSDF_LAZY_WEIGHT 0  // measured slower: the kernel is issue-bound, not traffic-bound
 #endif
+#ifndef SEMTSDF_CHAIN
+#define SEMTSDF_CHAIN 1  // a wave's last unit of a list overlaps the first unit of its next list
+#endif
+#ifndef SEMTSDF_WAVE_TRACE
+#define SEMTSDF_WAVE_TRACE 0  // instrumentation build only: per-wave phase timestamps (IntegrateArgs::wtrace)
+#endif
 constexpr unsigned kFlagMax = 255u;  // s - 1 <= 254 pending increments
 
 struct Proj {
@@ -1435,91 +1441,144 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
     }
 }
 
-// One list of the frame (general or free units) by the persistent waves: wave w takes the
-// groups w', w' + nwaves, ... with w' = (w - rot) mod nwaves (rot balances the extra groups of
-// the two lists), a group being kSlots consecutive entries, one unit per slot.
-template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT, bool SHARD, bool PIN, bool FREE, bool FULL = false>
-__device__ __forceinline__ unsigned integrate_list(const IntegrateArgs& a, const UnitGrid& ug, unsigned seg_cap,
-                                                   const float* __restrict__ s_rcp, const unsigned* list,
-                                                   const unsigned* list_count, unsigned wave, unsigned nwaves,
-                                                   unsigned rot, unsigned& n_touch, unsigned& n_gate,
-                                                   unsigned& n_lazy) {
-    const int lane = threadIdx.x & 63;
-    // the lane's offset from the unit origin (a volume has < 2^31 stored voxels per x-plane pair)
-    const unsigned coff = (unsigned)lane_zq(lane) * 32u + (unsigned)lane_y(lane) * 4u;  // lane's offset in its unit
-    // segment counts, one per lane; inclusive prefix over the lanes (kListSegs == 64)
+// One list of the frame as one persistent wave sees it: wave w takes the groups w', w' +
+// nwaves, ... with w' = (w - rot) mod nwaves (rot continues the round-robin of the lists
+// before it, so the waves with an extra group alternate), a group being kSlots consecutive
+// entries, one unit per slot.  The list is kListSegs segments; lane l holds the inclusive
+// prefix of the segment counts up to segment l.
+struct ListView {
+    const unsigned* list;
+    unsigned incl;             // per lane: entries in segments 0..lane
+    unsigned total, ngroups;   // wave-uniform
+    unsigned i;                // the wave's current group
+};
+
+__device__ __forceinline__ ListView list_view(const unsigned* list, const unsigned* list_count, unsigned wave,
+                                              unsigned nwaves, unsigned rot) {
     static_assert(kListSegs == 64, "one list segment per lane");
-    const unsigned cnt_l = list_count[lane * kListCountStride];
-    unsigned incl = cnt_l;
+    const int lane = threadIdx.x & 63;
+    ListView v;
+    v.list = list;
+    v.incl = list_count[lane * kListCountStride];
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
-        const unsigned o = (unsigned)__shfl_up((int)incl, off, 64);
-        if (lane >= off) incl += o;
+        const unsigned o = (unsigned)__shfl_up((int)v.incl, off, 64);
+        if (lane >= off) v.incl += o;
     }
-    const unsigned total = __builtin_amdgcn_readfirstlane((unsigned)__shfl((int)incl, 63, 64));
-    auto entry = [&](unsigned i) -> unsigned {  // i < total: segment = number of segments ending at or before i
-        const unsigned seg = (unsigned)__popcll(__ballot(incl <= i));
-        const unsigned before = seg ? __builtin_amdgcn_readfirstlane((unsigned)__shfl((int)incl, (int)seg - 1, 64)) : 0u;
-        const unsigned off = i - before;
-        // constant address space: the list is read-only here, so this is a scalar load
-        // (s_load, lgkmcnt) and never waits behind the wave's vector memory operations
-        const __attribute__((address_space(4))) unsigned* l4 = (const __attribute__((address_space(4))) unsigned*)list;
-        return l4[seg * seg_cap + off];
-    };
-    // group k of the list = entries k*kSlots .. k*kSlots+kSlots-1, one unit per slot of the wave
-    const unsigned ngroups = (total + kSlots - 1) / kSlots;
-    const int slot = lane_slot(lane);
-    auto group_entries = [&](unsigned grp, unsigned* e) {
+    v.total = __builtin_amdgcn_readfirstlane((unsigned)__shfl((int)v.incl, 63, 64));
+    v.ngroups = (v.total + kSlots - 1) / kSlots;
+    v.i = (wave + nwaves - rot % nwaves) % nwaves;
+    return v;
+}
+
+// Entry idx < total: its segment is the number of segments ending at or before idx.
+__device__ __forceinline__ unsigned list_entry(const ListView& v, unsigned idx, unsigned seg_cap) {
+    const unsigned seg = (unsigned)__popcll(__ballot(v.incl <= idx));
+    const unsigned before = seg ? __builtin_amdgcn_readfirstlane((unsigned)__shfl((int)v.incl, (int)seg - 1, 64)) : 0u;
+    // constant address space: the list is read-only here, so this is a scalar load (s_load,
+    // lgkmcnt) and never waits behind the wave's vector memory operations
+    const __attribute__((address_space(4))) unsigned* l4 = (const __attribute__((address_space(4))) unsigned*)v.list;
+    return l4[seg * seg_cap + (idx - before)];
+}
+
+__device__ __forceinline__ void group_entries(const ListView& v, unsigned grp, unsigned seg_cap, unsigned* e) {
 #pragma unroll
-        for (int k = 0; k < kSlots; ++k) {
-            const unsigned idx = grp * kSlots + k;
-            e[k] = idx < total ? entry(idx) : ~0u;
-        }
-    };
-    auto lane_pos = [&](const unsigned* e) -> UnitPos {  // the lane's unit (a group's first entry exists)
-        UnitPos p = unit_pos(ug, e[0]);
+    for (int k = 0; k < kSlots; ++k) {
+        const unsigned idx = grp * kSlots + k;
+        e[k] = idx < v.total ? list_entry(v, idx, seg_cap) : ~0u;
+    }
+}
+
+// The lane's unit of a group (the group's first entry exists).
+__device__ __forceinline__ UnitPos lane_pos(const UnitGrid& ug, const unsigned* e) {
+    const int slot = lane_slot(threadIdx.x & 63);
+    UnitPos p = unit_pos(ug, e[0]);
 #pragma unroll
-        for (int k = 1; k < kSlots; ++k) {
-            const bool have = e[k] != ~0u;
-            const UnitPos q = unit_pos(ug, have ? e[k] : e[0]);
-            if (slot == k) {
-                p = q;
-                p.ok = have;
-            }
-        }
-        return p;
-    };
-    unsigned i = (wave + nwaves - rot % nwaves) % nwaves;
-    if (i < ngroups) {
-        unsigned e[kSlots], en[kSlots];
-        group_entries(i, e);
-        UnitPos cur = lane_pos(e);
-        if (i + nwaves < ngroups) group_entries(i + nwaves, en);
-        Proj P;
-        Cls C;
-        Ld L;
-        Out O;
-        stage_project<SHARD, PIN, FREE, FULL>(a, cur, lane, P);
-        stage_classify<SEM, GATE, VOTE, COUNT, FREE>(a, P, C, true, n_touch, n_gate);
-        stage_load<SEM, CI32, VOTE, FREE>(a, cur, coff, C, L);
-        while (true) {
-            const bool has = i + nwaves < ngroups;
-            // the last iteration projects a copy of the current units, so the memory
-            // operations issued per iteration do not depend on the branch
-            const UnitPos nxt = has ? lane_pos(en) : cur;
-            if (i + 2u * nwaves < ngroups) group_entries(i + 2u * nwaves, en);
-            stage_project<SHARD, PIN, FREE, FULL>(a, nxt, lane, P);
-            if (SEMTSDF_FULLROW || C.tmask) stage_compute<SEM, GATE, CI32, VOTE, FREE>(a, s_rcp, C, L, O);
-            const StoreMeta Mc = store_meta(C);
-            stage_classify<SEM, GATE, VOTE, COUNT, FREE>(a, P, C, has, n_touch, n_gate);
-            stage_store<SEM, CI32, VOTE, FREE, COUNT>(a, cur, coff, Mc, O, n_lazy);
-            if (!has) break;
-            stage_load<SEM, CI32, VOTE, FREE>(a, nxt, coff, C, L);
-            cur = nxt;
-            i += nwaves;
+    for (int k = 1; k < kSlots; ++k) {
+        const bool have = e[k] != ~0u;
+        const UnitPos q = unit_pos(ug, have ? e[k] : e[0]);
+        if (slot == k) {
+            p = q;
+            p.ok = have;
         }
     }
-    return total;
+    return p;
+}
+
+// Pipeline state carried from one list into the next: the unit whose project, classify and
+// load stages were issued (primed) but not yet computed and stored.
+struct Pipe {
+    UnitPos cur;
+    Proj P;
+    Cls C;
+    Ld L;
+    Out O;
+    bool primed = false;
+};
+
+// Unit-kind of a list: 0 general, 1 free (projected), 2 full free (no projection).
+template <int KIND>
+struct KindOf {
+    static constexpr bool FREE = KIND != 0, FULL = KIND == 2;
+};
+
+// One list (kind KIND) by one persistent wave, software-pipelined.  The wave's last unit of
+// the list is computed and stored under the project / classify / load of its first unit of
+// the next list (kind NKIND, `nx`; NKIND < 0: none), which then starts primed: the pipeline
+// does not drain and refill between the lists.
+template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT, bool SHARD, bool PIN, int KIND, int NKIND>
+__device__ __forceinline__ void integrate_list(const IntegrateArgs& a, const UnitGrid& ug, unsigned seg_cap,
+                                               const float* __restrict__ s_rcp, ListView& v, const ListView* nx,
+                                               unsigned nwaves, Pipe& S, unsigned& n_touch, unsigned& n_gate,
+                                               unsigned& n_lazy) {
+    constexpr bool FREE = KindOf<KIND>::FREE, FULL = KindOf<KIND>::FULL;
+    constexpr bool NFREE = KindOf<(NKIND < 0 ? 0 : NKIND)>::FREE, NFULL = KindOf<(NKIND < 0 ? 0 : NKIND)>::FULL;
+    const int lane = threadIdx.x & 63;
+    // the lane's offset from the unit origin (a volume has < 2^31 stored voxels per x-plane pair)
+    const unsigned coff = (unsigned)lane_zq(lane) * 32u + (unsigned)lane_y(lane) * 4u;
+    if (!S.primed) {
+        if (v.i >= v.ngroups) return;  // no group of this list for the wave (the next list primes itself)
+        unsigned e[kSlots];
+        group_entries(v, v.i, seg_cap, e);
+        S.cur = lane_pos(ug, e);
+        stage_project<SHARD, PIN, FREE, FULL>(a, S.cur, lane, S.P);
+        stage_classify<SEM, GATE, VOTE, COUNT, FREE>(a, S.P, S.C, true, n_touch, n_gate);
+        stage_load<SEM, CI32, VOTE, FREE>(a, S.cur, coff, S.C, S.L);
+    }
+    unsigned en[kSlots];
+    if (v.i + nwaves < v.ngroups) group_entries(v, v.i + nwaves, seg_cap, en);
+    const bool chain = NKIND >= 0 && SEMTSDF_CHAIN && nx->i < nx->ngroups;
+    unsigned eb[kSlots];
+    if (NKIND >= 0 && SEMTSDF_CHAIN && chain) group_entries(*nx, nx->i, seg_cap, eb);
+    while (v.i + nwaves < v.ngroups) {
+        const UnitPos nxt = lane_pos(ug, en);
+        if (v.i + 2u * nwaves < v.ngroups) group_entries(v, v.i + 2u * nwaves, seg_cap, en);
+        stage_project<SHARD, PIN, FREE, FULL>(a, nxt, lane, S.P);
+        stage_compute<SEM, GATE, CI32, VOTE, FREE>(a, s_rcp, S.C, S.L, S.O);
+        const StoreMeta Mc = store_meta(S.C);
+        stage_classify<SEM, GATE, VOTE, COUNT, FREE>(a, S.P, S.C, true, n_touch, n_gate);
+        stage_store<SEM, CI32, VOTE, FREE, COUNT>(a, S.cur, coff, Mc, S.O, n_lazy);
+        stage_load<SEM, CI32, VOTE, FREE>(a, nxt, coff, S.C, S.L);
+        S.cur = nxt;
+        v.i += nwaves;
+    }
+    // the wave's last unit of this list
+    if (NKIND >= 0 && SEMTSDF_CHAIN && chain) {
+        const UnitPos nxt = lane_pos(ug, eb);
+        stage_project<SHARD, PIN, NFREE, NFULL>(a, nxt, lane, S.P);
+        stage_compute<SEM, GATE, CI32, VOTE, FREE>(a, s_rcp, S.C, S.L, S.O);
+        const StoreMeta Mc = store_meta(S.C);
+        stage_classify<SEM, GATE, VOTE, COUNT, NFREE>(a, S.P, S.C, true, n_touch, n_gate);
+        stage_store<SEM, CI32, VOTE, FREE, COUNT>(a, S.cur, coff, Mc, S.O, n_lazy);
+        stage_load<SEM, CI32, VOTE, NFREE>(a, nxt, coff, S.C, S.L);
+        S.cur = nxt;
+        S.primed = true;
+    } else {
+        stage_compute<SEM, GATE, CI32, VOTE, FREE>(a, s_rcp, S.C, S.L, S.O);
+        stage_store<SEM, CI32, VOTE, FREE, COUNT>(a, S.cur, coff, store_meta(S.C), S.O, n_lazy);
+        S.primed = false;
+    }
+    v.i += nwaves;
 }
 
 // Persistent wavefronts over the two live-unit lists of the frame: the free units first
@@ -1531,30 +1590,67 @@ template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT, bool SHARD, boo
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : SEMTSDF_INTEGRATE_WPE))) void k_integrate(
     IntegrateArgs a, UnitGrid ug, unsigned seg_cap) {
     __shared__ float s_rcp[kRcpTable];
-    for (int i = (int)threadIdx.x; i < kRcpTable; i += (int)blockDim.x) s_rcp[i] = a.rcp_table[i];
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
+    // instrumentation: per-wave wall-clock marks (entry, table loaded, after each list) and
+    // the wave's group counts per list
+    unsigned long long tr[5] = {0, 0, 0, 0, 0};
+    unsigned long long trn = 0;
     const unsigned wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     const unsigned nwaves = gridDim.x * (blockDim.x >> 6);
+    auto groups_of = [&](unsigned n, unsigned rot_) -> unsigned long long {
+        const unsigned ng = (n + kSlots - 1) / kSlots, i0 = (wave + nwaves - rot_ % nwaves) % nwaves;
+        return i0 < ng ? (ng - 1u - i0) / nwaves + 1u : 0u;
+    };
+    if (SEMTSDF_WAVE_TRACE) tr[0] = wall_clock64();
+    for (int i = (int)threadIdx.x; i < kRcpTable; i += (int)blockDim.x) s_rcp[i] = a.rcp_table[i];
+    __syncthreads();
+    if (SEMTSDF_WAVE_TRACE) tr[1] = tr[2] = tr[3] = wall_clock64();
+    const int lane = threadIdx.x & 63;
     unsigned n_touch = 0, n_gate = 0, n_lazy = 0;
-    unsigned rot = 0, nlive = 0;
-    if (GATE && !VOTE) {  // free units exist only in gated modes (free_ok)
-        const unsigned n1 = integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, true, false>(
-            a, ug, seg_cap, s_rcp, a.unit_list + (size_t)kListSegs * seg_cap, a.list_count + kListSegs * kListCountStride,
-            wave, nwaves, 0u, n_touch, n_gate, n_lazy);
-        const unsigned g1 = (n1 + kSlots - 1) / kSlots;
-        const unsigned n2 = integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, true, true>(
-            a, ug, seg_cap, s_rcp, a.unit_list + (size_t)2 * kListSegs * seg_cap,
-            a.list_count + 2 * kListSegs * kListCountStride, wave, nwaves, g1 % nwaves, n_touch, n_gate, n_lazy);
-        rot = (g1 + (n2 + kSlots - 1) / kSlots) % nwaves;
-        if (COUNT && blockIdx.x == 0 && threadIdx.x == 0) {
-            atomicAdd(a.counters + 4, (unsigned long long)(n1 + n2));
-            atomicAdd(a.counters + 5, (unsigned long long)n2);
+    unsigned nlive = 0;
+    Pipe S;
+    const unsigned* cnt = a.list_count;
+    const unsigned* lst = a.unit_list;
+    const size_t lstride = (size_t)kListSegs * seg_cap;
+    constexpr int kCnt = kListSegs * kListCountStride;
+    unsigned n0;
+    unsigned rot0 = 0;
+    if (GATE && !VOTE) {  // free units exist only in gated modes (free_ok): full free, free, general
+        ListView vf = list_view(lst + 2 * lstride, cnt + 2 * kCnt, wave, nwaves, 0u);
+        ListView v1 = list_view(lst + lstride, cnt + kCnt, wave, nwaves, vf.ngroups % nwaves);
+        rot0 = (vf.ngroups + v1.ngroups) % nwaves;
+        ListView v0 = list_view(lst, cnt, wave, nwaves, rot0);
+        integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 2, 1>(a, ug, seg_cap, s_rcp, vf, &v1, nwaves, S,
+                                                                       n_touch, n_gate, n_lazy);
+        if (SEMTSDF_WAVE_TRACE) tr[2] = wall_clock64();
+        integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 1, 0>(a, ug, seg_cap, s_rcp, v1, &v0, nwaves, S,
+                                                                       n_touch, n_gate, n_lazy);
+        if (SEMTSDF_WAVE_TRACE) {
+            tr[3] = wall_clock64();
+            trn = groups_of(vf.total, 0u) | (groups_of(v1.total, vf.ngroups % nwaves) << 20);
         }
-        if (COUNT) nlive += n1 + n2;
+        integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0, -1>(a, ug, seg_cap, s_rcp, v0, nullptr, nwaves, S,
+                                                                        n_touch, n_gate, n_lazy);
+        n0 = v0.total;
+        if (COUNT && blockIdx.x == 0 && threadIdx.x == 0) {
+            atomicAdd(a.counters + 4, (unsigned long long)(v1.total + vf.total));
+            atomicAdd(a.counters + 5, (unsigned long long)vf.total);
+        }
+        if (COUNT) nlive += v1.total + vf.total;
+    } else {
+        ListView v0 = list_view(lst, cnt, wave, nwaves, 0u);
+        integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0, -1>(a, ug, seg_cap, s_rcp, v0, nullptr, nwaves, S,
+                                                                        n_touch, n_gate, n_lazy);
+        n0 = v0.total;
     }
-    const unsigned n0 = integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, false>(
-        a, ug, seg_cap, s_rcp, a.unit_list, a.list_count, wave, nwaves, rot, n_touch, n_gate, n_lazy);
+    if (SEMTSDF_WAVE_TRACE && a.wtrace) {
+        tr[4] = wall_clock64();
+        trn |= groups_of(n0, rot0) << 40;
+        if (lane < 8) {
+            const unsigned long long hw = (unsigned long long)__smid() | ((unsigned long long)blockIdx.x << 32);
+            const unsigned long long v = lane < 5 ? tr[lane < 5 ? lane : 0] : lane == 5 ? hw : lane == 6 ? trn : 0ull;
+            a.wtrace[(size_t)wave * kWaveTraceWords + lane] = v;
+        }
+    }
     if (COUNT) {
         nlive += n0;
         unsigned long long t = n_touch, gg = n_gate, lz = n_lazy;
