@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SEMTSDF_ABI_VERSION 7
+#define SEMTSDF_ABI_VERSION 8
 #define SEMTSDF_MAX_OBJECTS 32 /* tsdf.cuh:4 */
 
 /* ---- status codes ------------------------------------------------------------ */
@@ -193,6 +193,15 @@ int semtsdf_parse_frame_dev(semtsdf_vol* v, const uint16_t* depth_d, const uint8
  * render on another stream; the association, which only reads the volume, may overlap it. */
 int semtsdf_parse_frame_dev_after(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d,
                                   uint8_t* mask_d, const float E[16], void* integrate_after_event, void* stream);
+/* parse_frame_dev plus one live view (semtsdf_raycast_dev arguments) of the volume as it
+ * stands BEFORE this frame -- the view Viewer::show_tsdf shows after the previous frame
+ * (kernel.cpp:96-107) -- rendered in the same launch as this frame's association march: both
+ * read that state and both are bound by their slowest rays, so each fills the other's tail.
+ * Without an association (first frame, non-semantic volume) the view is rendered first, alone.
+ * out_bgr_d / out_t_d are written by the time the frame's work on `stream` completes. */
+int semtsdf_parse_frame_view_dev(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d,
+                                 uint8_t* mask_d, const float E[16], const float s2w[16], const float c[3],
+                                 int mode, uint8_t* out_bgr_d, float* out_t_d, void* stream);
 
 /* ---- raycast render (a8: Viewer::show_tsdf viewer.cu:137-179) -------------------------
  * Orbit camera helper: s2w = rot(angle, dist) * Kinv, c = ((dist+0.5) sin, 0, (dist+0.5)(1-cos)). */

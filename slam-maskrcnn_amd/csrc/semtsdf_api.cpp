@@ -504,8 +504,10 @@ int tables_ready(semtsdf_vol* v, hipStream_t s) {
 
 // defer_relabel: the caller integrates this mask next; the relabel is left to that
 // integrate's prepass (v->pending_lut), saving a launch.
+// view (optional): a render of the same volume state launched together with the march
+// (k_march_fused); its arguments were validated by the caller.
 int associate_impl(semtsdf_vol* v, uint8_t* mask_d, const float E[16], hipStream_t s, bool want_decision,
-                   bool defer_relabel = false) {
+                   bool defer_relabel = false, const RenderArgs* view = nullptr) {
     if (v->p.z_nshards != 1) return fail(SEMTSDF_ERR_UNSUPPORTED, "association on a Z-sharded handle is not supported yet");
     if (!(v->p.flags & SEMTSDF_F_SEMANTIC)) return fail(SEMTSDF_ERR_STATE, "association needs a SEMANTIC volume");
     if (v->n_obs == 0) return fail(SEMTSDF_ERR_STATE, "association needs n_obs > 0 (tsdf.cu:426)");
@@ -529,7 +531,14 @@ int associate_impl(semtsdf_vol* v, uint8_t* mask_d, const float E[16], hipStream
         static const char* dbg = getenv("SEMTSDF_DEBUG_ASSOC");  // timing probes only
         a.debug = dbg ? atoi(dbg) : 0;
     }
-    HIPC(launch_assoc_march(a, s));
+    if (view) {
+        RenderArgs r = *view;
+        r.b = v->b;  // the map buffers as ensure_bmin left them
+        HIPC(launch_march_fused(a, r, s));
+        v->n_render++;
+    } else {
+        HIPC(launch_assoc_march(a, s));
+    }
     HIPC(launch_assoc_decide(v->tables_d, v->decision_d, 0, v->p.prior_mrcnn_err_rate, v->num_objs_d, s));
     v->tables_clean = true;  // the decide kernel clears them
     if (defer_relabel)
@@ -1098,15 +1107,23 @@ int semtsdf_parse_frame_dev(semtsdf_vol* v, const uint16_t* depth_d, const uint8
     return semtsdf_parse_frame_dev_after(v, depth_d, rgb_d, mask_d, E, nullptr, stream);
 }
 
-int semtsdf_parse_frame_dev_after(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d, uint8_t* mask_d,
-                                  const float E[16], void* integrate_after_event, void* stream) {
-    if (!v || !E || !depth_d || !rgb_d) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
-    hipStream_t s = pick(v, stream);
+static int launch_view(semtsdf_vol* v, const RenderArgs& view, hipStream_t s);
+static int render_args(semtsdf_vol* v, const float s2w[16], const float c[3], int mode, uint8_t* out_bgr_d,
+                       float* out_t_d, RenderArgs& a);
+
+// view (optional): a render of the volume state before this frame, launched with this
+// frame's association march when there is one (else on its own, first).
+static int parse_frame_dev_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d, uint8_t* mask_d,
+                                const float E[16], void* integrate_after_event, hipStream_t s,
+                                const RenderArgs* view) {
     const bool sem = v->p.flags & SEMTSDF_F_SEMANTIC;
+    if (sem && !mask_d) return fail(SEMTSDF_ERR_INVALID, "semantic volume needs a mask");
+    const bool fused = view && sem && v->n_obs > 0;
+    if (view && !fused)
+        if (int rc = launch_view(v, *view, s)) return rc;
     if (sem) {
-        if (!mask_d) return fail(SEMTSDF_ERR_INVALID, "semantic volume needs a mask");
         if (v->n_obs > 0) {
-            int rc = associate_impl(v, mask_d, E, s, false, true);
+            int rc = associate_impl(v, mask_d, E, s, false, true, fused ? view : nullptr);
             if (rc) return rc;
         } else {
             if (int rc = tables_ready(v, s)) return rc;
@@ -1125,6 +1142,21 @@ int semtsdf_parse_frame_dev_after(semtsdf_vol* v, const uint16_t* depth_d, const
     // call and the next association on this stream both find it current
     if (sem) return ensure_bmin(v, s);
     return SEMTSDF_OK;
+}
+
+int semtsdf_parse_frame_dev_after(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d, uint8_t* mask_d,
+                                  const float E[16], void* integrate_after_event, void* stream) {
+    if (!v || !E || !depth_d || !rgb_d) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    return parse_frame_dev_impl(v, depth_d, rgb_d, mask_d, E, integrate_after_event, pick(v, stream), nullptr);
+}
+
+int semtsdf_parse_frame_view_dev(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d, uint8_t* mask_d,
+                                 const float E[16], const float s2w[16], const float c[3], int mode,
+                                 uint8_t* out_bgr_d, float* out_t_d, void* stream) {
+    if (!v || !E || !depth_d || !rgb_d || !s2w || !c || !out_bgr_d) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    RenderArgs view;
+    if (int rc = render_args(v, s2w, c, mode, out_bgr_d, out_t_d, view)) return rc;
+    return parse_frame_dev_impl(v, depth_d, rgb_d, mask_d, E, nullptr, pick(v, stream), &view);
 }
 
 // ---- Z-sharded raycast protocol ------------------------------------------------------
@@ -1366,12 +1398,13 @@ int semtsdf_orbit_camera(const float Kinv[16], float angle, float dist, float s2
     return SEMTSDF_OK;
 }
 
-static int raycast_impl(semtsdf_vol* v, const float s2w[16], const float c[3], int mode, uint8_t* out_bgr_d,
-                        float* out_t_d, hipStream_t s) {
+static int render_args(semtsdf_vol* v, const float s2w[16], const float c[3], int mode, uint8_t* out_bgr_d,
+                       float* out_t_d, RenderArgs& a) {
     if (v->p.z_nshards != 1) return fail(SEMTSDF_ERR_UNSUPPORTED, "raycast on a Z-sharded handle is not supported yet");
     if (mode == SEMTSDF_RENDER_LABEL && !(v->p.flags & SEMTSDF_F_SEMANTIC))
         return fail(SEMTSDF_ERR_STATE, "label render needs a SEMANTIC volume");
-    RenderArgs a{};
+    if (mode != SEMTSDF_RENDER_LABEL && mode != SEMTSDF_RENDER_COLOR) return fail(SEMTSDF_ERR_INVALID, "bad render mode %d", mode);
+    a = RenderArgs{};
     a.g = v->g;
     a.b = v->b;
     for (int i = 0; i < 12; ++i) a.cam.s2w[i] = s2w[i];
@@ -1384,8 +1417,16 @@ static int raycast_impl(semtsdf_vol* v, const float s2w[16], const float c[3], i
     a.palette = v->palette_d;
     a.out_bgr = out_bgr_d;
     a.out_t = out_t_d;
+    return SEMTSDF_OK;
+}
+
+static int raycast_impl(semtsdf_vol* v, const float s2w[16], const float c[3], int mode, uint8_t* out_bgr_d,
+                        float* out_t_d, hipStream_t s) {
+    RenderArgs a;
+    if (int rc = render_args(v, s2w, c, mode, out_bgr_d, out_t_d, a)) return rc;
     EventPair ep;
     if (int rc = ensure_bmin(v, s)) return rc;
+    a.b = v->b;
     // instrumentation: SEMTSDF_RAY_STATS=<file> appends per-pixel march counters and
     // per-wave timestamps of every render
     static const char* rs_path = getenv("SEMTSDF_RAY_STATS");
@@ -1407,6 +1448,15 @@ static int raycast_impl(semtsdf_vol* v, const float s2w[16], const float c[3], i
             fclose(f);
         }
     }
+    v->n_render++;
+    return SEMTSDF_OK;
+}
+
+static int launch_view(semtsdf_vol* v, const RenderArgs& view, hipStream_t s) {
+    if (int rc = ensure_bmin(v, s)) return rc;
+    RenderArgs a = view;
+    a.b = v->b;
+    HIPC(launch_render(a, s));
     v->n_render++;
     return SEMTSDF_OK;
 }

@@ -1581,8 +1581,11 @@ __device__ __forceinline__ void integrate_list(const IntegrateArgs& a, const Uni
     v.i += nwaves;
 }
 
-// Persistent wavefronts over the two live-unit lists of the frame: the free units first
-// (sdf/weight only, when the mode allows them), then the general units.
+// Persistent wavefronts over the three live-unit lists of the frame: the full free units, the
+// free units (both sdf/weight only, when the mode allows them), then the general units, the
+// pipeline chained from each list into the next.  A static round-robin share: dynamic
+// schedules (per-XCD device atomics, a whole-CU workgroup sharing an LDS queue) evened the
+// waves' end times but ran slower.
 #ifndef SEMTSDF_INTEGRATE_WPE
 #define SEMTSDF_INTEGRATE_WPE 4  // waves per SIMD the register allocation targets (5 spills; measured equal)
 #endif
@@ -1679,11 +1682,11 @@ static unsigned resident_grid_cus() {
 }
 
 template <typename K>
-static unsigned resident_grid(K kernel) {
+static unsigned resident_grid(K kernel, int block = 256) {
     int dev = 0, cus = 0, per = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 1024;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 1024;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 256, 0) != hipSuccess || per < 1) per = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, block, 0) != hipSuccess || per < 1) per = 1;
     return (unsigned)(cus * per);
 }
 
@@ -1694,17 +1697,18 @@ static hipError_t launch_integrate_k(const IntegrateArgs& a, hipStream_t s, hipE
     // persistent grid of the resident capacity; the waves share the list evenly, so a grid
     // past residency (the occupancy query can over-report, MI355X_MICROARCH.md) only adds
     // late waves with the same share
-    static const unsigned grid0 = resident_grid(k_integrate<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>);
+    constexpr int block = 256;
+    static const unsigned grid0 = resident_grid(k_integrate<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>, block);
     const unsigned ncu = resident_grid_cus();
     unsigned grid = grid0;
     if (kProbes && a.debug >= 100) grid = grid0 * (unsigned)(a.debug - 100) / 8u;  // probe: fraction of residency
     static const char* gpc = getenv("SEMTSDF_GRID_PER_CU");              // probe: blocks per CU
     if (gpc && atoi(gpc) > 0) grid = ncu * (unsigned)atoi(gpc);
     if (e0) {  // timing: events recorded by the dispatch itself (kernel start / end)
-        hipExtLaunchKernelGGL((k_integrate<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>), dim3(grid), dim3(256), 0, s, e0,
+        hipExtLaunchKernelGGL((k_integrate<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>), dim3(grid), dim3(block), 0, s, e0,
                               e1, 0, a, ug, list_seg_cap(ug));
     } else {
-        hipLaunchKernelGGL((k_integrate<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>), dim3(grid), dim3(256), 0, s, a, ug,
+        hipLaunchKernelGGL((k_integrate<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>), dim3(grid), dim3(block), 0, s, a, ug,
                            list_seg_cap(ug));
     }
     return hipGetLastError();
@@ -2349,17 +2353,17 @@ inline bool oct_maps(const VolBufs& b) {
     return SEMTSDF_BRICK_DIST && SEMTSDF_BRICK_OCT && b.bmin && b.bdist && b.boct;
 }
 
+// One 16x16-pixel tile (bx, by) of the association march, a whole workgroup.
 template <bool OCT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_MARCH_WPE))) void k_assoc_march(AssocArgs a) {
-    __shared__ AssocLds s;
+__device__ __forceinline__ void assoc_tile(const AssocArgs& a, AssocLds& s, int bx, int by) {
     const int tid = threadIdx.x;
     assoc_lds_clear(s);
     __syncthreads();
     const bool sparse = a.box_thresh >= 0.0f && !a.probs_out;  // see assoc_accumulate_sparse
     const long long F0 = to_fix(logf(fmaxf(0.0f, a.eps)));      // an empty bin's term
 
-    const int x = blockIdx.x * 16 + (tid & 15);
-    const int y = blockIdx.y * 16 + (tid >> 4);
+    const int x = bx * 16 + (tid & 15);
+    const int y = by * 16 + (tid >> 4);
     if (x < a.width && y < a.height) {
         float ox, oy, oz, dx, dy, dz, t;
         ray_assoc(a.cam, x, y, &ox, &oy, &oz, &dx, &dy, &dz);
@@ -2402,6 +2406,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_MAR
         if (s.c1[tid]) atomicAdd(&T->c1[tid], s.c1[tid]);
         if (s.c2[tid]) atomicAdd(&T->c2[tid], s.c2[tid]);
     }
+}
+
+template <bool OCT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_MARCH_WPE))) void k_assoc_march(AssocArgs a) {
+    __shared__ AssocLds s;
+    assoc_tile<OCT>(a, s, (int)blockIdx.x, (int)blockIdx.y);
 }
 
 hipError_t launch_assoc_march(const AssocArgs& a, hipStream_t s) {
@@ -2571,12 +2581,13 @@ __device__ __forceinline__ void shade_hit(const VolGeom& g, const VolBufs& vb, c
 
 // STATS: instrumentation build of the kernel (a run-time select of the stats pointer would
 // keep MarchStats in scratch memory)
+// One 16x16-pixel tile (bx, by) of a render, a whole workgroup.
 template <bool STATS, bool OCT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_MARCH_WPE))) void k_render(RenderArgs a) {
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15);
-    const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
+__device__ __forceinline__ void render_tile(const RenderArgs& a, int bx, int by) {
+    const int x = bx * 16 + (threadIdx.x & 15);
+    const int y = by * 16 + (threadIdx.x >> 4);
     if (x >= a.width || y >= a.height) return;
-    if (STATS && a.row1 > 0 && ((int)blockIdx.y < a.row0 || (int)blockIdx.y >= a.row1)) return;
+    if (STATS && a.row1 > 0 && (by < a.row0 || by >= a.row1)) return;
     const int px = y * a.width + x;
     float ox, oy, oz, dx, dy, dz, t;
     ray_render(a.cam, x, y, &ox, &oy, &oz, &dx, &dy, &dz);
@@ -2598,13 +2609,56 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_MAR
         q[0] = ms.iters; q[1] = ms.lookups; q[2] = ms.evals; q[3] = ms.skipped;
         const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
         const size_t npx = (size_t)a.width * a.height;
-        const unsigned wave = (blockIdx.y * gridDim.x + blockIdx.x) * 4 + (threadIdx.x >> 6);
+        const unsigned wave = (unsigned)(by * ((a.width + 15) / 16) + bx) * 4 + (threadIdx.x >> 6);
         if ((threadIdx.x & 63) == 0) {
             unsigned long long* w = reinterpret_cast<unsigned long long*>(a.ray_stats + npx * 4) + wave * 2;
             w[0] = t_start;
             w[1] = t_end;
         }
     }
+}
+
+template <bool STATS, bool OCT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_MARCH_WPE))) void k_render(RenderArgs a) {
+    render_tile<STATS, OCT>(a, (int)blockIdx.x, (int)blockIdx.y);
+}
+
+// A render of the volume and the association march of the next frame in one launch: both
+// read the same volume state (the association of frame k + 1 marches the state the live
+// view of frame k shows), and both are bound by their slowest rays, so one grid lets the
+// tiles of each fill the other's tail.  Workgroup b: tiles alternate (association, render)
+// while both have tiles left, then the rest of the larger one.
+template <bool OCT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_MARCH_WPE))) void k_march_fused(
+    AssocArgs aa, RenderArgs ra, int na, int nr) {
+    __shared__ AssocLds s;
+    const int b = (int)blockIdx.x, m = min(na, nr);
+    bool assoc;
+    int t;
+    if (b < 2 * m) {
+        assoc = (b & 1) == 0;
+        t = b >> 1;
+    } else {
+        assoc = na > nr;
+        t = b - m;
+    }
+    if (assoc) {
+        const int tx = (aa.width + 15) / 16;
+        assoc_tile<OCT>(aa, s, t % tx, t / tx);
+    } else {
+        const int tx = (ra.width + 15) / 16;
+        render_tile<false, OCT>(ra, t % tx, t / tx);
+    }
+}
+
+hipError_t launch_march_fused(const AssocArgs& aa, const RenderArgs& ra, hipStream_t s) {
+    const int na = ((aa.width + 15) / 16) * ((aa.height + 15) / 16);
+    const int nr = ((ra.width + 15) / 16) * ((ra.height + 15) / 16);
+    if (oct_maps(aa.b))
+        hipLaunchKernelGGL(k_march_fused<true>, dim3(na + nr), dim3(256), 0, s, aa, ra, na, nr);
+    else
+        hipLaunchKernelGGL(k_march_fused<false>, dim3(na + nr), dim3(256), 0, s, aa, ra, na, nr);
+    return hipGetLastError();
 }
 
 hipError_t launch_render(const RenderArgs& a, hipStream_t s) {

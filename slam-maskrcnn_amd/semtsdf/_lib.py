@@ -150,6 +150,7 @@ SIGNATURES = {
     "semtsdf_parse_frame": (_I, [_P, _P, _P, _P, _P, C.POINTER(AssocStats), _P]),
     "semtsdf_parse_frame_dev": (_I, [_P, _P, _P, _P, _P, _P]),
     "semtsdf_parse_frame_dev_after": (_I, [_P, _P, _P, _P, _P, _P, _P]),
+    "semtsdf_parse_frame_view_dev": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P]),
     "semtsdf_orbit_camera": (_I, [_P, _F, _F, _P, _P]),
     "semtsdf_raycast": (_I, [_P, _P, _P, _I, _P, _P, _P]),
     "semtsdf_raycast_dev": (_I, [_P, _P, _P, _I, _P, _P, _P]),

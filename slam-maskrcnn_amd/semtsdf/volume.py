@@ -202,6 +202,19 @@ class Volume:
                                                        C.c_void_p(integrate_after_event) if integrate_after_event
                                                        else None, stream))
 
+    def parse_frame_view_dev(self, depth_ptr: int, rgb_ptr: int, mask_ptr: int | None, E, s2w, c, mode,
+                             out_ptr: int, t_ptr: int | None = None, stream=None):
+        """parse_frame_dev plus one live view of the volume as it stands before this frame (the
+        view shown after the previous frame), rendered in the same launch as this frame's
+        association march (semtsdf_parse_frame_view_dev)."""
+        e = L.f32(E, 16)
+        s = L.f32(s2w, 16)
+        cc = L.f32(c, 3)
+        L.check(L.load().semtsdf_parse_frame_view_dev(self._h, C.c_void_p(depth_ptr), C.c_void_p(rgb_ptr),
+                                                      C.c_void_p(mask_ptr) if mask_ptr else None, L.ptr(e),
+                                                      L.ptr(s), L.ptr(cc), int(mode), C.c_void_p(out_ptr),
+                                                      C.c_void_p(t_ptr) if t_ptr else None, stream))
+
     def associate_dev(self, mask_ptr: int, E, stream=None, want_stats=False):
         e = L.f32(E, 16)
         st = L.AssocStats() if want_stats else None

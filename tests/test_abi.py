@@ -27,7 +27,7 @@ def test_library_exports_every_symbol():
     lib = L.load()
     for n in declared():
         assert hasattr(lib, n), n
-    assert lib.semtsdf_abi_version() == 7
+    assert lib.semtsdf_abi_version() == 8
 
 
 def test_structs_match_header_sizes():

@@ -780,6 +780,62 @@ def test_render_stream_beside_association_equals_serial(S, stream):
         assert np.array_equal(sa[key], sb[key]), key
 
 
+@pytest.mark.parametrize("D", [96, 160])
+def test_parse_frame_view_fused_equals_serial(S, stream, D):
+    """semtsdf_parse_frame_view_dev (the live view of the state before the frame rendered in
+    the same launch as the frame's association march) gives the same views (images and hit
+    distances, label and colour modes), relabelled masks and volume as raycast_dev followed by
+    parse_frame_dev; the first frame (no association) renders the view alone."""
+    import torch
+
+    semtsdf, L = S
+    st, frames = stream
+    dev = torch.device("cuda", 0)
+    npx = 640 * 480
+    d_in = [torch.from_numpy(fr.depth.reshape(-1).view(np.int16)).to(dev) for fr in frames]
+    r_in = [torch.from_numpy(fr.rgb.reshape(-1)).to(dev) for fr in frames]
+    m_in = [torch.from_numpy(np.ascontiguousarray(fr.mask).reshape(-1)).to(dev) for fr in frames]
+    torch.cuda.synchronize()
+
+    def run(fused):
+        p = semtsdf.default_params(D, KI, 640, 480)
+        semtsdf.place_from_frame(p, frames[0].depth, float(np.mean(frames[0].depth[frames[0].depth > 0])) / 5000.0,
+                                 L.PLACE_SFM)
+        p.flags = L.F_SEMANTIC | L.F_GATE_COLOR
+        vol = semtsdf.Volume(p, 0)
+        masks = [m.clone() for m in m_in]
+        torch.cuda.synchronize()
+        views = []
+        for k in range(len(frames)):
+            fr = frames[k]
+            E = (fr.w2c @ frames[0].c2w).astype(np.float32)
+            out = torch.zeros(npx * 3, dtype=torch.uint8, device=dev)
+            tt = torch.zeros(npx, dtype=torch.float32, device=dev)
+            s2w, c = semtsdf.orbit_camera(list(p.Kinv), 0.05 * k, 1.5)
+            mode = L.RENDER_COLOR if k % 3 == 2 else L.RENDER_LABEL
+            if fused:
+                vol.parse_frame_view_dev(d_in[k].data_ptr(), r_in[k].data_ptr(), masks[k].data_ptr(), E, s2w, c, mode,
+                                         out.data_ptr(), tt.data_ptr())
+            else:
+                vol.raycast_dev(s2w, c, mode, out.data_ptr(), tt.data_ptr())
+                vol.parse_frame_dev(d_in[k].data_ptr(), r_in[k].data_ptr(), masks[k].data_ptr(), E)
+            views += [out, tt]
+        vol.sync()
+        torch.cuda.synchronize()
+        state = vol.download(hist=True)
+        res = [v.cpu() for v in views], [m.cpu() for m in masks]
+        vol.close()
+        return res, state
+
+    (va, ma), sa = run(False)
+    (vb, mb), sb = run(True)
+    assert sum(int(v.count_nonzero()) for v in va[::2]) > 0
+    for x, y in zip(va + ma, vb + mb):
+        assert torch.equal(x, y)
+    for key in ("sdf", "wt", "color", "hist"):
+        assert np.array_equal(sa[key], sb[key]), key
+
+
 @pytest.mark.parametrize("D", [64, 128])
 def test_gpu_histogram_matches_reference_class_count(S, oracle, D):
     """The HIP label path pinned to the reference's own code: a semantic, ungated volume
