@@ -33,6 +33,7 @@ The N = 1 line measures C3 (512^3), so value_N / value_1 is not a speed-up.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import hashlib
 import json
 import os
@@ -321,14 +322,15 @@ def run_pipeline(semtsdf, L, p, local, n_frames=100, n_warm=5):
             f.write("\n".join(st.tum_lines(n_all)) + "\n")
         traj = tum.read_traj(gt)  # tsdf_utils.py:23-29
     dev = torch.device("cuda", local)
-    # pinned host frames (a capture pipeline's DMA buffers)
-    h_d = torch.empty((n_all, NPX), dtype=torch.int16).pin_memory()
-    h_r = torch.empty((n_all, NPX * 3), dtype=torch.uint8).pin_memory()
-    h_m = torch.empty((n_all, NPX), dtype=torch.uint8).pin_memory()
+    # pinned host frames (a capture pipeline's buffers): depth u16, rgb u8x3, mask u8 of a
+    # frame back to back, copied by one kernel (semtsdf_memcpy kind 4: the runtime's DMA copy
+    # from pinned memory blocked the host loop for the transfer, tools/host_overhead.py)
+    h_all = torch.empty((n_all, NPX * 6), dtype=torch.uint8).pin_memory()
     for k, fr in enumerate(frames):
-        h_d[k].copy_(torch.from_numpy(fr.depth.reshape(-1).view(np.int16)))
-        h_r[k].copy_(torch.from_numpy(fr.rgb.reshape(-1)))
-        h_m[k].copy_(torch.from_numpy(fr.mask.reshape(-1)))
+        h_all[k, :NPX * 2].copy_(torch.from_numpy(fr.depth.reshape(-1).view(np.uint8)))
+        h_all[k, NPX * 2:NPX * 5].copy_(torch.from_numpy(fr.rgb.reshape(-1)))
+        h_all[k, NPX * 5:].copy_(torch.from_numpy(fr.mask.reshape(-1)))
+    lib = L.load()
     mean_m = tum.mean_depth_m(frames[0].depth)
     ext0_inv = np.linalg.inv(P.parse_pos(traj[0, 1:]))  # frame 0 places the volume (tsdf.cu:173-214)
 
@@ -337,10 +339,11 @@ def run_pipeline(semtsdf, L, p, local, n_frames=100, n_warm=5):
         vstream = torch.cuda.ExternalStream(vol.stream, device=dev)
         cstream = torch.cuda.Stream(device=dev)
         rstream = torch.cuda.Stream(device=dev) if overlap else vstream
-        ring = 2
-        d_d = torch.empty((ring, NPX), dtype=torch.int16, device=dev)
-        d_r = torch.empty((ring, NPX * 3), dtype=torch.uint8, device=dev)
-        d_m = torch.empty((ring, NPX), dtype=torch.uint8, device=dev)
+        # frame k + ring - lag is uploaded after frame k into the slot frame k - lag used
+        ring, lag = 4, 2
+        d_all = torch.empty((ring, NPX * 6), dtype=torch.uint8, device=dev)
+        slot = [(d_all[s].data_ptr(), d_all[s].data_ptr() + NPX * 2, d_all[s].data_ptr() + NPX * 5)
+                for s in range(ring)]
         outs = [torch.empty(NPX * 3, dtype=torch.uint8, device=dev) for _ in range(2)]
         copied = [torch.cuda.Event() for _ in range(ring)]
         used = [torch.cuda.Event() for _ in range(ring)]
@@ -350,28 +353,25 @@ def run_pipeline(semtsdf, L, p, local, n_frames=100, n_warm=5):
 
         def upload(k):
             s = k % ring
-            with torch.cuda.stream(cstream):
-                cstream.wait_event(used[s])
-                d_d[s].copy_(h_d[k], non_blocking=True)
-                d_r[s].copy_(h_r[k], non_blocking=True)
-                d_m[s].copy_(h_m[k], non_blocking=True)
-                copied[s].record(cstream)
+            cstream.wait_event(used[s])
+            L.check(lib.semtsdf_memcpy(ctypes.c_void_p(slot[s][0]), ctypes.c_void_p(h_all[k].data_ptr()), NPX * 6, 4,
+                                       ctypes.c_void_p(cstream.cuda_stream)))
+            copied[s].record(cstream)
 
         def frame(k, first):
             s = k % ring
             E = P.relative_pose(P.parse_pos(traj[k, 1:]), ext0_inv)  # host pose path (tsdf.cu:217)
             vstream.wait_event(copied[s])
             after = rendered.cuda_event if (overlap and not first) else None
+            pd, pr, pm = slot[s]
             if fused:  # the view shown after frame k - 1, in the launch of frame k's association
                 s2w, c = semtsdf.orbit_camera(list(p.Kinv), 0.01 * (k - 1), mean_m)
-                vol.parse_frame_view_dev(d_d[s].data_ptr(), d_r[s].data_ptr(), d_m[s].data_ptr(), E, s2w, c,
-                                         L.RENDER_LABEL, outs[(k - 1) % 2].data_ptr())
+                vol.parse_frame_view_dev(pd, pr, pm, E, s2w, c, L.RENDER_LABEL, outs[(k - 1) % 2].data_ptr())
                 used[s].record(vstream)
-                if k + ring < n_all:
-                    upload(k + ring)
+                if k + ring - lag < n_all:
+                    upload(k + ring - lag)
                 return
-            vol.parse_frame_dev(d_d[s].data_ptr(), d_r[s].data_ptr(), d_m[s].data_ptr(), E,
-                                integrate_after_event=after)
+            vol.parse_frame_dev(pd, pr, pm, E, integrate_after_event=after)
             used[s].record(vstream)
             s2w, c = semtsdf.orbit_camera(list(p.Kinv), 0.01 * k, mean_m)
             if overlap:
@@ -380,10 +380,10 @@ def run_pipeline(semtsdf, L, p, local, n_frames=100, n_warm=5):
             vol.raycast_dev(s2w, c, L.RENDER_LABEL, outs[k % 2].data_ptr(), stream=rstream.cuda_stream)
             if overlap:
                 rendered.record(rstream)
-            if k + ring < n_all:
-                upload(k + ring)
+            if k + ring - lag < n_all:
+                upload(k + ring - lag)
 
-        for k in range(ring):
+        for k in range(ring - lag):
             upload(1 + k)
         for k in range(1, 1 + n_warm):
             frame(k, k == 1)
@@ -447,7 +447,7 @@ def run_pipeline(semtsdf, L, p, local, n_frames=100, n_warm=5):
         "overlapped_frames_per_s": n_frames / t_ovl,
         "overlapped_equals_serial": same,
         "frames": n_frames, "warmup_frames": n_warm,
-        "per_frame": "host TUM pose (read_traj -> parse_pos) + async pinned H2D of depth/RGB/mask on a copy stream "
+        "per_frame": "host TUM pose (read_traj -> parse_pos) + H2D of depth/RGB/mask from pinned memory by a copy kernel on a copy stream "
                      "+ association raycast + relabel + integrate + 1 label raycast view; frames_per_s: the view "
                      "of the state after frame k-1 is rendered in the launch of frame k's association march "
                      "(semtsdf_parse_frame_view_dev: the view a viewer shows after frame k-1, one frame later); "

@@ -125,7 +125,9 @@ int semtsdf_stream_destroy(void* stream);
 int semtsdf_stream_sync(void* stream);
 int semtsdf_dev_malloc(void** out, size_t bytes);
 int semtsdf_dev_free(void* ptr);
-/* kind: 1 = host->device, 2 = device->host, 3 = device->device (async on stream) */
+/* kind: 1 = host->device, 2 = device->host, 3 = device->device (async on stream);
+ * 4 = a copy kernel on stream reading a device-accessible source (pinned host memory),
+ *     16-B aligned pointers and size: does not block the calling thread */
 int semtsdf_memcpy(void* dst, const void* src, size_t bytes, int kind, void* stream);
 
 /* ---- parameters / placement (a1) --------------------------------------------------- */

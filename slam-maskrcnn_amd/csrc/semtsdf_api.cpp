@@ -89,6 +89,7 @@ struct semtsdf_vol {
     } fs[2];
     int next_set = 0;
     hipStream_t prep_stream = nullptr;   // created on the first asynchronous integrate
+    hipEvent_t in_ev = nullptr;          // parse_frame: the caller's work before the frame (inputs ready)
     bool async_used = false;
     // association state
     AssocTables* tables_d = nullptr;
@@ -166,6 +167,7 @@ void free_all(semtsdf_vol* v) {
         if (f.set_free) (void)hipEventDestroy(f.set_free);
     }
     if (v->prep_stream) (void)hipStreamDestroy(v->prep_stream);
+    if (v->in_ev) (void)hipEventDestroy(v->in_ev);
     if (v->stream) (void)hipStreamDestroy(v->stream);
 }
 
@@ -358,9 +360,12 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
     if (a.debug == 2) return SEMTSDF_OK;
     // a deferred relabel of this frame's association is applied by the prepass (in place):
     // that prepass follows the association on s
+    // asynchronous with a pending relabel: the prepass writes the frame's raw labels beside
+    // the association, and the relabel of the mask and of the records' label bytes follows
+    // the decision on s (k_relabel_records)
     const uint8_t* lut = mask_d ? v->pending_lut : nullptr;
     v->pending_lut = nullptr;
-    if (lut) async = false;
+    const bool relabel_after = async && lut;
     if (async && !v->prep_stream) {
         int lo = 0, hi = 0;
         if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
@@ -385,7 +390,7 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
     EventPair epp;
     timing_begin(v, v->ev_prep, ps, &epp);
     HIPC(launch_depth_pyramid(depth_d, rgb_d, const_cast<uint8_t*>(mask_d), v->p.width, v->p.height, v->p.depth_scale,
-                              F.pyr, F.list_count, ps, lut));
+                              F.pyr, F.list_count, ps, relabel_after ? nullptr : lut));
     HIPC(launch_cull(a, ps));
     timing_end(v, v->ev_prep, ps, &epp);
     v->n_prep++;
@@ -393,6 +398,8 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
         HIPC(hipEventRecord(F.prep_done, ps));
         HIPC(hipStreamWaitEvent(s, F.prep_done, 0));
     }
+    if (relabel_after)
+        HIPC(launch_relabel_records(const_cast<uint8_t*>(mask_d), (int)npx(v), F.pyr.px, v->decision_d, s));
     // the volume's writer: after the last empty-space map update
     if (int rc = after_bmin(v, s)) return rc;
     v->wmax_bound += 1;
@@ -667,6 +674,11 @@ int semtsdf_memcpy(void* dst, const void* src, size_t bytes, int kind, void* str
         case 1: k = hipMemcpyHostToDevice; break;
         case 2: k = hipMemcpyDeviceToHost; break;
         case 3: k = hipMemcpyDeviceToDevice; break;
+        case 4:  // a copy kernel: the source is read by the GPU (pinned host memory over the bus)
+            if (((uintptr_t)dst | (uintptr_t)src | bytes) & 15u)
+                return fail(SEMTSDF_ERR_INVALID, "kernel copy needs 16-B aligned pointers and size");
+            HIPC(launch_copy_host(src, dst, bytes / 16, (hipStream_t)stream));
+            return SEMTSDF_OK;
         default: return fail(SEMTSDF_ERR_INVALID, "bad memcpy kind %d", kind);
     }
     HIPC(hipMemcpyAsync(dst, src, bytes, k, (hipStream_t)stream));
@@ -1121,6 +1133,13 @@ static int parse_frame_dev_impl(semtsdf_vol* v, const uint16_t* depth_d, const u
     const bool fused = view && sem && v->n_obs > 0;
     if (view && !fused)
         if (int rc = launch_view(v, *view, s)) return rc;
+    // with an association, the frame's prepass (depth pyramid, cull) runs on the prep stream
+    // beside the march (it reads only the frame's inputs), from the work queued so far on s
+    const bool overlap_prep = sem && v->n_obs > 0 && !integrate_after_event;
+    if (overlap_prep) {
+        if (!v->in_ev) HIPC(hipEventCreateWithFlags(&v->in_ev, hipEventDisableTiming));
+        HIPC(hipEventRecord(v->in_ev, s));
+    }
     if (sem) {
         if (v->n_obs > 0) {
             int rc = associate_impl(v, mask_d, E, s, false, true, fused ? view : nullptr);
@@ -1134,7 +1153,8 @@ static int parse_frame_dev_impl(semtsdf_vol* v, const uint16_t* depth_d, const u
     // the integrate is the frame's only write of the volume: readers of the previous state on
     // other streams (a live render) finish first; the association above, a read, may overlap them
     if (integrate_after_event) HIPC(hipStreamWaitEvent(s, (hipEvent_t)integrate_after_event, 0));
-    int rc = integrate_impl(v, depth_d, rgb_d, sem ? mask_d : nullptr, nullptr, E, s);
+    int rc = integrate_impl(v, depth_d, rgb_d, sem ? mask_d : nullptr, nullptr, E, s, overlap_prep,
+                            overlap_prep ? v->in_ev : nullptr);
     if (rc) return relabel_unconsumed(v, mask_d, s, rc);
     v->n_obs++;
     // the next frame's association (and a live view) march this state: refresh the

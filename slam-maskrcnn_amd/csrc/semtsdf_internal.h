@@ -265,8 +265,10 @@ hipError_t launch_assoc_decide(AssocTables* t, AssocDecision* d, int num_objs, f
                                int* num_objs_dev, hipStream_t s);
 hipError_t launch_first_frame_objs(const AssocTables* t, int* num_objs_dev, hipStream_t s);
 hipError_t launch_relabel(uint8_t* mask, int npx, const AssocDecision* d, hipStream_t s);
+hipError_t launch_relabel_records(uint8_t* mask, int npx, uint2* rec, const AssocDecision* d, hipStream_t s);
 hipError_t launch_render(const RenderArgs& a, hipStream_t s);
 hipError_t launch_march_fused(const AssocArgs& aa, const RenderArgs& ra, hipStream_t s);
+hipError_t launch_copy_host(const void* src, void* dst, size_t n16, hipStream_t s);
 // chunk [v0, v0+nv) of the bin-major histogram <-> voxel-major [nv][32] staging buffer
 hipError_t launch_hist_chunk_to_vm(const uint32_t* bm, uint32_t* vm, const VolGeom& g, uint64_t v0, uint64_t nv,
                                    hipStream_t s);

@@ -170,6 +170,17 @@ hipError_t launch_copy_f4(const void* src, void* dst, size_t n16, hipStream_t s)
     return hipGetLastError();
 }
 
+// Copy from device-accessible host memory (pinned) by a kernel on a few CUs: the runtime's DMA
+// copy from pinned memory measured as blocking the calling thread for the whole transfer while
+// the volume's kernels run (tools/host_overhead.py), which stalls a host loop feeding frames.
+hipError_t launch_copy_host(const void* src, void* dst, size_t n16, hipStream_t s) {
+    if (n16 == 0) return hipSuccess;
+    size_t blocks = (n16 + 255) / 256;
+    if (blocks > 64) blocks = 64;
+    hipLaunchKernelGGL(k_copy_f4, dim3((unsigned)blocks), dim3(256), 0, s, (const f32x4*)src, (f32x4*)dst, n16);
+    return hipGetLastError();
+}
+
 // dst[i] = min(dst[i], src[i]) over int64: the in-process stand-in of an all-reduce MIN
 // (shards driven from one process, semtsdf_min_i64)
 __global__ __launch_bounds__(256) void k_min_i64(long long* __restrict__ dst, const long long* __restrict__ src, size_t n) {
@@ -2531,6 +2542,46 @@ hipError_t launch_relabel(uint8_t* mask, int npx, const AssocDecision* d, hipStr
     int blocks = (npx + 255) / 256;
     if (blocks > 512) blocks = 512;
     hipLaunchKernelGGL(k_relabel, dim3(blocks), dim3(256), 0, s, mask, npx, d);
+    return hipGetLastError();
+}
+
+// The relabel of a frame whose prepass ran beside its association march (raw labels in the
+// pixel records): the mask in place and the label byte of each pixel record (records of
+// four pixels per lane when the mask is 4-byte aligned).
+__global__ __launch_bounds__(256) void k_relabel_records(uint8_t* __restrict__ mask, int npx, uint2* __restrict__ rec,
+                                                         const AssocDecision* __restrict__ d) {
+    __shared__ unsigned char s_lut[256];
+    s_lut[threadIdx.x] = d->lut[threadIdx.x];
+    __syncthreads();
+    const bool vec = ((uintptr_t)mask & 3u) == 0 && (npx & 3) == 0;
+    if (vec) {
+        const int n4 = npx >> 2;
+        for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
+            const unsigned m4 = reinterpret_cast<const unsigned*>(mask)[i];
+            unsigned o4 = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const unsigned m = s_lut[(m4 >> (8 * j)) & 0xFFu];
+                o4 |= m << (8 * j);
+                uint2& r = rec[4 * i + j];
+                r.y = (r.y & 0x00FFFFFFu) | (m << 24);
+            }
+            reinterpret_cast<unsigned*>(mask)[i] = o4;
+        }
+        return;
+    }
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < npx; i += gridDim.x * blockDim.x) {
+        const unsigned m = s_lut[mask[i]];
+        mask[i] = (uint8_t)m;
+        rec[i].y = (rec[i].y & 0x00FFFFFFu) | (m << 24);
+    }
+}
+
+hipError_t launch_relabel_records(uint8_t* mask, int npx, uint2* rec, const AssocDecision* d, hipStream_t s) {
+    int blocks = (npx / 4 + 255) / 256;
+    if (blocks > 512) blocks = 512;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_relabel_records, dim3(blocks), dim3(256), 0, s, mask, npx, rec, d);
     return hipGetLastError();
 }
 

@@ -785,7 +785,10 @@ def test_parse_frame_view_fused_equals_serial(S, stream, D):
     """semtsdf_parse_frame_view_dev (the live view of the state before the frame rendered in
     the same launch as the frame's association march) gives the same views (images and hit
     distances, label and colour modes), relabelled masks and volume as raycast_dev followed by
-    parse_frame_dev; the first frame (no association) renders the view alone."""
+    parse_frame_dev, and as the host-pointer parse_frame (whose prepass runs after the
+    decision and relabels in place, where the device paths run the prepass beside the march
+    and relabel the mask and the pixel records after it); the first frame (no association)
+    renders the view alone."""
     import torch
 
     semtsdf, L = S
@@ -813,7 +816,13 @@ def test_parse_frame_view_fused_equals_serial(S, stream, D):
             tt = torch.zeros(npx, dtype=torch.float32, device=dev)
             s2w, c = semtsdf.orbit_camera(list(p.Kinv), 0.05 * k, 1.5)
             mode = L.RENDER_COLOR if k % 3 == 2 else L.RENDER_LABEL
-            if fused:
+            if fused == "host":
+                vol.raycast_dev(s2w, c, mode, out.data_ptr(), tt.data_ptr())
+                vol.sync()
+                m = np.ascontiguousarray(frames[k].mask.copy())
+                vol.parse_frame(fr.depth, fr.rgb, m, E)
+                masks[k].copy_(torch.from_numpy(m.reshape(-1)))
+            elif fused:
                 vol.parse_frame_view_dev(d_in[k].data_ptr(), r_in[k].data_ptr(), masks[k].data_ptr(), E, s2w, c, mode,
                                          out.data_ptr(), tt.data_ptr())
             else:
@@ -828,12 +837,13 @@ def test_parse_frame_view_fused_equals_serial(S, stream, D):
         return res, state
 
     (va, ma), sa = run(False)
-    (vb, mb), sb = run(True)
     assert sum(int(v.count_nonzero()) for v in va[::2]) > 0
-    for x, y in zip(va + ma, vb + mb):
-        assert torch.equal(x, y)
-    for key in ("sdf", "wt", "color", "hist"):
-        assert np.array_equal(sa[key], sb[key]), key
+    for variant in (True, "host"):
+        (vb, mb), sb = run(variant)
+        for x, y in zip(va + ma, vb + mb):
+            assert torch.equal(x, y), variant
+        for key in ("sdf", "wt", "color", "hist"):
+            assert np.array_equal(sa[key], sb[key]), (variant, key)
 
 
 @pytest.mark.parametrize("D", [64, 128])
