@@ -1533,6 +1533,22 @@ struct KindOf {
     static constexpr bool FREE = KIND != 0, FULL = KIND == 2;
 };
 
+// The project / classify / load stages of the wave's first group of list v (v.i < v.ngroups).
+template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT, bool SHARD, bool PIN, int KIND>
+__device__ __forceinline__ void list_prime(const IntegrateArgs& a, const UnitGrid& ug, unsigned seg_cap,
+                                           const ListView& v, Pipe& S, unsigned& n_touch, unsigned& n_gate) {
+    constexpr bool FREE = KindOf<KIND>::FREE, FULL = KindOf<KIND>::FULL;
+    const int lane = threadIdx.x & 63;
+    const unsigned coff = (unsigned)lane_zq(lane) * 32u + (unsigned)lane_y(lane) * 4u;
+    unsigned e[kSlots];
+    group_entries(v, v.i, seg_cap, e);
+    S.cur = lane_pos(ug, e);
+    stage_project<SHARD, PIN, FREE, FULL>(a, S.cur, lane, S.P);
+    stage_classify<SEM, GATE, VOTE, COUNT, FREE>(a, S.P, S.C, true, n_touch, n_gate);
+    stage_load<SEM, CI32, VOTE, FREE>(a, S.cur, coff, S.C, S.L);
+    S.primed = true;
+}
+
 // One list (kind KIND) by one persistent wave, software-pipelined.  The wave's last unit of
 // the list is computed and stored under the project / classify / load of its first unit of
 // the next list (kind NKIND, `nx`; NKIND < 0: none), which then starts primed: the pipeline
@@ -1547,15 +1563,10 @@ __device__ __forceinline__ void integrate_list(const IntegrateArgs& a, const Uni
     const int lane = threadIdx.x & 63;
     // the lane's offset from the unit origin (a volume has < 2^31 stored voxels per x-plane pair)
     const unsigned coff = (unsigned)lane_zq(lane) * 32u + (unsigned)lane_y(lane) * 4u;
-    if (!S.primed) {
-        if (v.i >= v.ngroups) return;  // no group of this list for the wave (the next list primes itself)
-        unsigned e[kSlots];
-        group_entries(v, v.i, seg_cap, e);
-        S.cur = lane_pos(ug, e);
-        stage_project<SHARD, PIN, FREE, FULL>(a, S.cur, lane, S.P);
-        stage_classify<SEM, GATE, VOTE, COUNT, FREE>(a, S.P, S.C, true, n_touch, n_gate);
-        stage_load<SEM, CI32, VOTE, FREE>(a, S.cur, coff, S.C, S.L);
-    }
+    // no group of this list for the wave: the next list primes itself (a primed pipeline
+    // always holds a unit of the first list, in order, that has a group for the wave)
+    if (v.i >= v.ngroups) return;
+    if (!S.primed) list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, KIND>(a, ug, seg_cap, v, S, n_touch, n_gate);
     unsigned en[kSlots];
     if (v.i + nwaves < v.ngroups) group_entries(v, v.i + nwaves, seg_cap, en);
     const bool chain = NKIND >= 0 && SEMTSDF_CHAIN && nx->i < nx->ngroups;
@@ -1615,9 +1626,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
         return i0 < ng ? (ng - 1u - i0) / nwaves + 1u : 0u;
     };
     if (SEMTSDF_WAVE_TRACE) tr[0] = wall_clock64();
+    // the reciprocal table is first read by a compute stage: the wave primes its first group
+    // (gathers and state loads in flight) before the workgroup's barrier
     for (int i = (int)threadIdx.x; i < kRcpTable; i += (int)blockDim.x) s_rcp[i] = a.rcp_table[i];
-    __syncthreads();
-    if (SEMTSDF_WAVE_TRACE) tr[1] = tr[2] = tr[3] = wall_clock64();
     const int lane = threadIdx.x & 63;
     unsigned n_touch = 0, n_gate = 0, n_lazy = 0;
     unsigned nlive = 0;
@@ -1633,6 +1644,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
         ListView v1 = list_view(lst + lstride, cnt + kCnt, wave, nwaves, vf.ngroups % nwaves);
         rot0 = (vf.ngroups + v1.ngroups) % nwaves;
         ListView v0 = list_view(lst, cnt, wave, nwaves, rot0);
+        if (vf.i < vf.ngroups)
+            list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 2>(a, ug, seg_cap, vf, S, n_touch, n_gate);
+        else if (v1.i < v1.ngroups)
+            list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 1>(a, ug, seg_cap, v1, S, n_touch, n_gate);
+        else if (v0.i < v0.ngroups)
+            list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0>(a, ug, seg_cap, v0, S, n_touch, n_gate);
+        __syncthreads();
+        if (SEMTSDF_WAVE_TRACE) tr[1] = tr[2] = tr[3] = wall_clock64();
         integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 2, 1>(a, ug, seg_cap, s_rcp, vf, &v1, nwaves, S,
                                                                        n_touch, n_gate, n_lazy);
         if (SEMTSDF_WAVE_TRACE) tr[2] = wall_clock64();
@@ -1652,6 +1671,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
         if (COUNT) nlive += v1.total + vf.total;
     } else {
         ListView v0 = list_view(lst, cnt, wave, nwaves, 0u);
+        if (v0.i < v0.ngroups)
+            list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0>(a, ug, seg_cap, v0, S, n_touch, n_gate);
+        __syncthreads();
+        if (SEMTSDF_WAVE_TRACE) tr[1] = tr[2] = tr[3] = wall_clock64();
         integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0, -1>(a, ug, seg_cap, s_rcp, v0, nullptr, nwaves, S,
                                                                         n_touch, n_gate, n_lazy);
         n0 = v0.total;
