@@ -90,7 +90,6 @@ struct semtsdf_vol {
     int next_set = 0;
     hipStream_t prep_stream = nullptr;   // created on the first asynchronous integrate
     hipEvent_t in_ev = nullptr;          // parse_frame: the caller's work before the frame (inputs ready)
-    hipEvent_t stats_ev = nullptr;       // parse_frame: the frame's mask statistics (prep stream) done
     bool async_used = false;
     // association state
     AssocTables* tables_d = nullptr;
@@ -169,7 +168,6 @@ void free_all(semtsdf_vol* v) {
     }
     if (v->prep_stream) (void)hipStreamDestroy(v->prep_stream);
     if (v->in_ev) (void)hipEventDestroy(v->in_ev);
-    if (v->stats_ev) (void)hipEventDestroy(v->stats_ev);
     if (v->stream) (void)hipStreamDestroy(v->stream);
 }
 
@@ -311,7 +309,6 @@ int ensure_prep_stream(semtsdf_vol* v) {
         HIPC(hipEventCreateWithFlags(&f.prep_done, hipEventDisableTiming));
         HIPC(hipEventCreateWithFlags(&f.set_free, hipEventDisableTiming));
     }
-    HIPC(hipEventCreateWithFlags(&v->stats_ev, hipEventDisableTiming));
     return SEMTSDF_OK;
 }
 
@@ -521,20 +518,16 @@ int tables_ready(semtsdf_vol* v, hipStream_t s) {
 // integrate's prepass (v->pending_lut), saving a launch.
 // view (optional): a render of the same volume state launched together with the march
 // (k_march_fused); its arguments were validated by the caller.
-// stats_done (optional): the frame's mask statistics were launched by the caller (on the prep
-// stream, after the tables were made ready on s); the decision waits for this event.
 int associate_impl(semtsdf_vol* v, uint8_t* mask_d, const float E[16], hipStream_t s, bool want_decision,
-                   bool defer_relabel = false, const RenderArgs* view = nullptr, hipEvent_t stats_done = nullptr) {
+                   bool defer_relabel = false, const RenderArgs* view = nullptr) {
     if (v->p.z_nshards != 1) return fail(SEMTSDF_ERR_UNSUPPORTED, "association on a Z-sharded handle is not supported yet");
     if (!(v->p.flags & SEMTSDF_F_SEMANTIC)) return fail(SEMTSDF_ERR_STATE, "association needs a SEMANTIC volume");
     if (v->n_obs == 0) return fail(SEMTSDF_ERR_STATE, "association needs n_obs > 0 (tsdf.cu:426)");
     EventPair ep;
     timing_begin(v, v->ev_assoc, s, &ep);
     if (int rc = ensure_bmin(v, s)) return rc;
-    if (!stats_done) {
-        if (int rc = tables_ready(v, s)) return rc;
-        HIPC(launch_mask_stats(mask_d, (int)npx(v), v->tables_d, s));
-    }
+    if (int rc = tables_ready(v, s)) return rc;
+    HIPC(launch_mask_stats(mask_d, (int)npx(v), v->tables_d, s));
     AssocArgs a{};
     a.g = v->g;
     a.b = v->b;
@@ -558,7 +551,6 @@ int associate_impl(semtsdf_vol* v, uint8_t* mask_d, const float E[16], hipStream
     } else {
         HIPC(launch_assoc_march(a, s));
     }
-    if (stats_done) HIPC(hipStreamWaitEvent(s, stats_done, 0));
     HIPC(launch_assoc_decide(v->tables_d, v->decision_d, 0, v->p.prior_mrcnn_err_rate, v->num_objs_d, s));
     v->tables_clean = true;  // the decide kernel clears them
     if (defer_relabel)
@@ -1132,6 +1124,9 @@ int semtsdf_parse_frame_dev(semtsdf_vol* v, const uint16_t* depth_d, const uint8
     return semtsdf_parse_frame_dev_after(v, depth_d, rgb_d, mask_d, E, nullptr, stream);
 }
 
+#ifndef SEMTSDF_OVERLAP_PREP
+#define SEMTSDF_OVERLAP_PREP 1  // parse_frame_dev paths: the frame prepass on the prep stream beside the march
+#endif
 static int launch_view(semtsdf_vol* v, const RenderArgs& view, hipStream_t s);
 static int render_args(semtsdf_vol* v, const float s2w[16], const float c[3], int mode, uint8_t* out_bgr_d,
                        float* out_t_d, RenderArgs& a);
@@ -1148,21 +1143,16 @@ static int parse_frame_dev_impl(semtsdf_vol* v, const uint16_t* depth_d, const u
         if (int rc = launch_view(v, *view, s)) return rc;
     // with an association, the frame's prepass (depth pyramid, cull) runs on the prep stream
     // beside the march (it reads only the frame's inputs), from the work queued so far on s
-    // (and so do the mask statistics, ahead of it)
-    const bool overlap_prep = sem && v->n_obs > 0 && !integrate_after_event;
+    // (the mask statistics stay on s: on the prep stream they slowed the fused view + march
+    // launch, 2.45 -> 2.20 k frames/s same-box, profiles/r03/s2/ab_pipeline_mask_stats.txt)
+    const bool overlap_prep = SEMTSDF_OVERLAP_PREP && sem && v->n_obs > 0 && !integrate_after_event;
     if (overlap_prep) {
-        if (int rc = ensure_prep_stream(v)) return rc;
-        if (int rc = tables_ready(v, s)) return rc;
         if (!v->in_ev) HIPC(hipEventCreateWithFlags(&v->in_ev, hipEventDisableTiming));
         HIPC(hipEventRecord(v->in_ev, s));
-        HIPC(hipStreamWaitEvent(v->prep_stream, v->in_ev, 0));
-        HIPC(launch_mask_stats(mask_d, (int)npx(v), v->tables_d, v->prep_stream));
-        HIPC(hipEventRecord(v->stats_ev, v->prep_stream));
     }
     if (sem) {
         if (v->n_obs > 0) {
-            int rc = associate_impl(v, mask_d, E, s, false, true, fused ? view : nullptr,
-                                    overlap_prep ? v->stats_ev : nullptr);
+            int rc = associate_impl(v, mask_d, E, s, false, true, fused ? view : nullptr);
             if (rc) return rc;
         } else {
             if (int rc = tables_ready(v, s)) return rc;
