@@ -590,7 +590,7 @@ def run_mask_overlap(semtsdf, L, p, local, frames, f0, n_frames=48, n_warm=4, ge
 
 
 # ----------------------------------------------------------------------------- C2
-def run_c2(semtsdf, L, local, frames, f0, K=30, warmup=3):
+def run_c2(semtsdf, L, local, frames, f0, K=30, warmup=3, traffic_json=None):
     """C2: 256^3 TSDF + colour (NumPy rule: int32 colour, no gate), synthetic stream."""
     D = 256
     p = place(semtsdf, L, D, f0)
@@ -618,6 +618,7 @@ def run_c2(semtsdf, L, local, frames, f0, K=30, warmup=3):
     vol.close()
     dbuf.free()
     rbuf.free()
+    c2_traffic, c2_src = read_traffic(traffic_json, D, 1)
     return {
         "workload": "C2: 256^3 TSDF + colour (sdf f32, weight i32, colour i32x3, NumPy rule: colour ungated), "
                     "synthetic 640x480 stream, ground-truth poses",
@@ -629,7 +630,9 @@ def run_c2(semtsdf, L, local, frames, f0, K=30, warmup=3):
         "live_units_per_frame": int(tc.bricks / K),
         "roofline": {"bound": "hbm", "achieved": round(b / (kern_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(b / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "traffic": c2_traffic, "traffic_source": c2_src,
                      "algorithmic_bytes_per_launch": int(b), "bytes_rule": "22 N_touch + 5 W H (SURVEY §8d)"},
+        "touched_mvox_per_s": round(touched / (kern_ms * 1e-3) / 1e6, 1),
     }
 
 
@@ -808,6 +811,8 @@ def main():
     ap.add_argument("--cpu-planes", type=int, default=64)
     ap.add_argument("--cpu-slabs", type=int, default=10)
     ap.add_argument("--cpu-workers", type=int, default=0, help="N-core CPU baseline workers (0 = host cores)")
+    ap.add_argument("--c2-traffic-json", default=os.path.join(ROOT, "profiles", "traffic_c2_latest.json"),
+                    help="PMC bytes per launch of the C2 integrate (tools/diag_c2.sh)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="per-launch HBM bytes of the integrate kernel from rocprofv3 PMC (tools/traffic.py)")
     args = ap.parse_args()
@@ -898,7 +903,7 @@ def main():
         elif args.only == "masks":
             r = run_mask_overlap(semtsdf, L, p, local, frames, f0)
         elif args.only == "c2":
-            r = run_c2(semtsdf, L, local, frames, f0, args.steps, args.warmup)
+            r = run_c2(semtsdf, L, local, frames, f0, args.steps, args.warmup, args.c2_traffic_json)
         else:
             r = run_c4_single(semtsdf, L, local, frames, f0, args.steps, args.warmup)
         print(json.dumps({"only": args.only, args.only: r}), flush=True)
@@ -952,7 +957,7 @@ def main():
     if not args.no_pipeline and emu_world <= 1:
         pipeline, orbit = run_pipeline(semtsdf, L, p, local)
         masks = run_mask_overlap(semtsdf, L, p, local, frames, f0)
-        c2 =run_c2(semtsdf, L, local, frames, f0, args.steps, args.warmup)
+        c2 = run_c2(semtsdf, L, local, frames, f0, args.steps, args.warmup, args.c2_traffic_json)
         if not args.no_c4:
             c4 = run_c4_single(semtsdf, L, local, frames, f0, args.steps, args.warmup)
     copy_bw = copy_bandwidth(local) if not args.no_pipeline else None

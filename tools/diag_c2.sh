@@ -13,5 +13,8 @@ step bench $?
 BENCH_ARGS="--only c2 --steps 10 --warmup 2" bash $R/tools/pmc_integrate.sh gpurun_out/$TAG/pmc FETCH_SIZE WRITE_SIZE \
   "SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" > $O/pmc.log 2>&1
 step pmc $?
-python3 $R/tools/pmc_summary.py $O/pmc "k_integrate<false, false, true, false, false, false, true>" > $O/pmc_summary.txt 2>&1
+KER="k_integrate<false, false, false, false, false, false, true>"
+python3 $R/tools/pmc_summary.py $O/pmc "$KER" > $O/pmc_summary.txt 2>&1
 step pmc_summary $?
+python3 $R/tools/traffic.py $O/pmc "$KER" $O/traffic.json 256 > $O/traffic.log 2>&1
+step traffic $?

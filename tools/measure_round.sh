@@ -22,10 +22,10 @@ step traffic $?
 python3 $R/tools/pmc_summary.py $O/pmc "$KER" > $O/pmc_summary.txt 2>&1
 step pmc_summary $?
 cd $R
-timeout -k 10 600 python3 bench.py --traffic-json $O/traffic.json > $O/bench.json 2> $O/bench.err
+timeout -k 10 600 python3 bench.py --traffic-json $O/traffic.json ${C2_TRAFFIC:+--c2-traffic-json $C2_TRAFFIC} > $O/bench.json 2> $O/bench.err
 step bench $?
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python3 $R/bench.py --no-cpu-baseline --traffic-json $O/traffic.json > $O/bench_prof.json 2> $O/bench_prof.err
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python3 $R/bench.py --no-cpu-baseline --no-pipeline --traffic-json $O/traffic.json > $O/bench_prof.json 2> $O/bench_prof.err
 step rocprof_stats $?
 cd $R
 bash $R/tools/pmc_march.sh gpurun_out/$TAG/pmcm > $O/pmcm_summary.txt 2>&1
