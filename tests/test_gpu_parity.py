@@ -846,6 +846,58 @@ def test_parse_frame_view_fused_equals_serial(S, stream, D):
             assert np.array_equal(sa[key], sb[key]), (variant, key)
 
 
+def test_parse_frame_ragged_image_device_equals_host_and_oracle(S, oracle, stream):
+    """A 637 x 479 image (pixel count not a multiple of 4, rows not 4-aligned): the device
+    parse path (prepass beside the march, the relabel of mask and pixel records after the
+    decision, k_relabel_records' per-pixel path) equals the host-pointer parse_frame and the
+    C oracle (masks, object counts, every array)."""
+    import torch
+
+    semtsdf, L = S
+    st, frames = stream
+    Wr, Hr = 637, 479
+    dev = torch.device("cuda", 0)
+    crop = [(np.ascontiguousarray(fr.depth[:Hr, :Wr]), np.ascontiguousarray(fr.rgb[:Hr, :Wr]),
+             np.ascontiguousarray(fr.mask[:Hr, :Wr])) for fr in frames]
+
+    def make_vol():
+        p = semtsdf.default_params(64, KI, Wr, Hr)
+        semtsdf.place_from_frame(p, crop[0][0], float(np.mean(crop[0][0][crop[0][0] > 0])) / 5000.0, L.PLACE_SFM)
+        p.flags = L.F_SEMANTIC | L.F_GATE_COLOR
+        return p, semtsdf.Volume(p, 0)
+
+    p, vh = make_vol()
+    _, vd = make_vol()
+    g = oracle.OGeom.from_params(p)
+    ost = oracle.OState([64] * 3, p.mu, semantic=True)
+    num = 0
+    for k in range(1, len(frames)):
+        d, c, m = crop[k]
+        E = (frames[k].w2c @ frames[0].c2w).astype(np.float32)
+        mh = m.copy()
+        vh.parse_frame(d, c, mh, E)
+        dd = torch.from_numpy(d.reshape(-1).view(np.int16)).to(dev)
+        cd = torch.from_numpy(c.reshape(-1)).to(dev)
+        md = torch.from_numpy(m.reshape(-1).copy()).to(dev)
+        torch.cuda.synchronize()
+        vd.parse_frame_dev(dd.data_ptr(), cd.data_ptr(), md.data_ptr(), E)
+        vd.sync()
+        m_ref = m.copy()
+        if k == 1:
+            num = int(m_ref.max()) + 1
+        else:
+            probs, box = oracle.march_probs(g, list(p.Kinv), E, Wr, Hr, ost.sdf, ost.hist, p.box_thresh)
+            m_ref, num, _, _, _ = oracle.filter_overlaps(probs, box, m_ref, k - 1, num, p.prior_mrcnn_err_rate, 1)
+        oracle.integrate(g, ost, list(p.K), E, d, c, m_ref, flags=0x3)
+        assert np.array_equal(mh, m_ref), f"host mask, frame {k}"
+        assert np.array_equal(md.cpu().numpy().reshape(Hr, Wr), m_ref), f"device mask, frame {k}"
+        assert vh.state().num_objs == num and vd.state().num_objs == num
+    assert_same(vh, ost, hist=True)
+    assert_same(vd, ost, hist=True)
+    vh.close()
+    vd.close()
+
+
 @pytest.mark.parametrize("D", [64, 128])
 def test_gpu_histogram_matches_reference_class_count(S, oracle, D):
     """The HIP label path pinned to the reference's own code: a semantic, ungated volume
