@@ -404,7 +404,7 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
         HIPC(hipStreamWaitEvent(s, F.prep_done, 0));
     }
     if (relabel_after)
-        HIPC(launch_relabel_records(const_cast<uint8_t*>(mask_d), (int)npx(v), F.pyr.px, v->decision_d, s));
+        HIPC(launch_relabel_records(const_cast<uint8_t*>(mask_d), v->p.width, v->p.height, F.pyr, v->decision_d, s));
     // the volume's writer: after the last empty-space map update
     if (int rc = after_bmin(v, s)) return rc;
     v->wmax_bound += 1;
@@ -857,8 +857,12 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
         DepthPyramid& pyr = f.pyr;
         pyr.w0 = (p->width + 7) / 8; pyr.h0 = (p->height + 7) / 8;
         pyr.w1 = (p->width + 31) / 32; pyr.h1 = (p->height + 31) / 32;
-        if ((rc = dev_alloc(v, (void**)&pyr.px, (px + 1) * 8))) return bail(rc);
-        if (hipMemset(pyr.px, 0, (px + 1) * 8) != hipSuccess) return bail(fail(SEMTSDF_ERR_HIP, "memset failed"));
+        pyr.tw = (p->width + 3) / 4;
+        pyr.zero = (unsigned)pyr.tw * (unsigned)((p->height + 3) / 4) * 16u;
+        // the records of the padding pixels of edge tiles and the zero record stay zero
+        const size_t nrec = (size_t)pyr.zero + 1;
+        if ((rc = dev_alloc(v, (void**)&pyr.px, nrec * 8))) return bail(rc);
+        if (hipMemset(pyr.px, 0, nrec * 8) != hipSuccess) return bail(fail(SEMTSDF_ERR_HIP, "memset failed"));
         if ((rc = dev_alloc(v, (void**)&pyr.l0, (size_t)pyr.w1 * 4 * pyr.h1 * 4 * sizeof(uint2)))) return bail(rc);
         if ((rc = dev_alloc(v, (void**)&pyr.l1, (size_t)pyr.w1 * pyr.h1 * sizeof(uint2)))) return bail(rc);
         if ((rc = dev_alloc(v, (void**)&f.unit_list, unit_list_capacity(g) * sizeof(unsigned)))) return bail(rc);

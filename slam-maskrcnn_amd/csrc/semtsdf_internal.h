@@ -86,13 +86,23 @@ struct VolBufs {
 // nonzero raw depth (bits 16-31; 0 when the tile has no nonzero pixel), used by the unit
 // culler (dead units, and free units whose touched voxels all have f == 1).
 struct DepthPyramid {
-    uint2* px;      // [H][W] pixel records {bits of depth / depth_scale (IEEE, tsdf.cu:49),
-                    //                       r | g << 8 | b << 16 | label << 24}: one 8-B gather per voxel;
-                    // record W*H is zero (the target of off-image voxels)
+    uint2* px;      // pixel records {bits of depth / depth_scale (IEEE, tsdf.cu:49),
+                    //                r | g << 8 | b << 16 | label << 24}: one 8-B gather per voxel,
+                    // in 4 x 4-pixel tiles of one 128-B line each (rec_index): the voxels of a
+                    // unit project onto a compact patch of the image, which then spans few lines;
+                    // record `zero` (after the tiles) is zero: the target of off-image voxels
     uint2* l0;  // [ceil(H/8)][ceil(W/8)]  {max | (0xFFFF - min nonzero) << 16, 1 if a pixel has depth 0}
     uint2* l1;  // [ceil(H/32)][ceil(W/32)]
     int w0, h0, w1, h1;
+    int tw;         // 4-pixel tiles per image row: ceil(W / 4)
+    unsigned zero;  // index of the zero record: ceil(W / 4) * ceil(H / 4) * 16
 };
+
+// Pixel record of pixel (u, v): 4 x 4 tiles, 16 records (one 128-B line) each, the tile's rows
+// of 4 consecutive records.
+__device__ inline unsigned rec_index(const DepthPyramid& p, unsigned u, unsigned v) {
+    return ((__umul24(v >> 2, (unsigned)p.tw) + (u >> 2)) << 4) | ((v & 3u) << 2) | (u & 3u);
+}
 
 struct IntegrateArgs {
     VolGeom g;
@@ -265,7 +275,7 @@ hipError_t launch_assoc_decide(AssocTables* t, AssocDecision* d, int num_objs, f
                                int* num_objs_dev, hipStream_t s);
 hipError_t launch_first_frame_objs(const AssocTables* t, int* num_objs_dev, hipStream_t s);
 hipError_t launch_relabel(uint8_t* mask, int npx, const AssocDecision* d, hipStream_t s);
-hipError_t launch_relabel_records(uint8_t* mask, int npx, uint2* rec, const AssocDecision* d, hipStream_t s);
+hipError_t launch_relabel_records(uint8_t* mask, int w, int h, const DepthPyramid& p, const AssocDecision* d, hipStream_t s);
 hipError_t launch_render(const RenderArgs& a, hipStream_t s);
 hipError_t launch_march_fused(const AssocArgs& aa, const RenderArgs& ra, hipStream_t s);
 hipError_t launch_copy_host(const void* src, void* dst, size_t n16, hipStream_t s);

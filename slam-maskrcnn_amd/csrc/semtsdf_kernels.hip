@@ -498,8 +498,8 @@ __global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restric
                 o.z = (c1 >> 16) | ((c2 & 0xFFu) << 16) | (((lab >> 16) & 0xFFu) << 24);
                 o.w = (c2 >> 8) | ((lab >> 24) << 24);
             }
-            // depth[img] / 5000.f (tsdf.cu:49), once per pixel
-            uint4* dst = reinterpret_cast<uint4*>(p.px + px0);
+            // depth[img] / 5000.f (tsdf.cu:49), once per pixel; x0 % 4 == 0: one tile row
+            uint4* dst = reinterpret_cast<uint4*>(p.px + rec_index(p, (unsigned)x0, (unsigned)yy));
             dst[0] = make_uint4(__float_as_uint((float)d[0] / scale), o.x, __float_as_uint((float)d[1] / scale), o.y);
             dst[1] = make_uint4(__float_as_uint((float)d[2] / scale), o.z, __float_as_uint((float)d[3] / scale), o.w);
         } else {
@@ -519,7 +519,7 @@ __global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restric
                     c = (unsigned)rgb[px * 3] | ((unsigned)rgb[px * 3 + 1] << 8) | ((unsigned)rgb[px * 3 + 2] << 16) |
                         (lab << 24);
                 }
-                p.px[px] = make_uint2(__float_as_uint((float)d / scale), c);
+                p.px[rec_index(p, (unsigned)(x0 + k), (unsigned)yy)] = make_uint2(__float_as_uint((float)d / scale), c);
             }
         }
     }
@@ -920,7 +920,8 @@ constexpr unsigned kFlagMax = 255u;  // s - 1 <= 254 pending increments
 struct Proj {
     float qz[4];
     uint2 rec[4];  // gathered pixel record {metres bits, rgbl}
-    int img[4];    // pixel index; W*H (the zero record) off-image or on an invalid plane
+    int img[4];    // record index (rec_index); pyr.zero (the zero record) off-image or on an invalid plane
+    int lin[4];    // vote mode: the pixel's row-major index, W*H off-image
     unsigned sflag;  // steady flag of the lane's sdf line (below)
 };
 
@@ -974,7 +975,7 @@ struct Out {
 
 // Screen position s = M p + m (DESIGN.md §4 contract; per-row bases then one fma per
 // coordinate per voxel), the exact pixel through the reciprocal, and the record gather.
-template <bool SHARD, bool PIN, bool FREE, bool FULL>
+template <bool SHARD, bool PIN, bool FREE, bool FULL, bool LIN>
 __device__ __forceinline__ void stage_project(const IntegrateArgs& a, const UnitPos& up, int lane, Proj& P) {
     const VolGeom& g = a.g;
     if (FULL) {  // full free unit (unit_cull == 3): every voxel touched with f == 1, nothing to project
@@ -1038,7 +1039,8 @@ __device__ __forceinline__ void stage_project(const IntegrateArgs& a, const Unit
         const int iu = cvt_flr(q.x), iv = cvt_flr(q.y);  // the window holds only |q| < 2^23
         slow |= ((zok & !fast) ? 1u : 0u) << k;
         const bool in = zok & fast & ((unsigned)iu < (unsigned)a.width) & ((unsigned)iv < (unsigned)a.height);
-        P.img[k] = in ? (int)__umul24((unsigned)iv, (unsigned)a.width) + iu : npx;
+        P.img[k] = in ? (int)rec_index(a.pyr, (unsigned)iu, (unsigned)iv) : (int)a.pyr.zero;
+        if (LIN) P.lin[k] = in ? (int)__umul24((unsigned)iv, (unsigned)a.width) + iu : npx;
     }
     if (slow) {  // rare: exact IEEE quotients (the screen position is recomputed)
 #pragma unroll
@@ -1049,7 +1051,8 @@ __device__ __forceinline__ void stage_project(const IntegrateArgs& a, const Unit
             const float sx = fmaf(a.M[2], pz, bsx), sy = fmaf(a.M[5], pz, bsy), sz = fmaf(a.M[8], pz, bsz);
             const int ix = f2i_rd(sx / sz), iy = f2i_rd(sy / sz);
             const bool in = ix >= 0 && ix < a.width && iy >= 0 && iy < a.height;
-            P.img[k] = in ? iy * a.width + ix : npx;
+            P.img[k] = in ? (int)rec_index(a.pyr, (unsigned)ix, (unsigned)iy) : (int)a.pyr.zero;
+            if (LIN) P.lin[k] = in ? iy * a.width + ix : npx;
         }
     }
     // steady flag of the lane's sdf line (one byte per 128-B line, unconditional)
@@ -1109,7 +1112,7 @@ __device__ __forceinline__ void stage_classify(const IntegrateArgs& a, const Pro
         dslow |= ((t & !(fabsf(dc) >= 0x1p-60f)) ? 1u : 0u) << k;
         tmask |= (t ? 1u : 0u) << k;
         C.pix[k] = P.rec[k].y;
-        if (VOTE) C.img[k] = P.img[k];
+        if (VOTE) C.img[k] = P.lin[k];
     }
     C.sflag = P.sflag;
     if (dslow || !a.fastdiv) {  // rare: tiny differences, or mu outside the reciprocal range
@@ -1543,7 +1546,7 @@ __device__ __forceinline__ void list_prime(const IntegrateArgs& a, const UnitGri
     unsigned e[kSlots];
     group_entries(v, v.i, seg_cap, e);
     S.cur = lane_pos(ug, e);
-    stage_project<SHARD, PIN, FREE, FULL>(a, S.cur, lane, S.P);
+    stage_project<SHARD, PIN, FREE, FULL, VOTE>(a, S.cur, lane, S.P);
     stage_classify<SEM, GATE, VOTE, COUNT, FREE>(a, S.P, S.C, true, n_touch, n_gate);
     stage_load<SEM, CI32, VOTE, FREE>(a, S.cur, coff, S.C, S.L);
     S.primed = true;
@@ -1575,7 +1578,7 @@ __device__ __forceinline__ void integrate_list(const IntegrateArgs& a, const Uni
     while (v.i + nwaves < v.ngroups) {
         const UnitPos nxt = lane_pos(ug, en);
         if (v.i + 2u * nwaves < v.ngroups) group_entries(v, v.i + 2u * nwaves, seg_cap, en);
-        stage_project<SHARD, PIN, FREE, FULL>(a, nxt, lane, S.P);
+        stage_project<SHARD, PIN, FREE, FULL, VOTE>(a, nxt, lane, S.P);
         stage_compute<SEM, GATE, CI32, VOTE, FREE>(a, s_rcp, S.C, S.L, S.O);
         const StoreMeta Mc = store_meta(S.C);
         stage_classify<SEM, GATE, VOTE, COUNT, FREE>(a, S.P, S.C, true, n_touch, n_gate);
@@ -1587,7 +1590,7 @@ __device__ __forceinline__ void integrate_list(const IntegrateArgs& a, const Uni
     // the wave's last unit of this list
     if (NKIND >= 0 && SEMTSDF_CHAIN && chain) {
         const UnitPos nxt = lane_pos(ug, eb);
-        stage_project<SHARD, PIN, NFREE, NFULL>(a, nxt, lane, S.P);
+        stage_project<SHARD, PIN, NFREE, NFULL, VOTE>(a, nxt, lane, S.P);
         stage_compute<SEM, GATE, CI32, VOTE, FREE>(a, s_rcp, S.C, S.L, S.O);
         const StoreMeta Mc = store_meta(S.C);
         stage_classify<SEM, GATE, VOTE, COUNT, NFREE>(a, S.P, S.C, true, n_touch, n_gate);
@@ -2569,42 +2572,46 @@ hipError_t launch_relabel(uint8_t* mask, int npx, const AssocDecision* d, hipStr
 }
 
 // The relabel of a frame whose prepass ran beside its association march (raw labels in the
-// pixel records): the mask in place and the label byte of each pixel record (records of
-// four pixels per lane when the mask is 4-byte aligned).
-__global__ __launch_bounds__(256) void k_relabel_records(uint8_t* __restrict__ mask, int npx, uint2* __restrict__ rec,
+// pixel records): the mask in place and the label byte of each pixel record.  One image row
+// per blockIdx.y; four pixels per lane when the rows are 4-byte aligned (one tile row of
+// records).
+__global__ __launch_bounds__(256) void k_relabel_records(uint8_t* __restrict__ mask, int w, int h, DepthPyramid p,
                                                          const AssocDecision* __restrict__ d) {
     __shared__ unsigned char s_lut[256];
     s_lut[threadIdx.x] = d->lut[threadIdx.x];
     __syncthreads();
-    const bool vec = ((uintptr_t)mask & 3u) == 0 && (npx & 3) == 0;
-    if (vec) {
-        const int n4 = npx >> 2;
-        for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
-            const unsigned m4 = reinterpret_cast<const unsigned*>(mask)[i];
-            unsigned o4 = 0;
+    const bool vec = ((uintptr_t)mask & 3u) == 0 && (w & 3) == 0;
+    for (int y = blockIdx.y; y < h; y += gridDim.y) {
+        uint8_t* row = mask + (size_t)y * w;
+        if (vec) {
+            for (int x4 = blockIdx.x * blockDim.x + threadIdx.x; x4 < (w >> 2); x4 += gridDim.x * blockDim.x) {
+                const unsigned m4 = reinterpret_cast<const unsigned*>(row)[x4];
+                unsigned o4 = 0;
+                uint2* r = p.px + rec_index(p, (unsigned)(4 * x4), (unsigned)y);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const unsigned m = s_lut[(m4 >> (8 * j)) & 0xFFu];
-                o4 |= m << (8 * j);
-                uint2& r = rec[4 * i + j];
+                for (int j = 0; j < 4; ++j) {
+                    const unsigned m = s_lut[(m4 >> (8 * j)) & 0xFFu];
+                    o4 |= m << (8 * j);
+                    r[j].y = (r[j].y & 0x00FFFFFFu) | (m << 24);
+                }
+                reinterpret_cast<unsigned*>(row)[x4] = o4;
+            }
+        } else {
+            for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < w; x += gridDim.x * blockDim.x) {
+                const unsigned m = s_lut[row[x]];
+                row[x] = (uint8_t)m;
+                uint2& r = p.px[rec_index(p, (unsigned)x, (unsigned)y)];
                 r.y = (r.y & 0x00FFFFFFu) | (m << 24);
             }
-            reinterpret_cast<unsigned*>(mask)[i] = o4;
         }
-        return;
-    }
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < npx; i += gridDim.x * blockDim.x) {
-        const unsigned m = s_lut[mask[i]];
-        mask[i] = (uint8_t)m;
-        rec[i].y = (rec[i].y & 0x00FFFFFFu) | (m << 24);
     }
 }
 
-hipError_t launch_relabel_records(uint8_t* mask, int npx, uint2* rec, const AssocDecision* d, hipStream_t s) {
-    int blocks = (npx / 4 + 255) / 256;
-    if (blocks > 512) blocks = 512;
-    if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(k_relabel_records, dim3(blocks), dim3(256), 0, s, mask, npx, rec, d);
+hipError_t launch_relabel_records(uint8_t* mask, int w, int h, const DepthPyramid& p, const AssocDecision* d,
+                                  hipStream_t s) {
+    const int bx = ((w + 3) / 4 + 255) / 256;
+    const int by = h < 512 ? (h > 0 ? h : 1) : 512;
+    hipLaunchKernelGGL(k_relabel_records, dim3(bx, by), dim3(256), 0, s, mask, w, h, p, d);
     return hipGetLastError();
 }
 
