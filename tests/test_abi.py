@@ -40,3 +40,26 @@ def test_structs_match_header_sizes():
     assert C.sizeof(L.AssocStats) == 4 * (2 + 32 + 32) + 256
     # semtsdf_timing: 5 doubles-or-u64 groups of 8 bytes each, 14 fields
     assert C.sizeof(L.Timing) == 8 * 14
+
+
+def test_argument_errors_without_a_device():
+    """Argument checks of the ABI 8 entry points return errors (and a message) before any
+    GPU work: NULL handles/pointers, misaligned kernel copies, bad memcpy kinds."""
+    import ctypes as C
+
+    from semtsdf import _lib as L
+
+    lib = L.load()
+    E = (C.c_float * 16)()
+    s2w = (C.c_float * 16)()
+    c = (C.c_float * 3)()
+    buf = C.c_void_p(0x1000)
+    rc = lib.semtsdf_parse_frame_view_dev(None, buf, buf, buf, E, s2w, c, L.RENDER_LABEL, buf, None, None)
+    assert rc != 0 and b"NULL" in lib.semtsdf_last_error()
+    # kernel copy (kind 4): 16-B alignment of both pointers and the size is checked first
+    rc = lib.semtsdf_memcpy(C.c_void_p(0x1004), C.c_void_p(0x2000), 64, 4, None)
+    assert rc != 0 and b"16-B" in lib.semtsdf_last_error()
+    rc = lib.semtsdf_memcpy(C.c_void_p(0x1000), C.c_void_p(0x2000), 40, 4, None)
+    assert rc != 0 and b"16-B" in lib.semtsdf_last_error()
+    rc = lib.semtsdf_memcpy(C.c_void_p(0x1000), C.c_void_p(0x2000), 64, 7, None)
+    assert rc != 0 and b"kind" in lib.semtsdf_last_error()
