@@ -679,11 +679,21 @@ int semtsdf_memcpy(void* dst, const void* src, size_t bytes, int kind, void* str
         case 1: k = hipMemcpyHostToDevice; break;
         case 2: k = hipMemcpyDeviceToHost; break;
         case 3: k = hipMemcpyDeviceToDevice; break;
-        case 4:  // a copy kernel: the source is read by the GPU (pinned host memory over the bus)
+        case 4: {  // a copy kernel: the source is read by the GPU (pinned host memory over the bus)
             if (((uintptr_t)dst | (uintptr_t)src | bytes) & 15u)
                 return fail(SEMTSDF_ERR_INVALID, "kernel copy needs 16-B aligned pointers and size");
+            // both ends must be GPU-addressable (device memory, or host memory pinned/registered
+            // with the runtime): a kernel touching pageable memory would fault on the device
+            for (const void* ptr : {static_cast<const void*>(dst), src}) {
+                hipPointerAttribute_t at{};
+                if (hipPointerGetAttributes(&at, ptr) != hipSuccess || !at.devicePointer) {
+                    (void)hipGetLastError();
+                    return fail(SEMTSDF_ERR_INVALID, "kernel copy: %p is not device-accessible memory", ptr);
+                }
+            }
             HIPC(launch_copy_host(src, dst, bytes / 16, (hipStream_t)stream));
             return SEMTSDF_OK;
+        }
         default: return fail(SEMTSDF_ERR_INVALID, "bad memcpy kind %d", kind);
     }
     HIPC(hipMemcpyAsync(dst, src, bytes, k, (hipStream_t)stream));

@@ -1138,3 +1138,26 @@ def test_async_prepass_integrate_matches_oracle(S, oracle, stream):
     for b in (d, r, m):
         b.free()
     vol.close()
+
+
+def test_kernel_copy_from_pinned_and_refusal_of_pageable(S):
+    """semtsdf_memcpy kind 4 (the copy kernel the live loop uploads frames with) copies from
+    pinned host memory bit for bit, and refuses pageable host memory (a kernel reading it would
+    fault) with an error instead of launching."""
+    import ctypes as C
+
+    import torch
+
+    semtsdf, L = S
+    lib = L.load()
+    n = 640 * 480 * 6
+    h = torch.randint(0, 256, (n,), dtype=torch.uint8).pin_memory()
+    d = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    L.check(lib.semtsdf_memcpy(C.c_void_p(d.data_ptr()), C.c_void_p(h.data_ptr()), n, 4, None))
+    torch.cuda.synchronize()
+    assert torch.equal(d.cpu(), h)
+    pageable = np.zeros(n + 16, np.uint8)
+    off = (-pageable.ctypes.data) % 16
+    rc = lib.semtsdf_memcpy(C.c_void_p(d.data_ptr()), C.c_void_p(pageable.ctypes.data + off), n, 4, None)
+    assert rc != 0 and b"device-accessible" in lib.semtsdf_last_error()
