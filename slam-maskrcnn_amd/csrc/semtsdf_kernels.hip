@@ -1177,7 +1177,7 @@ __device__ __forceinline__ bool tile_line_all(bool p) {
 }
 
 #ifndef SEMTSDF_NT_LOAD
-#define SEMTSDF_NT_LOAD 1
+#define SEMTSDF_NT_LOAD 0  // nt loads measured 3-5 % slower once the pipeline was chained (r03, same box)
 #endif
 #ifndef SEMTSDF_NT_STORE
 #define SEMTSDF_NT_STORE 1
