@@ -1151,6 +1151,11 @@ __device__ __forceinline__ void stage_classify(const IntegrateArgs& a, const Pro
 #ifndef SEMTSDF_FULLROW
 #define SEMTSDF_FULLROW 1
 #endif
+// The steady flag of a line is decided from the values of all 8 lanes of the line after the
+// update, so lanes of a line must not read the dummy line when another lane of it updates
+// (a per-lane build measured 2.5 % faster and flagged unsteady lines steady: the sharded
+// GPU test caught it, profiles/r03/s2/ab_full_row.txt).
+static_assert(SEMTSDF_FULLROW || !SEMTSDF_STEADY, "steady-line flags need whole-line state traffic");
 // Whole-line state traffic: a 128-B line of a per-voxel array is the 8 lanes of one
 // z-quad (lane % 8); when any of them updates, all 8 load and store it (unchanged values
 // included), so every line written back is fully dirty.
