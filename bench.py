@@ -223,9 +223,22 @@ def loaded_lib_sha256() -> str:
         return hashlib.sha256(f.read()).hexdigest()
 
 
+def loaded_build_key() -> str | None:
+    """Key of the sources, flags and compiler the loaded library was built from: a driver-side
+    rebuild of the same sources keeps it (the .so bytes may differ)."""
+    from semtsdf import _lib as L
+
+    lib = L.load()
+    if not hasattr(lib, "semtsdf_build_key"):
+        return None
+    k = lib.semtsdf_build_key()
+    k = k.decode() if k else None
+    return None if k in (None, "unknown") else k
+
+
 def read_traffic(path, dim, world):
     """PMC bytes per launch of the integrate kernel, only if measured on this very library
-    binary (tools/traffic.py stamps its SHA-256) and configuration."""
+    build (tools/traffic.py stamps the build key and the binary's SHA-256) and configuration."""
     if not path or not os.path.exists(path):
         return None, "no traffic record"
     try:
@@ -235,6 +248,9 @@ def read_traffic(path, dim, world):
         return None, f"unreadable traffic record: {e}"
     if tj.get("dim") != dim or tj.get("n_gpus", 1) != world:
         return None, "traffic record is for another configuration"
+    key = loaded_build_key()
+    if tj.get("build_key") and key == tj["build_key"]:
+        return tj.get("bytes_per_launch"), f"PMC FETCH_SIZE x2 + WRITE_SIZE of build key {key[:12]}"
     if tj.get("lib_sha256") != loaded_lib_sha256():
         return None, "traffic record was measured on another library build"
     return tj.get("bytes_per_launch"), f"PMC FETCH_SIZE x2 + WRITE_SIZE of lib {tj['lib_sha256'][:12]}"

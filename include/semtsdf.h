@@ -118,6 +118,9 @@ typedef struct semtsdf_timing {
 /* ---- library ------------------------------------------------------------------------ */
 const char* semtsdf_last_error(void);
 int semtsdf_abi_version(void);
+/* SHA-256 (hex) of the sources, hipcc flags and compiler version the library was built from
+ * (__graft_entry__.build_key): the key PMC traffic records are stamped with. */
+const char* semtsdf_build_key(void);
 int semtsdf_device_count(int* out);
 int semtsdf_set_device(int device);
 int semtsdf_stream_create(void** out_stream);

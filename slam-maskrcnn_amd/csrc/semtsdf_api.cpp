@@ -125,6 +125,7 @@ struct semtsdf_vol {
     int64_t wmax_bound = 0;        // upper bound of every weight (uploads, +1 per integrate): byte storage
                                    // is left before a colour mean could take the int32 wrap (w >= 2^23)
     const uint8_t* pending_lut = nullptr;  // relabel table the next integrate's prepass applies
+    unsigned long long* wtrace_d = nullptr;  // instrumentation: per-wave trace slots (kWtSlots, allocated once)
     bool tables_clean = false;     // tables_d holds the cleared state (left by k_assoc_decide)
     // instrumentation
     int instr = 0;
@@ -155,7 +156,7 @@ void free_all(semtsdf_vol* v) {
                     v->fs[1].pyr.l0, v->fs[1].pyr.l1, v->tables_d, v->decision_d,
                     v->num_objs_d, v->probs_d, v->box_d, v->palette_d, v->render_d, v->render_t_d,
                     v->counters_d, v->ray_state_d, v->fs[0].unit_list, v->fs[0].list_count, v->fs[1].unit_list,
-                    v->fs[1].list_count, v->rcp_table_d};
+                    v->fs[1].list_count, v->rcp_table_d, v->wtrace_d};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (v->decision_h) (void)hipHostFree(v->decision_h);
@@ -375,8 +376,9 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
     // asynchronous with a pending relabel: the prepass writes the frame's raw labels beside
     // the association, and the relabel of the mask and of the records' label bytes follows
     // the decision on s (k_relabel_records)
+    // the pending table stays set until the launch consuming it is queued: an error before
+    // that leaves it for relabel_unconsumed (the decision already advanced num_objs)
     const uint8_t* lut = mask_d ? v->pending_lut : nullptr;
-    v->pending_lut = nullptr;
     const bool relabel_after = async && lut;
     if (async)
         if (int rc = ensure_prep_stream(v)) return rc;
@@ -396,6 +398,7 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
     timing_begin(v, v->ev_prep, ps, &epp);
     HIPC(launch_depth_pyramid(depth_d, rgb_d, const_cast<uint8_t*>(mask_d), v->p.width, v->p.height, v->p.depth_scale,
                               F.pyr, F.list_count, ps, relabel_after ? nullptr : lut));
+    if (lut && !relabel_after) v->pending_lut = nullptr;  // consumed by the prepass
     HIPC(launch_cull(a, ps));
     timing_end(v, v->ev_prep, ps, &epp);
     v->n_prep++;
@@ -403,8 +406,10 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
         HIPC(hipEventRecord(F.prep_done, ps));
         HIPC(hipStreamWaitEvent(s, F.prep_done, 0));
     }
-    if (relabel_after)
+    if (relabel_after) {
         HIPC(launch_relabel_records(const_cast<uint8_t*>(mask_d), v->p.width, v->p.height, F.pyr, v->decision_d, s));
+        v->pending_lut = nullptr;
+    }
     // the volume's writer: after the last empty-space map update
     if (int rc = after_bmin(v, s)) return rc;
     v->wmax_bound += 1;
@@ -417,11 +422,13 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
     // per-wave phase timestamps of the first 32 integrates (kWaveTraceWords u64 per wave slot)
     static const char* wt_path = getenv("SEMTSDF_WAVE_TRACE");
     static int wt_calls = 0;
-    constexpr size_t kWtSlots = 65536;
+    constexpr size_t kWtSlots = 65536;  // waves past it are not traced (the kernel checks wtrace_slots)
     const bool wt = wt_path && wt_calls < 32;
     if (wt) {
         ++wt_calls;
-        HIPC(hipMalloc((void**)&a.wtrace, kWtSlots * kWaveTraceWords * 8));
+        if (!v->wtrace_d) HIPC(hipMalloc((void**)&v->wtrace_d, kWtSlots * kWaveTraceWords * 8));
+        a.wtrace = v->wtrace_d;
+        a.wtrace_slots = (unsigned)kWtSlots;
         HIPC(hipMemsetAsync(a.wtrace, 0, kWtSlots * kWaveTraceWords * 8, s));
     }
     HIPC(launch_integrate(a, s, ep.a, ep.b));
@@ -429,7 +436,6 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
         std::vector<unsigned long long> h(kWtSlots * kWaveTraceWords);
         HIPC(hipMemcpyAsync(h.data(), a.wtrace, h.size() * 8, hipMemcpyDeviceToHost, s));
         HIPC(hipStreamSynchronize(s));
-        HIPC(hipFree(a.wtrace));
         if (FILE* f = fopen(wt_path, "ab")) {
             fwrite(h.data(), 8, h.size(), f);
             fclose(f);
@@ -632,6 +638,10 @@ extern "C" {
 
 const char* semtsdf_last_error(void) { return g_err.c_str(); }
 int semtsdf_abi_version(void) { return SEMTSDF_ABI_VERSION; }
+#ifndef SEMTSDF_BUILD_KEY
+#define SEMTSDF_BUILD_KEY "unknown"
+#endif
+const char* semtsdf_build_key(void) { return SEMTSDF_BUILD_KEY; }
 
 int semtsdf_device_count(int* out) {
     if (!out) return fail(SEMTSDF_ERR_INVALID, "out is NULL");
@@ -683,15 +693,22 @@ int semtsdf_memcpy(void* dst, const void* src, size_t bytes, int kind, void* str
             if (((uintptr_t)dst | (uintptr_t)src | bytes) & 15u)
                 return fail(SEMTSDF_ERR_INVALID, "kernel copy needs 16-B aligned pointers and size");
             // both ends must be GPU-addressable (device memory, or host memory pinned/registered
-            // with the runtime): a kernel touching pageable memory would fault on the device
-            for (const void* ptr : {static_cast<const void*>(dst), src}) {
+            // with the runtime): a kernel touching pageable memory would fault on the device.
+            // The kernel gets each end's device address, which for hipHostRegister'd memory
+            // need not equal the host address.
+            void* dev[2] = {nullptr, nullptr};
+            const void* ends[2] = {dst, src};
+            for (int e = 0; e < 2; ++e) {
                 hipPointerAttribute_t at{};
-                if (hipPointerGetAttributes(&at, ptr) != hipSuccess || !at.devicePointer) {
+                if (hipPointerGetAttributes(&at, ends[e]) != hipSuccess || !at.devicePointer) {
                     (void)hipGetLastError();
-                    return fail(SEMTSDF_ERR_INVALID, "kernel copy: %p is not device-accessible memory", ptr);
+                    return fail(SEMTSDF_ERR_INVALID, "kernel copy: %p is not device-accessible memory", ends[e]);
                 }
+                dev[e] = at.devicePointer;
+                if (((uintptr_t)dev[e]) & 15u)
+                    return fail(SEMTSDF_ERR_INVALID, "kernel copy: device address of %p is not 16-B aligned", ends[e]);
             }
-            HIPC(launch_copy_host(src, dst, bytes / 16, (hipStream_t)stream));
+            HIPC(launch_copy_host(dev[1], dev[0], bytes / 16, (hipStream_t)stream));
             return SEMTSDF_OK;
         }
         default: return fail(SEMTSDF_ERR_INVALID, "bad memcpy kind %d", kind);

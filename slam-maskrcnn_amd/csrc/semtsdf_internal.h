@@ -138,6 +138,7 @@ struct IntegrateArgs {
     int color_wide;                // colour stored as int32 x 4 (else u8 x 4; see semtsdf_vol::color_wide)
     unsigned long long* wtrace;    // instrumentation (build with SEMTSDF_WAVE_TRACE=1, run with
                                    // SEMTSDF_WAVE_TRACE=<file>): per wave kWaveTraceWords timestamps
+    unsigned wtrace_slots;         // waves wtrace holds (waves past it are not traced)
 };
 constexpr int kWaveTraceWords = 8;
 

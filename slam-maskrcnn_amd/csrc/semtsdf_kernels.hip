@@ -17,10 +17,9 @@
 //   mix    = fmaf(t, b, (1-t)*a)                                 (utils.cu:94-96)
 //   normalize(v) = v * (1/sqrtf(dot3(v,v)))
 //
-// Memory layout: flat x-major volume, z fastest; a workgroup owns an 8(x) x 8(y) x 32(z)
-// brick and its 256 lanes map to (z, y), so every wave-instruction touches two
-// contiguous 128-B runs of the sdf/weight planes.  The histogram is bin-major
-// ([32][voxels]) so lanes that see the same instance label update contiguous words.
+// Memory layout: every per-voxel array in 1x8x32 (x, y, z) tiles of 256
+// consecutive voxels, ordered (z/4, y, z%4) inside the tile (tile_index); the histogram is
+// bin-major ([32][voxels]) so lanes that see the same instance label update contiguous words.
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 #include <stdint.h>
@@ -28,6 +27,10 @@
 #include <stddef.h>
 #include <stdlib.h>
 #include "semtsdf_internal.h"
+
+#ifndef SEMTSDF_LAZY_WEIGHT
+#define SEMTSDF_LAZY_WEIGHT 0  // lazy weights (k_integrate): measured slower, off by default
+#endif
 
 namespace semtsdf {
 
@@ -428,6 +431,7 @@ __global__ __launch_bounds__(256) void k_flush_lazy(int32_t* __restrict__ wt, ui
 }
 
 hipError_t launch_flush_lazy(const VolGeom& g, const VolBufs& b, hipStream_t s) {
+    if (!SEMTSDF_LAZY_WEIGHT) return hipSuccess;  // no pending counts exist in this build
     const uint64_t n = g.nvox;
     if (n == 0) return hipSuccess;  // a shard that owns no chunk
     const unsigned grid = (unsigned)((n + 255) / 256 < 65536 ? (n + 255) / 256 : 65536);
@@ -906,9 +910,6 @@ __device__ __forceinline__ uint64_t unit_tile(const VolGeom& g, const UnitPos& u
 // s - 1 pending increments of every weight of the line.  Any other update of the line adds
 // the pending count first (stage_compute), and k_flush_lazy folds the counts into the weights
 // before they are read out (download, upload, checkpoint).
-#ifndef SEMTSDF_LAZY_WEIGHT
-#define SEMTSDF_LAZY_WEIGHT 0  // measured slower: the kernel is issue-bound, not traffic-bound
-#endif
 #ifndef SEMTSDF_CHAIN
 #define SEMTSDF_CHAIN 1  // a wave's last unit of a list overlaps the first unit of its next list
 #endif
@@ -1687,7 +1688,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
                                                                         n_touch, n_gate, n_lazy);
         n0 = v0.total;
     }
-    if (SEMTSDF_WAVE_TRACE && a.wtrace) {
+    if (SEMTSDF_WAVE_TRACE && a.wtrace && wave < a.wtrace_slots) {
         tr[4] = wall_clock64();
         trn |= groups_of(n0, rot0) << 40;
         if (lane < 8) {

@@ -123,6 +123,7 @@ _PP = C.POINTER(C.c_void_p)
 SIGNATURES = {
     "semtsdf_last_error": (C.c_char_p, []),
     "semtsdf_abi_version": (_I, []),
+    "semtsdf_build_key": (C.c_char_p, []),
     "semtsdf_device_count": (_I, [C.POINTER(C.c_int)]),
     "semtsdf_set_device": (_I, [_I]),
     "semtsdf_stream_create": (_I, [_PP]),

@@ -5,6 +5,6 @@ set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 N=$1; shift
 mkdir -p $R/build
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared -std=c++17 "$@" \
-  $R/slam-maskrcnn_amd/csrc/semtsdf_kernels.hip $R/slam-maskrcnn_amd/csrc/semtsdf_api.cpp -o $R/build/var_$N.so
+cd $R && python3 -c "import sys, __graft_entry__ as g; g.build_lib(force=True, extra_flags=sys.argv[2:], out=sys.argv[1])" \
+  $R/build/var_$N.so "$@"
 echo built build/var_$N.so

@@ -25,6 +25,19 @@ def lib_sha256(path=None):
         return hashlib.sha256(f.read()).hexdigest()
 
 
+def lib_build_key(path=None):
+    """The build key compiled into the library (semtsdf_build_key, __graft_entry__.build_key)."""
+    import ctypes
+
+    path = path or os.environ.get("SEMTSDF_LIB", os.path.join(ROOT, "slam-maskrcnn_amd", "semtsdf", "libsemtsdf.so"))
+    try:
+        fn = ctypes.CDLL(path).semtsdf_build_key
+    except (OSError, AttributeError):
+        return None
+    fn.restype = ctypes.c_char_p
+    return fn().decode()
+
+
 def main():
     d, pat, out, dim = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
     n_gpus = int(sys.argv[5]) if len(sys.argv) > 5 else 1
@@ -42,7 +55,8 @@ def main():
     rec = {"kernel": pat, "dim": dim, "n_gpus": n_gpus, "dispatches": len(agg["FETCH_SIZE"]),
            "fetch_size_kib_raw": fetch_kib, "write_size_kib_raw": write_kib,
            "fetch_bytes": fetch, "write_bytes": write, "bytes_per_launch": fetch + write,
-           "correction": "FETCH_SIZE x2 (gfx950 wide-read tally), WRITE_SIZE x1", "lib_sha256": lib_sha256()}
+           "correction": "FETCH_SIZE x2 (gfx950 wide-read tally), WRITE_SIZE x1", "lib_sha256": lib_sha256(),
+           "build_key": lib_build_key()}
     with open(out, "w") as f:
         json.dump(rec, f, indent=1)
     print(json.dumps(rec))
