@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SEMTSDF_ABI_VERSION 8
+#define SEMTSDF_ABI_VERSION 9
 #define SEMTSDF_MAX_OBJECTS 32 /* tsdf.cuh:4 */
 
 /* ---- status codes ------------------------------------------------------------ */
@@ -40,6 +40,8 @@ extern "C" {
 #define SEMTSDF_ERR_STATE (-5)       /* call out of order (e.g. raycast on a sharded handle) */
 #define SEMTSDF_ERR_COMM (-6)        /* collective failure */
 #define SEMTSDF_ERR_UNSUPPORTED (-7) /* feature not available for this handle/mode */
+#define SEMTSDF_NEED_PIXELS 1        /* semtsdf_shard_assoc_apply: the decision needs the per-pixel
+                                        data of every shard (semtsdf_shard_assoc_pixels) */
 
 /* ---- volume flags -------------------------------------------------------------- */
 #define SEMTSDF_F_SEMANTIC 0x1u   /* 32-bin per-voxel instance histogram (SfM tsdf.cu:61) */
@@ -96,6 +98,9 @@ typedef struct semtsdf_assoc_stats {
     int32_t assigned_prev[SEMTSDF_MAX_OBJECTS]; /* current label i -> previous id, or -1 */
     float assigned_prob[SEMTSDF_MAX_OBJECTS];   /* exp(A/C) of the accepted match */
     uint8_t lut[256];                   /* old label -> new label applied to the mask */
+    uint32_t exact_rows;                /* bit i: current label i was decided from its exact f32
+                                           pixel-order sums (the rows the fixed-point certificate
+                                           could not decide) */
 } semtsdf_assoc_stats;
 
 /* Accumulated kernel timings (HIP events on the launch stream). */
@@ -113,6 +118,8 @@ typedef struct semtsdf_timing {
     uint64_t full_units;  /* of those, free units whose every voxel is touched (no projection; count mode only) */
     uint64_t lazy_voxels; /* touched voxels of steady lines whose +1 weight went to the line's pending count
                              instead of a weight store (count mode only) */
+    uint64_t assoc_exact_frames; /* association decisions that took the exact f32 path (always counted) */
+    uint64_t assoc_exact_rows;   /* rows decided on it, summed over those decisions */
 } semtsdf_timing;
 
 /* ---- library ------------------------------------------------------------------------ */
@@ -184,6 +191,15 @@ int semtsdf_associate_dev(semtsdf_vol* v, uint8_t* mask_d, const float E[16],
 /* Debug/parity: per-pixel probs [H*W*32] f32 and box_mask [H*W*32] u8 exactly as the
  * reference back_proj_kernel leaves them (zeros where no hit).  Host outputs. */
 int semtsdf_assoc_probs(semtsdf_vol* v, const float E[16], float* probs, uint8_t* box_mask, void* stream);
+/* TSDF::filter_overlaps (tsdf.cu:304-416) on given inputs: probs_d f32 [H*W][32], box_d u8
+ * [H*W][32] (nonzero = set), mask_d u8 [H*W] relabelled in place; n_obs, num_objs and the
+ * knobs of the handle (n_obs > 0).  The decision the association march feeds, on the
+ * reference's own function boundary (device pointers; async unless stats is given). */
+int semtsdf_filter_overlaps_dev(semtsdf_vol* v, const float* probs_d, const uint8_t* box_d, uint8_t* mask_d,
+                                semtsdf_assoc_stats* stats_host_or_null, void* stream);
+/* The association's f32 logf (fn 0) / expf (fn 1) on the device over n values (device
+ * pointers): the host C library's results bit for bit (semtsdf_libm.h), for verification. */
+int semtsdf_libm_eval(int fn, const float* x_d, float* y_d, size_t n, void* stream);
 
 /* ---- per-frame driver (a7: TSDF::parse_frame/launch_kernel tsdf.cu:171-228,418-504) ----
  * Integrated-frame count n_obs: if n_obs > 0 associate (relabels mask), else
@@ -245,6 +261,16 @@ int semtsdf_shard_assoc_partial(semtsdf_vol* v, const void* gathered_d, const ui
                                 int64_t* partial_d, void* stream);
 int semtsdf_shard_assoc_apply(semtsdf_vol* v, const int64_t* reduced_d, uint8_t* mask_d,
                               semtsdf_assoc_stats* stats, void* stream);
+/* When assoc_apply returns SEMTSDF_NEED_PIXELS (some labels are too close to call from the
+ * reduced fixed-point sums; nothing was decided or relabelled):
+ *   assoc_pixels(gathered, px): this shard's per-pixel association data, zeros for pixels it
+ *       does not own; all-reduce(SUM, int32) px over the group;
+ *   assoc_apply_exact(reduced, px_reduced, mask, stats): decide + relabel.
+ * px: SEMTSDF_ASSOC_PIXEL_WORDS int32 words per pixel (device memory). */
+#define SEMTSDF_ASSOC_PIXEL_WORDS 34
+int semtsdf_shard_assoc_pixels(semtsdf_vol* v, const void* gathered_d, int32_t* px_d, void* stream);
+int semtsdf_shard_assoc_apply_exact(semtsdf_vol* v, const int64_t* reduced_d, const int32_t* px_d, uint8_t* mask_d,
+                                    semtsdf_assoc_stats* stats, void* stream);
 /* dst[i] = min(dst[i], src[i]) over n int64 (device, async on stream): the exchange
  * SEMTSDF_EXCHANGE_MIN for shards driven from one process. */
 int semtsdf_min_i64(int64_t* dst_d, const int64_t* src_d, size_t n, void* stream);
@@ -282,7 +308,8 @@ int semtsdf_upload(semtsdf_vol* v, const float* sdf, const int32_t* wt, const vo
                    const uint32_t* hist, const int32_t* cls, const int32_t* cls_cnt);
 
 /* ---- measurement ------------------------------------------------------------------------ */
-/* enable bit0: record HIP events around kernels; bit1: count touched/gated voxels. */
+/* enable bit0: record HIP events around kernels; bit1: count touched/gated voxels; bit2: every
+ * association row takes the exact f32 path (tests and its cost measurement). */
 int semtsdf_set_instrumentation(semtsdf_vol* v, int enable);
 int semtsdf_get_timing(semtsdf_vol* v, semtsdf_timing* out); /* synchronises the stream */
 int semtsdf_reset_timing(semtsdf_vol* v);

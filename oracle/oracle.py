@@ -76,6 +76,8 @@ def lib():
         _lib.oracle_orbit_camera.restype = None
         _lib.oracle_project.argtypes = [P, P, P, P, C.c_int, C.c_int, P, C.c_int, C.c_int]
         _lib.oracle_project.restype = None
+        _lib.oracle_libm_mismatches.argtypes = [C.c_int, P, P, C.c_long, C.c_uint32]
+        _lib.oracle_libm_mismatches.restype = C.c_long
     return _lib
 
 

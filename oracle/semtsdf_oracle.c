@@ -791,3 +791,24 @@ int oracle_div_rcp_mismatches(const float* a, int n, float b) {
     }
     return bad;
 }
+
+/* ---------------------------------------------------------------- libm check
+ * Test support for the device's association log/exp (semtsdf_libm.h): number of i for which
+ * y[i] differs in bits from this C library's logf(x[i]) (fn 0) or expf(x[i]) (fn 1) -- the
+ * functions the reference's host filter_overlaps calls (tsdf.cu:318,329,343).  x[i] may be
+ * NULL-generated: when x == NULL the inputs are the consecutive float bit patterns u0 + i. */
+long oracle_libm_mismatches(int fn, const float* x, const float* y, long n, uint32_t u0) {
+    long bad = 0;
+    for (long i = 0; i < n; ++i) {
+        float xi;
+        if (x) {
+            xi = x[i];
+        } else {
+            const uint32_t u = u0 + (uint32_t)i;
+            memcpy(&xi, &u, 4);
+        }
+        const float r = fn == 0 ? logf(xi) : expf(xi);
+        if (memcmp(&r, &y[i], 4) != 0) ++bad;
+    }
+    return bad;
+}

@@ -94,6 +94,9 @@ struct semtsdf_vol {
     // association state
     AssocTables* tables_d = nullptr;
     AssocDecision* decision_d = nullptr;
+    AssocExact* exact_d = nullptr;  // the decision's exact path: flagged rows' f32 sums, counter
+    AssocPixels px{};               // per-pixel data of the last association march (exact path)
+    bool assoc_ray_done = false;    // sharded: the last ray protocol was an association (its records stand)
     int* num_objs_d = nullptr;
     float* probs_d = nullptr;     // debug only (allocated lazily)
     uint8_t* box_d = nullptr;
@@ -156,7 +159,7 @@ void free_all(semtsdf_vol* v) {
                     v->fs[1].pyr.l0, v->fs[1].pyr.l1, v->tables_d, v->decision_d,
                     v->num_objs_d, v->probs_d, v->box_d, v->palette_d, v->render_d, v->render_t_d,
                     v->counters_d, v->ray_state_d, v->fs[0].unit_list, v->fs[0].list_count, v->fs[1].unit_list,
-                    v->fs[1].list_count, v->rcp_table_d, v->wtrace_d};
+                    v->fs[1].list_count, v->rcp_table_d, v->wtrace_d, v->exact_d, v->px.bits, v->px.p};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (v->decision_h) (void)hipHostFree(v->decision_h);
@@ -520,6 +523,24 @@ int tables_ready(semtsdf_vol* v, hipStream_t s) {
     return SEMTSDF_OK;
 }
 
+// Arguments of the decision (k_assoc_decide) on the frame's raw mask; px.bits == nullptr: no
+// per-pixel data (rows needing the exact path are reported in exact_missing).
+DecideArgs decide_args(semtsdf_vol* v, const uint8_t* mask_d, AssocPixels px, bool certify_only = false) {
+    DecideArgs d{};
+    d.T = v->tables_d;
+    d.D = v->decision_d;
+    d.X = v->exact_d;
+    d.num_objs_dev = v->num_objs_d;
+    d.eps = v->p.prior_mrcnn_err_rate;
+    d.n_obs = (float)v->n_obs;
+    d.mask = mask_d;
+    d.px = px;
+    d.npx = (int)npx(v);
+    d.force_exact = (v->instr & 4) ? 1 : 0;
+    d.certify_only = certify_only ? 1 : 0;
+    return d;
+}
+
 // defer_relabel: the caller integrates this mask next; the relabel is left to that
 // integrate's prepass (v->pending_lut), saving a launch.
 // view (optional): a render of the same volume state launched together with the march
@@ -545,6 +566,7 @@ int associate_impl(semtsdf_vol* v, uint8_t* mask_d, const float E[16], hipStream
     a.box_thresh = v->p.box_thresh;
     a.mask = mask_d;
     a.tables = v->tables_d;
+    a.px = v->px;
     {
         static const char* dbg = getenv("SEMTSDF_DEBUG_ASSOC");  // timing probes only
         a.debug = dbg ? atoi(dbg) : 0;
@@ -557,7 +579,7 @@ int associate_impl(semtsdf_vol* v, uint8_t* mask_d, const float E[16], hipStream
     } else {
         HIPC(launch_assoc_march(a, s));
     }
-    HIPC(launch_assoc_decide(v->tables_d, v->decision_d, 0, v->p.prior_mrcnn_err_rate, v->num_objs_d, s));
+    HIPC(launch_assoc_decide(decide_args(v, mask_d, v->px), s));
     v->tables_clean = true;  // the decide kernel clears them
     if (defer_relabel)
         v->pending_lut = &v->decision_d->lut[0];
@@ -572,6 +594,7 @@ int associate_impl(semtsdf_vol* v, uint8_t* mask_d, const float E[16], hipStream
 void decision_to_stats(const AssocDecision& d, semtsdf_assoc_stats* st) {
     st->max_obj_now = d.max_obj_now;
     st->num_objs = d.num_objs_after;
+    st->exact_rows = d.exact_rows;
     for (int i = 0; i < kMaxObjects; ++i) {
         st->assigned_prev[i] = d.assigned_prev[i];
         st->assigned_prob[i] = d.assigned_prob[i];
@@ -905,6 +928,12 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     }
     if ((rc = dev_alloc(v, (void**)&v->tables_d, sizeof(AssocTables)))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->decision_d, sizeof(AssocDecision)))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&v->exact_d, sizeof(AssocExact)))) return bail(rc);
+    if (hipMemset(v->exact_d, 0, sizeof(AssocExact)) != hipSuccess) return bail(fail(SEMTSDF_ERR_HIP, "memset failed"));
+    if ((p->flags & SEMTSDF_F_SEMANTIC) && p->z_nshards == 1) {  // the association's per-pixel data
+        if ((rc = dev_alloc(v, (void**)&v->px.bits, npx(v) * sizeof(uint2)))) return bail(rc);
+        if ((rc = dev_alloc(v, (void**)&v->px.p, npx(v) * kMaxObjects * sizeof(float)))) return bail(rc);
+    }
     if ((rc = dev_alloc(v, (void**)&v->num_objs_d, 16))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->counters_d, kCounters * sizeof(unsigned long long)))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->palette_d, sizeof(kPalette)))) return bail(rc);
@@ -1050,6 +1079,36 @@ int semtsdf_associate_dev(semtsdf_vol* v, uint8_t* mask_d, const float E[16], se
         HIPC(hipStreamSynchronize(s));
         decision_to_stats(*v->decision_h, stats);
     }
+    return SEMTSDF_OK;
+}
+
+int semtsdf_filter_overlaps_dev(semtsdf_vol* v, const float* probs_d, const uint8_t* box_d, uint8_t* mask_d,
+                                semtsdf_assoc_stats* stats, void* stream) {
+    if (!v || !probs_d || !box_d || !mask_d) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    if (!(v->p.flags & SEMTSDF_F_SEMANTIC) || !v->px.bits)
+        return fail(SEMTSDF_ERR_STATE, "filter_overlaps needs an unsharded SEMANTIC volume");
+    if (v->n_obs == 0) return fail(SEMTSDF_ERR_STATE, "filter_overlaps needs n_obs > 0 (tsdf.cu:317 divides by it)");
+    HIPC(hipSetDevice(v->device));
+    hipStream_t s = pick(v, stream);
+    if (int rc = tables_ready(v, s)) return rc;
+    HIPC(launch_mask_stats(mask_d, (int)npx(v), v->tables_d, s));
+    HIPC(launch_assoc_from_probs(probs_d, box_d, mask_d, (int)npx(v), (float)v->n_obs, v->p.prior_mrcnn_err_rate,
+                                 v->tables_d, v->px, s));
+    HIPC(launch_assoc_decide(decide_args(v, mask_d, v->px), s));
+    v->tables_clean = true;
+    HIPC(launch_relabel(mask_d, (int)npx(v), v->decision_d, s));
+    if (stats) {
+        HIPC(hipMemcpyAsync(v->decision_h, v->decision_d, sizeof(AssocDecision), hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+        decision_to_stats(*v->decision_h, stats);
+    }
+    return SEMTSDF_OK;
+}
+
+int semtsdf_libm_eval(int fn, const float* x_d, float* y_d, size_t n, void* stream) {
+    if (fn != 0 && fn != 1) return fail(SEMTSDF_ERR_INVALID, "fn must be 0 (logf) or 1 (expf)");
+    if (n && (!x_d || !y_d)) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    HIPC(launch_libm_eval(fn, x_d, y_d, n, (hipStream_t)stream));
     return SEMTSDF_OK;
 }
 
@@ -1275,6 +1334,7 @@ int semtsdf_shard_ray_begin(semtsdf_vol* v, int kind, const float cam[16], const
     if (int rc = ensure_bmin(v, v->stream)) return rc;
     HIPC(hipStreamSynchronize(v->stream));  // the protocol's steps may run on another stream
     v->ray_kind = kind;
+    v->assoc_ray_done = false;
     v->ray_nrec = exchange == SEMTSDF_EXCHANGE_MIN ? 1 : v->p.z_nshards;
     v->ray_next = 0;
     if (record_bytes) *record_bytes = 8 * npx(v);
@@ -1339,6 +1399,44 @@ int semtsdf_shard_assoc_partial(semtsdf_vol* v, const void* gathered_d, const ui
     HIPC(launch_shard_assoc_partial(a, s));
     timing_end(v, v->ev_assoc, s, &ep);
     v->ray_kind = -1;
+    v->assoc_ray_done = true;
+    return SEMTSDF_OK;
+}
+
+int semtsdf_shard_assoc_pixels(semtsdf_vol* v, const void* gathered_d, int32_t* px_d, void* stream) {
+    if (!v || !gathered_d || !px_d) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    if (!v->assoc_ray_done) return fail(SEMTSDF_ERR_STATE, "assoc_pixels needs a completed association protocol");
+    HIPC(hipSetDevice(v->device));
+    hipStream_t s = pick(v, stream);
+    ShardRayArgs a = shard_args(v);
+    a.gathered = (const int2*)gathered_d;
+    HIPC(launch_shard_assoc_pixels(a, px_d, s));
+    return SEMTSDF_OK;
+}
+
+int semtsdf_shard_assoc_apply_exact(semtsdf_vol* v, const int64_t* reduced_d, const int32_t* px_d, uint8_t* mask_d,
+                                    semtsdf_assoc_stats* stats, void* stream) {
+    if (!v || !reduced_d || !px_d || !mask_d) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    HIPC(hipSetDevice(v->device));
+    hipStream_t s = pick(v, stream);
+    EventPair ep;
+    timing_begin(v, v->ev_assoc, s, &ep);
+    if (int rc = tables_ready(v, s)) return rc;
+    HIPC(launch_mask_stats(mask_d, (int)npx(v), v->tables_d, s));
+    HIPC(launch_tables_from_partial((const long long*)reduced_d, v->tables_d, s));
+    AssocPixels px;
+    px.bits = reinterpret_cast<uint2*>(const_cast<int32_t*>(px_d));
+    px.p = reinterpret_cast<float*>(const_cast<int32_t*>(px_d) + 2 * npx(v));
+    HIPC(launch_assoc_decide(decide_args(v, mask_d, px), s));
+    v->tables_clean = true;
+    HIPC(launch_relabel(mask_d, (int)npx(v), v->decision_d, s));
+    timing_end(v, v->ev_assoc, s, &ep);
+    v->n_assoc++;
+    if (stats) {
+        HIPC(hipMemcpyAsync(v->decision_h, v->decision_d, sizeof(AssocDecision), hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+        decision_to_stats(*v->decision_h, stats);
+    }
     return SEMTSDF_OK;
 }
 
@@ -1352,7 +1450,17 @@ int semtsdf_shard_assoc_apply(semtsdf_vol* v, const int64_t* reduced_d, uint8_t*
     if (int rc = tables_ready(v, s)) return rc;
     HIPC(launch_mask_stats(mask_d, (int)npx(v), v->tables_d, s));
     HIPC(launch_tables_from_partial((const long long*)reduced_d, v->tables_d, s));
-    HIPC(launch_assoc_decide(v->tables_d, v->decision_d, 0, v->p.prior_mrcnn_err_rate, v->num_objs_d, s));
+    // the certificate first: rows it cannot decide from the reduced sums need every pixel's
+    // data, which the shards hold in parts (semtsdf_shard_assoc_pixels)
+    HIPC(launch_assoc_decide(decide_args(v, mask_d, AssocPixels{}, true), s));
+    unsigned missing = 0;
+    HIPC(hipMemcpyAsync(&missing, &v->decision_d->exact_missing, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    if (missing) {
+        timing_end(v, v->ev_assoc, s, &ep);
+        return SEMTSDF_NEED_PIXELS;  // the tables stay filled for semtsdf_shard_assoc_apply_exact
+    }
+    HIPC(launch_assoc_decide(decide_args(v, mask_d, AssocPixels{}), s));
     v->tables_clean = true;  // the decide kernel clears them
     HIPC(launch_relabel(mask_d, (int)npx(v), v->decision_d, s));
     timing_end(v, v->ev_assoc, s, &ep);
@@ -1771,6 +1879,10 @@ int semtsdf_get_timing(semtsdf_vol* v, semtsdf_timing* out) {
     out->free_units = c[4];
     out->full_units = c[5];
     out->lazy_voxels = c[6];
+    unsigned xr[2] = {0, 0};  // AssocExact::frames, rows
+    HIPC(hipMemcpy(xr, &v->exact_d->frames, sizeof(xr), hipMemcpyDeviceToHost));
+    out->assoc_exact_frames = xr[0];
+    out->assoc_exact_rows = xr[1];
     out->prep_ms = v->t_prep;
     out->n_prep = v->n_prep;
     return SEMTSDF_OK;
@@ -1788,6 +1900,7 @@ int semtsdf_reset_timing(semtsdf_vol* v) {
     v->n_integrate = v->n_assoc = v->n_render = v->n_prep = 0;
     HIPC(hipMemset(v->counters_d, 0, 2 * sizeof(unsigned long long)));
     HIPC(hipMemset(v->counters_d + 3, 0, (kCounters - 3) * sizeof(unsigned long long)));
+    HIPC(hipMemset(&v->exact_d->frames, 0, 2 * sizeof(unsigned)));
     return SEMTSDF_OK;
 }
 

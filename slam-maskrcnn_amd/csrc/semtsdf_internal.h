@@ -157,7 +157,7 @@ struct AssocTables {
 };
 static_assert(sizeof(AssocTables) % 8 == 0, "AssocTables is cleared as 8-B words");
 
-// Decision output written by the single-workgroup decide kernel.
+// Decision output written by the decide kernel.
 struct AssocDecision {
     int max_obj_now;
     int num_objs_before;
@@ -166,6 +166,41 @@ struct AssocDecision {
     int assigned_prev[kMaxObjects];
     float assigned_prob[kMaxObjects];
     unsigned char lut[256];
+    unsigned exact_rows;    // bit i: row i decided from its exact f32 pixel-order sums
+    unsigned exact_missing; // bit i: row i needed them but no pixel data was given (decided from
+                            // the fixed-point sums; the sharded protocol then exchanges pixels)
+};
+
+// Per-pixel association data of the last march (the exact path of the decision): for pixel k
+// the bins present at its hit and its box bins (p > box_thresh), and the trilinear counts of
+// the present bins, bin-major (other entries are stale: readers test the present bit).
+struct AssocPixels {
+    uint2* bits;   // [npx] {present, box}
+    float* p;      // [kMaxObjects][npx]
+};
+
+// Scratch of the exact path: the flagged rows' f32 pixel-order sums and the decide
+// kernel's last-workgroup counter (left at 0).
+struct AssocExact {
+    float A[kMaxObjects][kMaxObjects];
+    unsigned counter;
+    unsigned frames;        // decisions that took the exact path (instrumentation)
+    unsigned rows;          // rows decided from exact sums, summed over frames
+    unsigned pad;
+};
+
+struct DecideArgs {
+    AssocTables* T;
+    AssocDecision* D;
+    AssocExact* X;
+    int* num_objs_dev;
+    float eps;              // prior_mrcnn_err_rate
+    float n_obs;
+    const uint8_t* mask;    // the frame's raw labels (the rows of the sums)
+    AssocPixels px;         // bits == nullptr: no pixel data (exact_missing)
+    int npx;
+    int force_exact;        // debug/tests: every present row takes the exact path
+    int certify_only;       // write the rows needing the exact path to D->exact_missing, decide nothing
 };
 
 struct MarchCamera {
@@ -189,6 +224,7 @@ struct AssocArgs {
     AssocTables* tables;
     float* probs_out;       // optional debug [H*W*32]
     uint8_t* box_out;       // optional debug [H*W*32]
+    AssocPixels px;         // per-pixel data for the decision's exact path (bits == nullptr: none)
     int debug;              // timing probes (SEMTSDF_DEBUG_ASSOC): 1 no accumulation, 2 no march
 };
 
@@ -244,6 +280,7 @@ hipError_t launch_shard_ray_step(const ShardRayArgs& a, hipStream_t s);
 hipError_t launch_shard_render_final(const ShardRayArgs& a, hipStream_t s);
 hipError_t launch_shard_render_finish(const ShardRayArgs& a, hipStream_t s);
 hipError_t launch_shard_assoc_partial(const ShardRayArgs& a, hipStream_t s);
+hipError_t launch_shard_assoc_pixels(const ShardRayArgs& a, int32_t* out, hipStream_t s);
 hipError_t launch_tables_from_partial(const long long* reduced, AssocTables* t, hipStream_t s);
 hipError_t launch_copy_f4(const void* src, void* dst, size_t n16, hipStream_t s);
 hipError_t launch_min_i64(long long* dst, const long long* src, size_t n, hipStream_t s);
@@ -272,8 +309,13 @@ hipError_t launch_cull(const IntegrateArgs& a, hipStream_t s);       // per-unit
 hipError_t launch_tables_init(AssocTables* t, hipStream_t s);  // zero sums, first_px = UINT_MAX
 hipError_t launch_mask_stats(const uint8_t* mask, int npx, AssocTables* t, hipStream_t s);
 hipError_t launch_assoc_march(const AssocArgs& a, hipStream_t s);
-hipError_t launch_assoc_decide(AssocTables* t, AssocDecision* d, int num_objs, float eps,
-                               int* num_objs_dev, hipStream_t s);
+hipError_t launch_assoc_decide(const DecideArgs& a, hipStream_t s);
+// reference filter_overlaps input (probs [npx][32] f32, box [npx][32] u8, tsdf.cu:304) -> the
+// tables and per-pixel data the march would leave (mask statistics included)
+hipError_t launch_assoc_from_probs(const float* probs, const uint8_t* box, const uint8_t* mask, int npx, float n_obs,
+                                   float eps, AssocTables* t, AssocPixels px, hipStream_t s);
+// the association's f32 log / exp (semtsdf_libm.h) over n values (fn 0: logf, 1: expf)
+hipError_t launch_libm_eval(int fn, const float* x, float* y, size_t n, hipStream_t s);
 hipError_t launch_first_frame_objs(const AssocTables* t, int* num_objs_dev, hipStream_t s);
 hipError_t launch_relabel(uint8_t* mask, int npx, const AssocDecision* d, hipStream_t s);
 hipError_t launch_relabel_records(uint8_t* mask, int w, int h, const DepthPyramid& p, const AssocDecision* d, hipStream_t s);

@@ -27,6 +27,7 @@
 #include <stddef.h>
 #include <stdlib.h>
 #include "semtsdf_internal.h"
+#include "semtsdf_libm.h"
 
 #ifndef SEMTSDF_LAZY_WEIGHT
 #define SEMTSDF_LAZY_WEIGHT 0  // lazy weights (k_integrate): measured slower, off by default
@@ -2339,14 +2340,14 @@ __device__ __forceinline__ void assoc_accumulate(AssocLds& s, const float* p, un
         atomicAdd(&s.c1[m], 1u);
 #pragma unroll
         for (int j = 1; j < kMaxObjects; ++j) {
-            const float L = logf(fmaxf(p[j] / n_obs, eps));
+            const float L = glibc::logf(fmaxf(p[j] / n_obs, eps));
             atomicAdd(reinterpret_cast<unsigned long long*>(&s.t1[m][j]), (unsigned long long)to_fix(L));
         }
     }
 #pragma unroll
     for (int n = 1; n < kMaxObjects; ++n) {
         if (p[n] > box_thresh) {
-            const float L = logf(fmaxf(1.0f - p[n] / n_obs, eps));
+            const float L = glibc::logf(fmaxf(1.0f - p[n] / n_obs, eps));
             const unsigned long long f = (unsigned long long)to_fix(L);
             atomicAdd(reinterpret_cast<unsigned long long*>(&s.t2[n]), f);
             atomicAdd(&s.c2[n], 1u);
@@ -2371,11 +2372,11 @@ __device__ __forceinline__ void assoc_accumulate_sparse(AssocLds& s, const float
     for (int j = 1; j < kMaxObjects; ++j) {
         if (!((bins >> j) & 1u) || p[j] == 0.0f) continue;
         if (lab) {
-            const long long d = to_fix(logf(fmaxf(p[j] / n_obs, eps))) - F0;
+            const long long d = to_fix(glibc::logf(fmaxf(p[j] / n_obs, eps))) - F0;
             if (d) atomicAdd(reinterpret_cast<unsigned long long*>(&s.t1[m][j]), (unsigned long long)d);
         }
         if (p[j] > box_thresh) {
-            const float L = logf(fmaxf(1.0f - p[j] / n_obs, eps));
+            const float L = glibc::logf(fmaxf(1.0f - p[j] / n_obs, eps));
             const unsigned long long f = (unsigned long long)to_fix(L);
             atomicAdd(reinterpret_cast<unsigned long long*>(&s.t2[j]), f);
             atomicAdd(&s.c2[j], 1u);
@@ -2385,6 +2386,22 @@ __device__ __forceinline__ void assoc_accumulate_sparse(AssocLds& s, const float
             }
         }
     }
+}
+
+// The pixel's data for the decision's exact path (AssocPixels): present and box bins, and the
+// counts of the present bins.  bins: the bins that may be nonzero (tri_hist).
+__device__ __forceinline__ void assoc_pixel_out(const AssocPixels& px, int npx, int k, const float* p, unsigned bins,
+                                                float box_thresh) {
+    unsigned pres = 0, box = 0;
+#pragma unroll
+    for (int j = 1; j < kMaxObjects; ++j) {
+        if (((bins >> j) & 1u) && p[j] != 0.0f) {
+            pres |= 1u << j;
+            px.p[(size_t)j * npx + k] = p[j];
+        }
+        if (p[j] > box_thresh) box |= 1u << j;
+    }
+    px.bits[k] = make_uint2(pres, box);
 }
 
 #ifndef SEMTSDF_MARCH_WPE
@@ -2403,7 +2420,7 @@ __device__ __forceinline__ void assoc_tile(const AssocArgs& a, AssocLds& s, int 
     assoc_lds_clear(s);
     __syncthreads();
     const bool sparse = a.box_thresh >= 0.0f && !a.probs_out;  // see assoc_accumulate_sparse
-    const long long F0 = to_fix(logf(fmaxf(0.0f, a.eps)));      // an empty bin's term
+    const long long F0 = to_fix(glibc::logf(fmaxf(0.0f, a.eps)));  // an empty bin's term
 
     const int x = bx * 16 + (tid & 15);
     const int y = by * 16 + (tid >> 4);
@@ -2419,6 +2436,7 @@ __device__ __forceinline__ void assoc_tile(const AssocArgs& a, AssocLds& s, int 
             bins = tri_hist(a.g, a.b, tr, p);
         }
         const int px = y * a.width + x;
+        if (a.px.bits) assoc_pixel_out(a.px, a.width * a.height, px, p, bins, a.box_thresh);
         if (a.probs_out) {
 #pragma unroll
             for (int k = 0; k < kMaxObjects; ++k) {
@@ -2466,88 +2484,403 @@ hipError_t launch_assoc_march(const AssocArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-// Decision (tsdf.cu:337-389), one workgroup of 256 lanes, every step parallel:
-// probabilities exp(A/C) per (i, j); per current label i its best previous id j (first
-// maximum, as the reference's strict '>'); per previous id j the winning label i (scanning
-// i in order with a strict '<', i.e. the reference's greedy overwrite); unmatched labels get
-// new ids in the order of their first pixel (tsdf.cu:378-387) by ranking first_px.
-// Leaves the tables cleared for the next frame (k_tables_init's state), so the host can skip
-// that launch.
-__global__ __launch_bounds__(256) void k_assoc_decide(AssocTables* T, AssocDecision* D, int* num_objs_dev, float eps) {
-    __shared__ double s_prob[kMaxObjects][kMaxObjects];
-    __shared__ int s_bestj[kMaxObjects];
-    __shared__ double s_bestp[kMaxObjects];
-    __shared__ int s_map_i[kMaxObjects];
-    __shared__ double s_map_p[kMaxObjects];
-    __shared__ int s_rev[256];
-    __shared__ unsigned s_first[256];
-    __shared__ int s_newcount;
+// ------------------------------------------------------------------------------------
+// Decision (tsdf.cu:337-389) with the reference's f32 arithmetic by construction.
+//
+// The reference sums its f32 log terms in pixel order (tsdf.cu:312-334), divides by the
+// count and takes expf (tsdf.cu:343); the decision compares those f32 values with strict
+// '>' (argmax, first maximum wins; acceptance against 3 * prior) and strict '<' (the greedy
+// keep-the-best per previous id).  The march's fixed-point sums S_fix are exact sums of the
+// same f32 terms up to 2^-29 per term, so every f32 value the reference forms lies in an
+// interval around them:
+//   |A_f32 - S| <= gamma |S|,  gamma = (n-1) u / (1 - (n-1) u),  u = 2^-24   (recursive
+//   summation of n same-sign terms: every partial sum is at most |A_f32|), |S - S_fix| <= n 2^-29,
+//   q = RN(A_f32 / n) within 2^-24 relative, expf within 0.502 ulp (< 2^-23 relative).
+// A row whose argmax, acceptance and greedy outcome are the same for every value in those
+// intervals is decided from the fixed-point sums; every other row ("flagged") is decided from
+// its exact f32 sums, recomputed from the per-pixel data in reference pixel order
+// (exact_row_sum: the sequential f32 additions evaluated as integer prefix sums per binade of
+// the running sum, bit-identical to the sequential loop) and the glibc expf restatement.
+//
+// One launch of 32 workgroups: each certifies the whole table (the same computation in
+// every workgroup), workgroup j >= 1 computes column j of the flagged rows, and the last
+// workgroup to finish (device-scope counter) decides, relabels the tables for the next frame
+// and resets the counter.  Unmatched labels get new ids in the order of their first pixel
+// (tsdf.cu:378-387) by ranking first_px.
+// ------------------------------------------------------------------------------------
+constexpr int kScanPer = 8;                    // pixels per lane of one scan chunk
+constexpr int kScanChunk = 256 * kScanPer;     // pixels per chunk (one workgroup)
+
+struct ScanLds {
+    long long wsum[4];
+    int wmin[4];
+    int first;
+    long long before;
+    float xv;
+};
+
+// workgroup exclusive scan of one int64 per lane (4 waves); returns the lane's exclusive
+// prefix and the total in *tot
+__device__ __forceinline__ long long wg_exscan(long long v, ScanLds& L, long long* tot) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    long long inc = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const long long o = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += o;
+    }
+    if (lane == 63) L.wsum[w] = inc;
+    __syncthreads();
+    long long base = 0, all = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (k < w) base += L.wsum[k];
+        all += L.wsum[k];
+    }
+    __syncthreads();
+    *tot = all;
+    return base + inc - v;
+}
+
+__device__ __forceinline__ int wg_min(int v, ScanLds& L) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, 64));
+    if (lane == 0) L.wmin[w] = v;
+    __syncthreads();
+    const int r = min(min(L.wmin[0], L.wmin[1]), min(L.wmin[2], L.wmin[3]));
+    __syncthreads();
+    return r;
+}
+
+// The reference's A[i][j] (tsdf.cu:312-334) for one current label i and previous id j: the f32
+// sum, in pixel order, of logf(max(p/n, eps)) over pixels labelled i and logf(max(1 - p/n, eps))
+// over the other pixels whose box bit j is set (every pixel adds at most one term).  The
+// sequential additions s <- RN(s + x) are evaluated in chunks of kScanChunk pixels: while s
+// stays in one binade [2^e, 2^(e+1)) (all terms <= 0, |s| grows), its grid is the multiples of
+// u = 2^(e-23) and RN(s + x) = s + round_u(x) exactly, so a chunk's steps are an integer prefix
+// sum of round_u(x) / u.  A step that would reach the next binade, a tie (x an odd multiple of
+// u/2, where the parity of s decides), a positive term or s == 0 is taken as the f32 addition
+// itself, and the chunk resumes after it with the new binade.
+__device__ float exact_row_sum(int i, int j, const DecideArgs& a, float c0, ScanLds& L) {
     const int tid = threadIdx.x;
-    const int max_now = (int)T->max_label + 1;
-    const double thr = (double)(3.0f * eps);
+    const float* pj = a.px.p + (size_t)j * a.npx;
+    float s = 0.0f;
+    for (int base = 0; base < a.npx; base += kScanChunk) {
+        float x[kScanPer];
+        bool any = false;
+#pragma unroll
+        for (int e = 0; e < kScanPer; ++e) {
+            const int k = base + tid * kScanPer + e;
+            float t = 0.0f;
+            if (k < a.npx) {
+                const unsigned m = a.mask[k];
+                const uint2 b = a.px.bits[k];
+                const bool pres = (b.x >> j) & 1u;
+                if (m == (unsigned)i) {
+                    const float p = pres ? pj[k] : 0.0f;
+                    t = p == 0.0f ? c0 : glibc::logf(fmaxf(p / a.n_obs, a.eps));
+                } else if ((b.y >> j) & 1u) {
+                    const float p = pres ? pj[k] : 0.0f;
+                    t = glibc::logf(fmaxf(1.0f - p / a.n_obs, a.eps));
+                }
+            }
+            x[e] = t;
+            any |= t != 0.0f;
+        }
+        if (!__syncthreads_or(any)) continue;
+        int pos = 0;  // chunk elements before pos are done
+        for (;;) {
+            const unsigned sb = glibc::f2u(s);
+            if (s == 0.0f || (sb >> 31) == 0u || ((sb >> 23) & 0xFFu) == 0u) {
+                // s == 0 (the first nonzero term is the sum), s > 0 or subnormal (not reached by
+                // same-sign terms of the association): one addition at a time
+                int f = kScanChunk;
+#pragma unroll
+                for (int e = 0; e < kScanPer; ++e) {
+                    const int idx = tid * kScanPer + e;
+                    if (idx >= pos && x[e] != 0.0f && idx < f) f = idx;
+                }
+                f = wg_min(f, L);
+                if (f == kScanChunk) break;
+                if (f >= tid * kScanPer && f < (tid + 1) * kScanPer) {
+#pragma unroll
+                    for (int e = 0; e < kScanPer; ++e)
+                        if (tid * kScanPer + e == f) L.xv = x[e];
+                }
+                __syncthreads();
+                s = s + L.xv;
+                __syncthreads();
+                pos = f + 1;
+                continue;
+            }
+            const int uexp = (int)((sb >> 23) & 0xFFu) - 150;             // u = 2^uexp
+            const long long S0 = (long long)((sb & 0x7FFFFFu) | 0x800000u);  // |s| / u
+            long long r[kScanPer];
+            bool viol[kScanPer];
+            long long lsum = 0;
+#pragma unroll
+            for (int e = 0; e < kScanPer; ++e) {
+                const int idx = tid * kScanPer + e;
+                r[e] = 0;
+                viol[e] = false;
+                if (idx >= pos && x[e] != 0.0f) {
+                    if (x[e] > 0.0f) {
+                        viol[e] = true;
+                    } else {
+                        const double v = ldexp(-(double)x[e], -uexp);  // |x| / u, exact
+                        if (v >= 0x1p25) {
+                            r[e] = 1ll << 25;
+                            viol[e] = true;
+                        } else {
+                            const double fl = floor(v), fr = v - fl;
+                            r[e] = (long long)fl + (fr > 0.5 ? 1 : 0);
+                            viol[e] = fr == 0.5;
+                        }
+                    }
+                }
+                lsum += r[e];
+            }
+            long long tot;
+            const long long ex = wg_exscan(lsum, L, &tot);
+            int f = kScanChunk;
+            long long run = ex;
+#pragma unroll
+            for (int e = 0; e < kScanPer; ++e) {
+                const int idx = tid * kScanPer + e;
+                run += r[e];
+                if ((viol[e] || S0 + run >= (1ll << 24)) && idx >= pos && idx < f) f = idx;
+            }
+            f = wg_min(f, L);
+            if (f == kScanChunk) {  // the rest of the chunk stays in this binade
+                s = -(float)ldexp((double)(S0 + tot), uexp);
+                break;
+            }
+            if (f >= tid * kScanPer && f < (tid + 1) * kScanPer) {
+                long long before = ex;
+#pragma unroll
+                for (int e = 0; e < kScanPer; ++e) {
+                    if (tid * kScanPer + e == f) L.xv = x[e];
+                    if (tid * kScanPer + e < f) before += r[e];
+                }
+                L.before = before;
+            }
+            __syncthreads();
+            s = -(float)ldexp((double)(S0 + L.before), uexp);  // exact: the steps before f
+            s = s + L.xv;                                        // step f as the f32 addition
+            __syncthreads();
+            pos = f + 1;
+            if (pos >= kScanChunk) break;
+        }
+    }
+    return s;
+}
+
+// Certified interval [lo, hi] of the reference's f32 exp(A/C) from the fixed-point sums, and
+// the point estimate mid (see above).  A fixed = the 2^-28 fixed-point sum, n = count.
+__device__ __forceinline__ void prob_interval(long long A, long long n, double* lo, double* hi, double* mid) {
+    if (n <= 0) { *lo = *hi = *mid = 0.0; return; }
+    const double dn = (double)n;
+    const double S = (double)A / kFixScale;
+    *mid = exp(S / dn);
+    const double g = (dn - 1.0) * 0x1p-24;
+    if (g >= 0.5) { *lo = 0.0; *hi = 2.0; return; }  // no certificate: the exact path decides
+    const double gam = g / (1.0 - g) * (1.0 + 0x1p-40);
+    const double slo = S - dn * 0x1p-29 * (1.0 + 0x1p-40);
+    const double shi = fmin(S + dn * 0x1p-29 * (1.0 + 0x1p-40), 0.0);
+    const double qlo = slo * (1.0 + gam) / dn * (1.0 + 0x1p-24 + 0x1p-40) - 0x1p-60;
+    const double qhi = shi * (1.0 - gam) / dn * (1.0 - 0x1p-24 - 0x1p-40) + 0x1p-60;
+    *lo = exp(qlo) * (1.0 - 0x1p-23 - 0x1p-40);
+    *hi = exp(qhi) * (1.0 + 0x1p-23 + 0x1p-40);
+}
+
+struct DecideLds {
+    double lo[kMaxObjects][kMaxObjects], hi[kMaxObjects][kMaxObjects], mid[kMaxObjects][kMaxObjects];
+    unsigned cand[kMaxObjects];   // flagged rows: the ids that can be their argmax
+    int win[kMaxObjects];         // certain rows: the argmax (-1: none / rejected)
+    unsigned flagged;
+    int last;
+    double prob[kMaxObjects][kMaxObjects];  // final: exact f32 (flagged rows) or the point estimate
+    int bestj[kMaxObjects];
+    double bestp[kMaxObjects];
+    int map_i[kMaxObjects];
+    double map_p[kMaxObjects];
+    int rev[256];
+    unsigned first[256];
+    int newcount;
+    ScanLds scan;
+};
+
+__global__ __launch_bounds__(256) void k_assoc_decide(DecideArgs a) {
+    __shared__ DecideLds L;
+    AssocTables* T = a.T;
+    const int tid = threadIdx.x;
+    const int max_now = min((int)T->max_label + 1, kMaxObjects);
+    const float thr_f = 3.0f * a.eps;  // tsdf.cu:349, a float product
+    const double thr = (double)thr_f;
+    // ---- certificate (every workgroup) ----
     for (int k = tid; k < kMaxObjects * kMaxObjects; k += 256) {
         const int i = k / kMaxObjects, j = k % kMaxObjects;
-        double prob = 0.0;
-        if (i >= 1 && j >= 1 && i < max_now && i < kMaxObjects) {
+        double lo = 0.0, hi = 0.0, mid = 0.0;
+        if (i >= 1 && j >= 1 && i < max_now) {
             const long long A = T->t1[i][j] + T->t2[j] - T->t3[i][j];
             const long long C = (long long)T->c1[i] + (long long)T->c2[j] - (long long)T->c3[i][j];
-            if (C != 0) prob = exp(((double)A / kFixScale) / (double)C);
+            prob_interval(A, C, &lo, &hi, &mid);
         }
-        s_prob[i][j] = prob;
+        L.lo[i][j] = lo;
+        L.hi[i][j] = hi;
+        L.mid[i][j] = mid;
     }
-    s_rev[tid] = -1;
-    s_first[tid] = T->first_px[tid];
-    if (tid == 0) s_newcount = 0;
+    if (tid == 0) L.flagged = 0u;
+    __syncthreads();
+    if (tid < kMaxObjects) {
+        const int i = tid;
+        unsigned cand = 0u;
+        int win = -1;
+        bool flag = false;
+        if (i >= 1 && i < max_now) {
+            // point-estimate argmax (first maximum) and the best lower bound
+            double mp = 0.0, maxlo = 0.0, maxhi = 0.0;
+            int w = -1;
+            for (int j = 1; j < kMaxObjects; ++j) {
+                if (L.mid[i][j] > mp) { mp = L.mid[i][j]; w = j; }
+                maxlo = fmax(maxlo, L.lo[i][j]);
+                maxhi = fmax(maxhi, L.hi[i][j]);
+            }
+            bool certain = true;
+            if (w < 0) {
+                certain = maxhi == 0.0;  // every count zero: no candidate (prob 0 everywhere)
+            } else {
+                for (int j = 1; j < kMaxObjects; ++j)
+                    if (j != w && !(L.hi[i][j] < L.lo[i][w])) certain = false;
+            }
+            if (!(maxhi > thr)) {
+                win = -1;  // every candidate is rejected whatever the argmax
+            } else if (certain && w >= 0 && L.lo[i][w] > thr) {
+                win = w;
+                cand = 1u << w;
+            } else {
+                flag = true;
+                for (int j = 1; j < kMaxObjects; ++j)
+                    if (L.hi[i][j] >= maxlo && L.hi[i][j] > thr) cand |= 1u << j;
+            }
+        }
+        L.cand[i] = cand;
+        L.win[i] = win;
+        if (flag) atomicOr(&L.flagged, 1u << i);
+    }
+    __syncthreads();
+    if (tid >= 1 && tid < kMaxObjects) {  // greedy per previous id j: potential winners
+        const int j = tid;
+        const unsigned F0 = L.flagged;
+        double bar = 0.0;
+        for (int i = 1; i < max_now; ++i)
+            if (!((F0 >> i) & 1u) && L.win[i] == j) bar = fmax(bar, L.lo[i][j]);
+        unsigned W = 0u;
+        for (int i = 1; i < max_now; ++i)
+            if (((L.cand[i] >> j) & 1u) && L.hi[i][j] >= bar) W |= 1u << i;
+        if (__popc(W) >= 2) atomicOr(&L.flagged, W);
+    }
+    __syncthreads();
+    unsigned F = L.flagged;
+    if (a.force_exact) F = ((1u << max_now) - 1u) & ~1u;
+    if (a.certify_only) {  // one workgroup: report, leave tables and counts as they are
+        if (tid == 0) {
+            a.D->exact_missing = F;
+            a.D->exact_rows = 0u;
+        }
+        return;
+    }
+    const bool have_px = a.px.bits != nullptr;
+    // ---- exact sums: column j = blockIdx.x of every flagged row ----
+    if (F && have_px && blockIdx.x >= 1) {
+        const int j = (int)blockIdx.x;
+        const float c0 = glibc::logf(fmaxf(0.0f, a.eps));
+        for (int i = 1; i < max_now; ++i) {
+            if (!((F >> i) & 1u)) continue;
+            const float A = exact_row_sum(i, j, a, c0, L.scan);
+            if (tid == 0) a.X->A[i][j] = A;
+        }
+    }
+    // ---- the last workgroup decides ----
+    __threadfence();
+    if (tid == 0) L.last = atomicAdd(&a.X->counter, 1u) == gridDim.x - 1u;
+    __syncthreads();
+    if (!L.last) return;
+    __threadfence();
+    AssocDecision* D = a.D;
+    const unsigned Fx = have_px ? F : 0u;
+    for (int k = tid; k < kMaxObjects * kMaxObjects; k += 256) {
+        const int i = k / kMaxObjects, j = k % kMaxObjects;
+        double prob = L.mid[i][j];
+        if (i >= 1 && j >= 1 && i < max_now && ((Fx >> i) & 1u)) {
+            const long long C = (long long)T->c1[i] + (long long)T->c2[j] - (long long)T->c3[i][j];
+            const float A = __hip_atomic_load(&a.X->A[i][j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            prob = C == 0 ? 0.0 : (double)glibc::expf(A / (float)C);  // tsdf.cu:343 in f32
+        }
+        L.prob[i][j] = prob;
+    }
+    L.rev[tid] = -1;
+    L.first[tid] = T->first_px[tid];
+    if (tid == 0) L.newcount = 0;
     __syncthreads();
     if (tid < kMaxObjects) {
         int max_j = -1;
         double max_p = 0.0;
         if (tid >= 1 && tid < max_now)
             for (int j = 1; j < kMaxObjects; ++j)
-                if (s_prob[tid][j] > max_p) { max_j = j; max_p = s_prob[tid][j]; }
-        s_bestj[tid] = max_j;
-        s_bestp[tid] = max_p;
+                if (L.prob[tid][j] > max_p) { max_j = j; max_p = L.prob[tid][j]; }
+        L.bestj[tid] = max_j;
+        L.bestp[tid] = max_p;
     }
     __syncthreads();
     if (tid < kMaxObjects) {
         int mi = -1;
         double mp = 0.0;
-        for (int i = 1; i < max_now && i < kMaxObjects; ++i)
-            if (s_bestj[i] == tid && s_bestp[i] > thr && (mi < 0 || mp < s_bestp[i])) { mi = i; mp = s_bestp[i]; }
-        s_map_i[tid] = mi;
-        s_map_p[tid] = mp;
+        for (int i = 1; i < max_now; ++i)
+            if (L.bestj[i] == tid && L.bestp[i] > thr && (mi < 0 || mp < L.bestp[i])) { mi = i; mp = L.bestp[i]; }
+        L.map_i[tid] = mi;
+        L.map_p[tid] = mp;
         D->assigned_prev[tid] = -1;
         D->assigned_prob[tid] = 0.0f;
     }
     __syncthreads();
-    if (tid < kMaxObjects && s_map_i[tid] >= 0) {
-        s_rev[s_map_i[tid]] = tid;
-        D->assigned_prev[s_map_i[tid]] = tid;
-        D->assigned_prob[s_map_i[tid]] = (float)s_map_p[tid];
+    if (tid < kMaxObjects && L.map_i[tid] >= 0) {
+        L.rev[L.map_i[tid]] = tid;
+        D->assigned_prev[L.map_i[tid]] = tid;
+        D->assigned_prob[L.map_i[tid]] = (float)L.map_p[tid];
     }
     __syncthreads();
-    const int num = *num_objs_dev;
+    const int num = *a.num_objs_dev;
     // lanes 1..255: a present, unmatched label gets num + (rank of its first pixel)
-    const bool fresh = tid >= 1 && s_rev[tid] < 0 && s_first[tid] != 0xFFFFFFFFu;
+    const bool fresh = tid >= 1 && L.rev[tid] < 0 && L.first[tid] != 0xFFFFFFFFu;
     int lut = tid;
-    if (tid >= 1 && s_rev[tid] >= 0) {
-        lut = s_rev[tid];
+    if (tid >= 1 && L.rev[tid] >= 0) {
+        lut = L.rev[tid];
     } else if (fresh) {
         int rank = 0;
         for (int u = 1; u < 256; ++u)
-            rank += (s_rev[u] < 0 && s_first[u] != 0xFFFFFFFFu && s_first[u] < s_first[tid]) ? 1 : 0;
+            rank += (L.rev[u] < 0 && L.first[u] != 0xFFFFFFFFu && L.first[u] < L.first[tid]) ? 1 : 0;
         lut = num + rank;
-        atomicAdd(&s_newcount, 1);
+        atomicAdd(&L.newcount, 1);
     }
     D->lut[tid] = (unsigned char)lut;
     __syncthreads();
     if (tid == 0) {
-        const int after = num + s_newcount;
-        D->max_obj_now = max_now;
+        const int after = num + L.newcount;
+        const int mx = (int)T->max_label + 1;
+        D->max_obj_now = mx;
         D->num_objs_before = num;
         D->num_objs_after = after;
-        D->bad_label = (after > kMaxObjects || max_now > kMaxObjects) ? 1 : 0;
-        *num_objs_dev = after;
+        D->bad_label = (after > kMaxObjects || mx > kMaxObjects) ? 1 : 0;
+        D->exact_rows = Fx;
+        D->exact_missing = have_px ? 0u : F;
+        *a.num_objs_dev = after;
+        if (Fx) {
+            a.X->frames += 1u;
+            a.X->rows += (unsigned)__popc(Fx);
+        }
+        a.X->counter = 0u;
     }
     // every read of T is above (the last barrier orders them): clear it for the next frame
     uint2* w = reinterpret_cast<uint2*>(T);
@@ -2556,10 +2889,92 @@ __global__ __launch_bounds__(256) void k_assoc_decide(AssocTables* T, AssocDecis
     T->first_px[tid] = 0xFFFFFFFFu;
 }
 
-hipError_t launch_assoc_decide(AssocTables* t, AssocDecision* d, int num_objs, float eps,
-                               int* num_objs_dev, hipStream_t s) {
-    (void)num_objs;
-    hipLaunchKernelGGL(k_assoc_decide, dim3(1), dim3(256), 0, s, t, d, num_objs_dev, eps);
+hipError_t launch_assoc_decide(const DecideArgs& a, hipStream_t s) {
+    // workgroup j >= 1 computes column j of the exact sums: one workgroup when there is no
+    // per-pixel data to compute them from
+    const unsigned grid = (a.certify_only || !a.px.bits) ? 1u : (unsigned)kMaxObjects;
+    hipLaunchKernelGGL(k_assoc_decide, dim3(grid), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// filter_overlaps from the reference's own inputs (tsdf.cu:304: probs [npx][32], box_mask
+// [npx][32]): the tables and per-pixel data the association march leaves, for a decision on
+// given probabilities (parity tests of the decision; the reference's function boundary).
+// The mask statistics are those of k_mask_stats (first pixel of every label, max label).
+__global__ __launch_bounds__(256) void k_assoc_from_probs(const float* __restrict__ probs,
+                                                          const uint8_t* __restrict__ box, const uint8_t* __restrict__ mask,
+                                                          int npx, float n_obs, float eps, AssocTables* t, AssocPixels px) {
+    __shared__ AssocLds s;
+    assoc_lds_clear(s);
+    __syncthreads();
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k < npx) {
+        float p[kMaxObjects];
+        unsigned bx = 0, pres = 0;
+#pragma unroll
+        for (int j = 0; j < kMaxObjects; ++j) {
+            p[j] = probs[(size_t)k * kMaxObjects + j];
+            if (box[(size_t)k * kMaxObjects + j]) bx |= 1u << j;
+            if (j >= 1 && p[j] != 0.0f) {
+                pres |= 1u << j;
+                px.p[(size_t)j * npx + k] = p[j];
+            }
+        }
+        px.bits[k] = make_uint2(pres, bx & ~1u);
+        const unsigned m = mask[k];
+        if (m > 0 && m < (unsigned)kMaxObjects) {
+            atomicAdd(&s.c1[m], 1u);
+#pragma unroll
+            for (int j = 1; j < kMaxObjects; ++j)
+                atomicAdd(reinterpret_cast<unsigned long long*>(&s.t1[m][j]),
+                          (unsigned long long)to_fix(glibc::logf(fmaxf(p[j] / n_obs, eps))));
+        }
+#pragma unroll
+        for (int n = 1; n < kMaxObjects; ++n) {
+            if (!((bx >> n) & 1u)) continue;
+            const unsigned long long f = (unsigned long long)to_fix(glibc::logf(fmaxf(1.0f - p[n] / n_obs, eps)));
+            atomicAdd(reinterpret_cast<unsigned long long*>(&s.t2[n]), f);
+            atomicAdd(&s.c2[n], 1u);
+            if (m > 0 && m < (unsigned)kMaxObjects) {
+                atomicAdd(reinterpret_cast<unsigned long long*>(&s.t3[m][n]), f);
+                atomicAdd(&s.c3[m][n], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < kMaxObjects * kMaxObjects; q += 256) {
+        const long long v1 = (&s.t1[0][0])[q];
+        if (v1) atomicAdd(reinterpret_cast<unsigned long long*>(&t->t1[0][0]) + q, (unsigned long long)v1);
+        const long long v3 = (&s.t3[0][0])[q];
+        if (v3) atomicAdd(reinterpret_cast<unsigned long long*>(&t->t3[0][0]) + q, (unsigned long long)v3);
+        const unsigned c3 = (&s.c3[0][0])[q];
+        if (c3) atomicAdd(&t->c3[0][0] + q, c3);
+    }
+    if (threadIdx.x < kMaxObjects) {
+        const int q = threadIdx.x;
+        if (s.t2[q]) atomicAdd(reinterpret_cast<unsigned long long*>(&t->t2[q]), (unsigned long long)s.t2[q]);
+        if (s.c1[q]) atomicAdd(&t->c1[q], s.c1[q]);
+        if (s.c2[q]) atomicAdd(&t->c2[q], s.c2[q]);
+    }
+}
+
+hipError_t launch_assoc_from_probs(const float* probs, const uint8_t* box, const uint8_t* mask, int npx, float n_obs,
+                                   float eps, AssocTables* t, AssocPixels px, hipStream_t s) {
+    if (npx <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_assoc_from_probs, dim3((npx + 255) / 256), dim3(256), 0, s, probs, box, mask, npx, n_obs, eps,
+                       t, px);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_libm_eval(int fn, const float* __restrict__ x, float* __restrict__ y, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+        y[i] = fn == 0 ? glibc::logf(x[i]) : glibc::expf(x[i]);
+}
+
+hipError_t launch_libm_eval(int fn, const float* x, float* y, size_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const size_t b = (n + 255) / 256;
+    hipLaunchKernelGGL(k_libm_eval, dim3((unsigned)(b < 65536 ? b : 65536)), dim3(256), 0, s, fn, x, y, n);
     return hipGetLastError();
 }
 
@@ -3202,6 +3617,48 @@ __global__ __launch_bounds__(256) void k_shard_assoc_partial(ShardRayArgs a) {
         if (s.c1[i]) atomicAdd(P + 2 * NN + kMaxObjects + i, (unsigned long long)s.c1[i]);
         if (s.c2[i]) atomicAdd(P + 2 * NN + 2 * kMaxObjects + i, (unsigned long long)s.c2[i]);
     }
+}
+
+// The shard's part of the association's per-pixel data (AssocPixels layout in one buffer:
+// uint2 bits [npx], then f32 p [32][npx]) for the decision's exact path: the owner of a pixel's
+// hit writes its bits and its 32 counts, every other shard zeros (pixels without a hit: shard
+// 0), so an int32 SUM over the shards is the single volume's data.
+__global__ __launch_bounds__(256) void k_shard_assoc_pixels(ShardRayArgs a, int32_t* __restrict__ out) {
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15);
+    const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= a.width || y >= a.height) return;
+    const int npx = a.width * a.height;
+    const int px = y * a.width + x;
+    const RayGeo r = shard_ray(a, x, y);
+    float t;
+    float p[kMaxObjects];
+#pragma unroll
+    for (int k = 0; k < kMaxObjects; ++k) p[k] = 0.0f;
+    bool mine;
+    unsigned bins = 0;
+    if (shard_resolve(a, r, px, npx, &t)) {
+        const float hx = fmaf(t, r.dx, r.ox), hy = fmaf(t, r.dy, r.oy), hz = fmaf(t, r.dz, r.oz);
+        mine = sample_owner(a.g, hz) == a.g.shard;
+        if (mine) bins = tri_hist(a.g, a.b, tri_setup(a.g, hx, hy, hz), p);
+    } else {
+        mine = a.g.shard == 0;
+    }
+    unsigned pres = 0, box = 0;
+#pragma unroll
+    for (int j = 1; j < kMaxObjects; ++j) {
+        if (((bins >> j) & 1u) && p[j] != 0.0f) pres |= 1u << j;
+        if (p[j] > a.box_thresh) box |= 1u << j;
+    }
+    uint2* bits = reinterpret_cast<uint2*>(out);
+    float* pp = reinterpret_cast<float*>(out + 2 * (size_t)npx);
+    bits[px] = mine ? make_uint2(pres, box) : make_uint2(0u, 0u);
+#pragma unroll
+    for (int j = 0; j < kMaxObjects; ++j) pp[(size_t)j * npx + px] = mine ? p[j] : 0.0f;
+}
+
+hipError_t launch_shard_assoc_pixels(const ShardRayArgs& a, int32_t* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_shard_assoc_pixels, dim3((a.width + 15) / 16, (a.height + 15) / 16), dim3(256), 0, s, a, out);
+    return hipGetLastError();
 }
 
 __global__ void k_tables_from_partial(const long long* __restrict__ P, AssocTables* T) {

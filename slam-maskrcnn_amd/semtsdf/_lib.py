@@ -38,6 +38,8 @@ RENDER_LABEL = 0
 RENDER_COLOR = 1
 RAY_ASSOC = 2
 ASSOC_PARTIAL_LEN = 3168
+ASSOC_PIXEL_WORDS = 34
+NEED_PIXELS = 1
 EXCHANGE_ALLGATHER = 0
 EXCHANGE_MIN = 1
 
@@ -91,6 +93,7 @@ class AssocStats(C.Structure):
         ("assigned_prev", C.c_int32 * MAX_OBJECTS),
         ("assigned_prob", C.c_float * MAX_OBJECTS),
         ("lut", C.c_uint8 * 256),
+        ("exact_rows", C.c_uint32),
     ]
 
 
@@ -110,6 +113,8 @@ class Timing(C.Structure):
         ("free_units", C.c_uint64),
         ("full_units", C.c_uint64),
         ("lazy_voxels", C.c_uint64),
+        ("assoc_exact_frames", C.c_uint64),
+        ("assoc_exact_rows", C.c_uint64),
     ]
 
 
@@ -148,6 +153,8 @@ SIGNATURES = {
     "semtsdf_associate": (_I, [_P, _P, _P, C.POINTER(AssocStats), _P]),
     "semtsdf_associate_dev": (_I, [_P, _P, _P, C.POINTER(AssocStats), _P]),
     "semtsdf_assoc_probs": (_I, [_P, _P, _P, _P, _P]),
+    "semtsdf_filter_overlaps_dev": (_I, [_P, _P, _P, _P, C.POINTER(AssocStats), _P]),
+    "semtsdf_libm_eval": (_I, [_I, _P, _P, C.c_size_t, _P]),
     "semtsdf_parse_frame": (_I, [_P, _P, _P, _P, _P, C.POINTER(AssocStats), _P]),
     "semtsdf_parse_frame_dev": (_I, [_P, _P, _P, _P, _P, _P]),
     "semtsdf_parse_frame_dev_after": (_I, [_P, _P, _P, _P, _P, _P, _P]),
@@ -160,6 +167,8 @@ SIGNATURES = {
     "semtsdf_shard_render_finish": (_I, [_P, _P, _P, _P, _P]),
     "semtsdf_shard_assoc_partial": (_I, [_P, _P, _P, _P, _P]),
     "semtsdf_shard_assoc_apply": (_I, [_P, _P, _P, C.POINTER(AssocStats), _P]),
+    "semtsdf_shard_assoc_pixels": (_I, [_P, _P, _P, _P]),
+    "semtsdf_shard_assoc_apply_exact": (_I, [_P, _P, _P, _P, C.POINTER(AssocStats), _P]),
     "semtsdf_shard_note_integrated": (_I, [_P, _P, _P]),
     "semtsdf_min_i64": (_I, [_P, _P, C.c_size_t, _P]),
     "semtsdf_masks_to_labels": (_I, [_P, _I, _I, _I, _I, _P, C.POINTER(C.c_int), _P]),

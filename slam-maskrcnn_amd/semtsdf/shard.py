@@ -236,13 +236,40 @@ class LocalShardGroup:
             L.check(lib.semtsdf_shard_assoc_partial(v.handle, C.c_void_p(g), C.c_void_p(m), C.c_void_p(pb.ptr),
                                                     self._s()))
         _sum_int64_dev([pb.ptr for pb in self.partial], self.reduced.ptr, L.ASSOC_PARTIAL_LEN, self.stream)
-        stats = []
-        for v, m in zip(self.vols, mask_ptrs):
-            st = L.AssocStats() if want_stats else None
-            L.check(lib.semtsdf_shard_assoc_apply(v.handle, C.c_void_p(self.reduced.ptr), C.c_void_p(m),
-                                                  C.byref(st) if st is not None else None, self._s()))
-            stats.append(st)
+        stats = [L.AssocStats() if want_stats else None for _ in self.vols]
+        byref = lambda st: C.byref(st) if st is not None else None
+        # every shard certifies the same reduced sums: all decide, or all need the pixels
+        rc = lib.semtsdf_shard_assoc_apply(self.vols[0].handle, C.c_void_p(self.reduced.ptr), C.c_void_p(mask_ptrs[0]),
+                                           byref(stats[0]), self._s())
+        if rc == L.NEED_PIXELS:
+            self._apply_exact(g, mask_ptrs, stats)
+            return stats
+        L.check(rc)
+        for v, m, st in zip(self.vols[1:], mask_ptrs[1:], stats[1:]):
+            L.check(lib.semtsdf_shard_assoc_apply(v.handle, C.c_void_p(self.reduced.ptr), C.c_void_p(m), byref(st),
+                                                  self._s()))
         return stats
+
+    def _apply_exact(self, g, mask_ptrs, stats):
+        """The decision's exact path: every shard's per-pixel data, summed (int32), then
+        decide + relabel on each shard."""
+        import ctypes as C
+
+        from . import _lib as L
+        from .volume import DeviceBuffer
+
+        lib = L.load()
+        nw = self.W * self.H * L.ASSOC_PIXEL_WORDS
+        parts = [DeviceBuffer(4 * nw) for _ in self.vols]
+        for v, pb in zip(self.vols, parts):
+            L.check(lib.semtsdf_shard_assoc_pixels(v.handle, C.c_void_p(g), C.c_void_p(pb.ptr), self._s()))
+        px = DeviceBuffer(4 * nw)
+        _sum_int32_dev([pb.ptr for pb in parts], px.ptr, nw, self.stream)
+        for v, m, st in zip(self.vols, mask_ptrs, stats):
+            L.check(lib.semtsdf_shard_assoc_apply_exact(v.handle, C.c_void_p(self.reduced.ptr), C.c_void_p(px.ptr),
+                                                        C.c_void_p(m), C.byref(st) if st is not None else None,
+                                                        self._s()))
+        self.vols[0].sync()  # the staging buffers are freed on return
 
     def parse_frame_dev(self, depth_ptr, rgb_ptr, mask_ptrs, E):
         import ctypes as C
@@ -254,6 +281,25 @@ class LocalShardGroup:
         for v, m in zip(self.vols, mask_ptrs):
             v.integrate_dev(depth_ptr, rgb_ptr, m, E, self.stream)
             L.check(L.load().semtsdf_shard_note_integrated(v.handle, C.c_void_p(m), self._s()))
+
+
+def _sum_int32_dev(ptrs, out_ptr, n, stream):
+    """out = sum of the int32 vectors at ptrs (device), via host staging (tests only)."""
+    import ctypes as C
+
+    import numpy as np
+
+    from . import _lib as L
+
+    lib = L.load()
+    acc = np.zeros(n, np.int32)
+    tmp = np.zeros(n, np.int32)
+    for p in ptrs:
+        L.check(lib.semtsdf_memcpy(L.ptr(tmp), C.c_void_p(p), 4 * n, 2, C.c_void_p(stream)))
+        L.check(lib.semtsdf_stream_sync(C.c_void_p(stream)))
+        acc += tmp
+    L.check(lib.semtsdf_memcpy(C.c_void_p(out_ptr), L.ptr(acc), 4 * n, 1, C.c_void_p(stream)))
+    L.check(lib.semtsdf_stream_sync(C.c_void_p(stream)))
 
 
 def _sum_int64_dev(ptrs, out_ptr, n, stream):
@@ -385,9 +431,24 @@ class DistShardGroup:
                                                     C.c_void_p(self.partial.data_ptr()), self._stream()))
             self.dist.all_reduce(self.partial, op=self.dist.ReduceOp.SUM, group=self.group)
             st = L.AssocStats() if want_stats else None
-            L.check(lib.semtsdf_shard_assoc_apply(self.vol.handle, C.c_void_p(self.partial.data_ptr()),
-                                                  C.c_void_p(mask_ptr), C.byref(st) if st is not None else None,
-                                                  self._stream()))
+            rc = lib.semtsdf_shard_assoc_apply(self.vol.handle, C.c_void_p(self.partial.data_ptr()),
+                                               C.c_void_p(mask_ptr), C.byref(st) if st is not None else None,
+                                               self._stream())
+            if rc == L.NEED_PIXELS:
+                # labels too close to call from the reduced sums (every rank certifies the same
+                # sums, so all take this branch): the per-pixel data of every shard, one
+                # all-reduce(SUM) over int32 words, then the exact decision
+                import torch
+
+                px = torch.empty(self.W * self.H * L.ASSOC_PIXEL_WORDS, dtype=torch.int32, device=self.device)
+                L.check(lib.semtsdf_shard_assoc_pixels(self.vol.handle, C.c_void_p(g), C.c_void_p(px.data_ptr()),
+                                                       self._stream()))
+                self.dist.all_reduce(px, op=self.dist.ReduceOp.SUM, group=self.group)
+                L.check(lib.semtsdf_shard_assoc_apply_exact(self.vol.handle, C.c_void_p(self.partial.data_ptr()),
+                                                            C.c_void_p(px.data_ptr()), C.c_void_p(mask_ptr),
+                                                            C.byref(st) if st is not None else None, self._stream()))
+            else:
+                L.check(rc)
         return st
 
     def parse_frame_dev(self, depth_ptr: int, rgb_ptr: int, mask_ptr: int, E):

@@ -280,8 +280,19 @@ class Volume:
         L.check(L.load().semtsdf_upload(self._h, *[L.ptr(a) for a in arrs]))
 
     # ---- instrumentation
-    def set_instrumentation(self, events: bool = True, count: bool = False):
-        L.check(L.load().semtsdf_set_instrumentation(self._h, (1 if events else 0) | (2 if count else 0)))
+    def set_instrumentation(self, events: bool = True, count: bool = False, force_exact: bool = False):
+        """events: HIP-event kernel timing; count: touched/gated voxel counters; force_exact: every
+        association row decided from its exact f32 pixel-order sums (tests, cost measurement)."""
+        flags = (1 if events else 0) | (2 if count else 0) | (4 if force_exact else 0)
+        L.check(L.load().semtsdf_set_instrumentation(self._h, flags))
+
+    def filter_overlaps_dev(self, probs_ptr: int, box_ptr: int, mask_ptr: int, stream=None) -> L.AssocStats:
+        """TSDF::filter_overlaps (tsdf.cu:304-416) on device arrays: probs f32 [H*W][32], box u8
+        [H*W][32], mask u8 [H*W] relabelled in place; uses this handle's n_obs and num_objs."""
+        st = L.AssocStats()
+        L.check(L.load().semtsdf_filter_overlaps_dev(self._h, C.c_void_p(probs_ptr), C.c_void_p(box_ptr),
+                                                     C.c_void_p(mask_ptr), C.byref(st), stream))
+        return st
 
     def timing(self) -> L.Timing:
         t = L.Timing()

@@ -27,7 +27,9 @@ def test_library_exports_every_symbol():
     lib = L.load()
     for n in declared():
         assert hasattr(lib, n), n
-    assert lib.semtsdf_abi_version() == 8
+    assert lib.semtsdf_abi_version() == 9
+    key = lib.semtsdf_build_key().decode()
+    assert len(key) == 64 and int(key, 16) >= 0  # the sha-256 build key (__graft_entry__.build_key)
 
 
 def test_structs_match_header_sizes():
@@ -37,9 +39,9 @@ def test_structs_match_header_sizes():
 
     # semtsdf_params: 3 i32 + 13 f32 + 32 f32 + 2 i32 + 5 f32 + u32 + 3 i32
     assert C.sizeof(L.Params) == 4 * (3 + 9 + 1 + 32 + 2 + 5 + 1 + 3)
-    assert C.sizeof(L.AssocStats) == 4 * (2 + 32 + 32) + 256
-    # semtsdf_timing: 5 doubles-or-u64 groups of 8 bytes each, 14 fields
-    assert C.sizeof(L.Timing) == 8 * 14
+    assert C.sizeof(L.AssocStats) == 4 * (2 + 32 + 32) + 256 + 4
+    # semtsdf_timing: 16 fields of 8 bytes (doubles or u64)
+    assert C.sizeof(L.Timing) == 8 * 16
 
 
 def test_argument_errors_without_a_device():
@@ -63,3 +65,12 @@ def test_argument_errors_without_a_device():
     assert rc != 0 and b"16-B" in lib.semtsdf_last_error()
     rc = lib.semtsdf_memcpy(C.c_void_p(0x1000), C.c_void_p(0x2000), 64, 7, None)
     assert rc != 0 and b"kind" in lib.semtsdf_last_error()
+    # ABI 9: the decision on given inputs, the libm check, the sharded exact path
+    rc = lib.semtsdf_filter_overlaps_dev(None, buf, buf, buf, None, None)
+    assert rc != 0 and b"NULL" in lib.semtsdf_last_error()
+    rc = lib.semtsdf_libm_eval(2, buf, buf, 16, None)
+    assert rc != 0 and b"fn" in lib.semtsdf_last_error()
+    rc = lib.semtsdf_shard_assoc_pixels(None, buf, buf, None)
+    assert rc != 0 and b"NULL" in lib.semtsdf_last_error()
+    rc = lib.semtsdf_shard_assoc_apply_exact(None, buf, buf, buf, None, None)
+    assert rc != 0 and b"NULL" in lib.semtsdf_last_error()

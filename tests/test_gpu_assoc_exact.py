@@ -1,0 +1,380 @@
+"""The association decision equals the reference's f32 rule by construction.
+
+filter_overlaps (src/SfM_CUDA/tsdf.cu:304-389) sums f32 logf terms in pixel order, divides
+by the count, takes expf and decides with strict comparisons in f32.  The device decides from
+2^-28 fixed-point sums when a certificate shows that every f32 value the reference can form
+gives the same decision, and recomputes the other rows' f32 sums exactly in pixel order.
+These tests build the near-ties where that matters: the oracle's f32 pixel-order rule
+(precision 0, the reference's arithmetic) and its double accumulation (precision 1) disagree,
+and the GPU must equal precision 0.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+KI = (520.9, 521.0, 325.1, 249.7)
+
+
+@pytest.fixture(scope="module")
+def S():
+    import semtsdf
+    from semtsdf import _lib as L
+
+    semtsdf.load()
+    return semtsdf, L
+
+
+def _decision_volume(S, W, H):
+    """A semantic handle used only for its decision (filter_overlaps_dev)."""
+    semtsdf, L = S
+    p = semtsdf.default_params(16, KI, W, H)
+    for a in range(3):
+        p.voxel[a] = 0.01
+        p.vol_start[a] = -0.08
+        p.vol_end[a] = 0.07
+    p.mu = 0.05
+    return semtsdf.Volume(p, 0)
+
+
+def test_device_libm_equals_host_exhaustively(S, oracle):
+    """The device's logf over [0.05, 1] and expf over [logf(0.05), 0] -- every input the
+    association's terms and means can take -- equal the host C library's bit for bit (the
+    reference calls logf/expf on the host, tsdf.cu:318,329,343)."""
+    import ctypes as C
+
+    import torch
+
+    semtsdf, L = S
+    lib = L.load()
+    f2u = lambda f: int(np.array([f], np.float32).view(np.uint32)[0])
+    c0 = np.float32(np.log(np.float32(0.05)))
+    ranges = [(0, f2u(0.05), f2u(1.0)), (1, 0x80000000, f2u(np.float32(-3.0)))]
+    chunk = 1 << 26
+    total = {0: 0, 1: 0}
+    for fn, lo, hi in ranges:
+        for u0 in range(lo, hi + 1, chunk):
+            n = min(chunk, hi + 1 - u0)
+            x = torch.arange(u0, u0 + n, dtype=torch.int64, device="cuda").to(torch.int32).view(torch.float32)
+            y = torch.empty_like(x)
+            L.check(lib.semtsdf_libm_eval(fn, C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), n, None))
+            torch.cuda.synchronize()
+            yh = np.ascontiguousarray(y.cpu().numpy())
+            bad = oracle.lib().oracle_libm_mismatches(fn, None, oracle._p(yh), n, u0)
+            assert bad == 0, f"fn {fn}: {bad} mismatches in [{u0:#x}, {u0 + n:#x})"
+            total[fn] += n
+    assert total[0] > 36_000_000 and total[1] > 1_000_000_000
+    assert f2u(c0) <= f2u(np.float32(-3.0))  # the expf range covers [logf(0.05), 0]
+
+
+# ---------------------------------------------------------------------------------------------
+# near-tie cases: (probs [npx, 32] f32, box [npx, 32] u8, mask [H, W] u8, n_obs, num_objs)
+# ---------------------------------------------------------------------------------------------
+def _blank(W, H):
+    return np.zeros((H * W, 32), np.float32), np.zeros((H, W), np.uint8)
+
+
+def _finish(probs, box_thresh=0.3):
+    return probs, (probs > box_thresh).astype(np.uint8)
+
+
+def case_split(rng, W, H):
+    """Current label 1 split evenly over previous ids j1 < j2 in pixel order: equal multisets
+    of terms, so the exact sums tie and only the f32 order separates them."""
+    probs, mask = _blank(W, H)
+    n_obs = int(rng.integers(2, 40))
+    x0, y0 = int(rng.integers(0, W // 3)), int(rng.integers(0, H // 3))
+    w, h = int(rng.integers(W // 4, W // 2)), int(rng.integers(H // 4, H // 2))
+    mask[y0:y0 + h, x0:x0 + w] = 1
+    idx = np.flatnonzero(mask.reshape(-1) == 1)
+    if idx.size % 2:
+        idx = idx[:-1]  # the odd pixel keeps zeros in both ids
+    j1, j2 = sorted(rng.choice(np.arange(1, 32), 2, replace=False))
+    a = np.float32(n_obs * rng.uniform(0.35, 1.0))
+    half = idx.size // 2
+    probs[idx[:half], j1] = a
+    probs[idx[half:], j2] = a
+    # other labels with their own previous ids
+    for lab in range(2, int(rng.integers(2, 5))):
+        yy, xx = int(rng.integers(0, H - 8)), int(rng.integers(0, W - 8))
+        m = np.zeros((H, W), bool)
+        m[yy:yy + 8, xx:xx + 8] = True
+        m &= mask == 0
+        mask[m] = lab
+        jj = int(rng.integers(1, 32))
+        probs[np.flatnonzero(m.reshape(-1)), jj] = np.float32(n_obs * rng.uniform(0.5, 1.0))
+    return (*_finish(probs), mask, n_obs, int(rng.integers(4, 12)))
+
+
+def case_greedy(rng, W, H):
+    """Current labels 1 and 2 of equal size both matching previous id j with equal terms:
+    the exact probabilities tie in the greedy keep-the-best (tsdf.cu:358)."""
+    probs, mask = _blank(W, H)
+    n_obs = int(rng.integers(2, 40))
+    w, h = int(rng.integers(8, W // 3)), int(rng.integers(8, H // 3))
+    ya, yb = int(rng.integers(0, H // 2 - h // 2)), int(rng.integers(H // 2, H - h))
+    xa, xb = int(rng.integers(0, W - w)), int(rng.integers(0, W - w))
+    first, second = (1, 2) if rng.random() < 0.5 else (2, 1)
+    mask[ya:ya + h, xa:xa + w] = first
+    mask[yb:yb + h, xb:xb + w] = second
+    j = int(rng.integers(1, 32))
+    a = np.float32(n_obs * rng.uniform(0.4, 1.0))
+    probs[np.flatnonzero(mask.reshape(-1) > 0), j] = a
+    return (*_finish(probs), mask, n_obs, int(rng.integers(4, 12)))
+
+
+def case_threshold(rng, W, H):
+    """One label whose best probability is near 3 * prior (tsdf.cu:349): a fraction phi of
+    its pixels carry p = a for id j, chosen so exp(mean log) ~ 0.15."""
+    probs, mask = _blank(W, H)
+    n_obs = int(rng.integers(2, 40))
+    w, h = int(rng.integers(W // 4, W // 2)), int(rng.integers(H // 4, H // 2))
+    mask[:h, :w] = 1
+    idx = np.flatnonzero(mask.reshape(-1) == 1)
+    j = int(rng.integers(1, 32))
+    a = np.float32(n_obs * rng.uniform(0.6, 1.0))
+    t = float(np.log(np.float32(a / np.float32(n_obs))))
+    c0 = float(np.log(np.float32(0.05)))
+    target = float(np.log(np.float32(0.15)))
+    phi = (c0 - target) / (c0 - t)
+    k = int(round(phi * idx.size))
+    order = rng.permutation(idx.size)
+    probs[idx[np.sort(order[:k])], j] = a
+    return (*_finish(probs), mask, n_obs, int(rng.integers(4, 12)))
+
+
+def case_random(rng, W, H):
+    """Several labels with continuous, overlapping probabilities (mostly decided by the
+    certificate)."""
+    probs, mask = _blank(W, H)
+    n_obs = int(rng.integers(1, 30))
+    for lab in range(1, int(rng.integers(2, 7))):
+        yy, xx = int(rng.integers(0, H - 10)), int(rng.integers(0, W - 10))
+        hh, ww = int(rng.integers(6, H // 2)), int(rng.integers(6, W // 2))
+        mask[yy:yy + hh, xx:xx + ww] = lab
+    for j in rng.choice(np.arange(1, 32), int(rng.integers(1, 6)), replace=False):
+        yy, xx = int(rng.integers(0, H - 10)), int(rng.integers(0, W - 10))
+        hh, ww = int(rng.integers(6, H // 2)), int(rng.integers(6, W // 2))
+        reg = np.zeros((H, W), bool)
+        reg[yy:yy + hh, xx:xx + ww] = True
+        sel = np.flatnonzero(reg.reshape(-1))
+        probs[sel, j] = (rng.uniform(0.0, 1.0, sel.size) * n_obs).astype(np.float32)
+    return (*_finish(probs), mask, n_obs, int(rng.integers(4, 12)))
+
+
+def _run(S, oracle, vol, case, W, H):
+    from semtsdf.volume import DeviceBuffer
+
+    probs, box, mask, n_obs, num_objs = case
+    npx = W * H
+    pb, bb, mb = DeviceBuffer(npx * 128), DeviceBuffer(npx * 32), DeviceBuffer(npx)
+    pb.upload(probs)
+    bb.upload(box)
+    mb.upload(mask)
+    vol.set_state(n_obs, num_objs)
+    st = vol.filter_overlaps_dev(pb.ptr, bb.ptr, mb.ptr)
+    got = np.zeros(npx, np.uint8)
+    mb.download(got)
+    vol.sync()
+    r0 = oracle.filter_overlaps(probs.reshape(-1), box.reshape(-1), mask, n_obs, num_objs, 0.05, precision=0)
+    r1 = oracle.filter_overlaps(probs.reshape(-1), box.reshape(-1), mask, n_obs, num_objs, 0.05, precision=1)
+    for b in (pb, bb, mb):
+        b.free()
+    return st, got, r0, r1
+
+
+@pytest.mark.parametrize("W,H,ncases", [(160, 120, 120), (640, 480, 8)])
+def test_decisions_equal_f32_pixel_order_rule_on_near_ties(S, oracle, W, H, ncases):
+    """Split, greedy and threshold near-ties plus random tables: the GPU's relabelled mask,
+    matches and object count equal the reference's f32 pixel-order rule (oracle precision 0)
+    in every case, including the cases where the double accumulation (precision 1) decides
+    differently; near-ties take the exact path (exact_rows)."""
+    rng = np.random.default_rng(1234 + W)
+    vol = _decision_volume(S, W, H)
+    kinds = [case_split, case_greedy, case_threshold, case_random]
+    disagree, exact_cases, tie_exact = 0, 0, 0
+    for c in range(ncases):
+        kind = kinds[c % len(kinds)]
+        case = kind(rng, W, H)
+        st, got, r0, r1 = _run(S, oracle, vol, case, W, H)
+        m0, n0, mx0, prev0, _ = r0
+        m1, n1, _, prev1, _ = r1
+        assert np.array_equal(got, m0.reshape(-1)), (c, kind.__name__)
+        assert st.num_objs == n0 and list(st.assigned_prev) == list(prev0), (c, kind.__name__)
+        assert st.max_obj_now == mx0
+        if not (np.array_equal(m0, m1) and list(prev0) == list(prev1)):
+            disagree += 1
+            assert st.exact_rows != 0, (c, kind.__name__)  # only the exact path can get these right
+        exact_cases += st.exact_rows != 0
+        if kind in (case_split, case_greedy):
+            tie_exact += st.exact_rows != 0
+    print(f"{W}x{H}: {ncases} cases, {disagree} where f32 and double accumulation disagree, "
+          f"{exact_cases} took the exact path ({tie_exact} ties)")
+    assert tie_exact == sum(1 for c in range(ncases) if c % 4 in (0, 1))  # every tie is certified uncertain
+    if ncases >= 100:
+        assert disagree >= 5  # the suite does exercise the regime where the rules differ
+    vol.close()
+
+
+def test_forced_exact_path_on_a_stream_equals_reference_rule(S, oracle):
+    """Every row decided from its exact f32 pixel-order sums (instrumentation bit 2) on 8
+    frames of the synthetic stream at 96^3: the same masks and matches as the oracle's f32
+    rule on the same volume state (the exact scan is exercised on real march data: present
+    and box bins, pixels without a hit, several labels)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from semtsdf.synth import SyntheticStream
+
+    semtsdf, L = S
+    st = SyntheticStream(seed=5, noise=True)
+    frames = [st.frame(k) for k in range(9)]
+    p = semtsdf.default_params(96, KI, 640, 480)
+    semtsdf.place_from_frame(p, frames[0].depth, float(np.mean(frames[0].depth[frames[0].depth > 0])) / 5000.0,
+                             L.PLACE_SFM)
+    vol = semtsdf.Volume(p, 0)
+    vol.set_instrumentation(events=False, force_exact=True)
+    g = oracle.OGeom.from_params(p)
+    ost = oracle.OState([96, 96, 96], p.mu, semantic=True)
+    bands = [(y, min(y + 60, 480)) for y in range(0, 480, 60)]
+    num, rows = 0, 0
+    for k in range(1, 9):
+        fr = frames[k]
+        E = (fr.w2c @ frames[0].c2w).astype(np.float32)
+        m_gpu = np.ascontiguousarray(fr.mask.copy())
+        stats = vol.parse_frame(fr.depth, fr.rgb, m_gpu, E)
+        m_ref = fr.mask.copy()
+        if k == 1:
+            num = int(m_ref.max()) + 1
+        else:
+            probs = np.zeros(640 * 480 * 32, np.float32)
+            box = np.zeros(640 * 480 * 32, np.uint8)
+            Ki = np.ascontiguousarray(np.array(list(p.Kinv), np.float32))
+            E16 = np.ascontiguousarray(E.reshape(16))
+
+            def band(r):
+                oracle.lib().oracle_march_probs(oracle._p(g.dims), oracle._p(g.geo), oracle._p(oracle.k9(Ki)),
+                                                oracle._p(E16), 640, 480, oracle._p(ost.sdf), oracle._p(ost.hist),
+                                                float(p.box_thresh), oracle._p(probs), oracle._p(box), r[0], r[1])
+
+            with ThreadPoolExecutor(8) as ex:
+                list(ex.map(band, bands))
+            m_ref, num, mx, prev, _ = oracle.filter_overlaps(probs, box, m_ref, k - 1, num, 0.05, precision=0)
+            assert list(stats.assigned_prev) == list(prev), k
+            assert stats.num_objs == num, k
+            assert stats.exact_rows == ((1 << mx) - 1) & ~1, k  # every present row took the exact path
+            rows += bin(stats.exact_rows).count("1")
+        assert np.array_equal(m_gpu, m_ref), f"frame {k}"
+        oracle.integrate(g, ost, list(p.K), E, fr.depth, fr.rgb, m_ref, flags=0x3)
+    t = vol.timing()
+    assert t.assoc_exact_frames == 7 and t.assoc_exact_rows == rows
+    vol.close()
+
+
+def test_association_on_real_tum_frames_equals_reference_rule(S, oracle):
+    """The two real fr2_desk frames (tests/golden/frames_tum_fr2.npz) with synthetic instance
+    masks (depth bands cut into tiles): frame a integrated, frame b associated against it.
+    The GPU's decision (certificate or exact path) equals the oracle's f32 pixel-order rule,
+    with and without the forced exact path."""
+    import os
+
+    from conftest import GOLDEN
+
+    semtsdf, L = S
+    d = np.load(os.path.join(GOLDEN, "frames_tum_fr2.npz"))
+
+    def masks(depth, shift):
+        m = np.zeros(depth.shape, np.uint8)
+        z = depth.astype(np.float32) / 5000.0
+        yy, xx = np.mgrid[0:480, 0:640]
+        lab = 1 + ((np.clip((z - 0.5) / 0.4, 0, 3)).astype(np.int32) * 4 + ((xx + shift) // 160) % 4)
+        m[depth > 0] = np.minimum(lab[depth > 0], 31).astype(np.uint8)
+        return m
+
+    E0 = np.eye(4, dtype=np.float32)
+    # frame b seen from a slightly moved camera (small rotation about y, shift in x)
+    ang = 0.02
+    E1 = np.array([[np.cos(ang), 0, np.sin(ang), 0.01], [0, 1, 0, 0], [-np.sin(ang), 0, np.cos(ang), 0],
+                   [0, 0, 0, 1]], np.float32)
+    for force in (False, True):
+        p = semtsdf.default_params(128, KI, 640, 480)
+        semtsdf.place_from_frame(p, d["depth_a"], float(np.mean(d["depth_a"][d["depth_a"] > 0])) / 5000.0,
+                                 L.PLACE_SFM)
+        vol = semtsdf.Volume(p, 0)
+        vol.set_instrumentation(events=False, force_exact=force)
+        g = oracle.OGeom.from_params(p)
+        ost = oracle.OState([128] * 3, p.mu, semantic=True)
+        ma = masks(d["depth_a"], 0)
+        vol.parse_frame(d["depth_a"], d["rgb_a"], np.ascontiguousarray(ma.copy()), E0)
+        oracle.integrate(g, ost, list(p.K), E0, d["depth_a"], d["rgb_a"], ma, flags=0x3)
+        num = int(ma.max()) + 1
+        mb = masks(d["depth_b"], 40)
+        m_gpu = np.ascontiguousarray(mb.copy())
+        stats = vol.parse_frame(d["depth_b"], d["rgb_b"], m_gpu, E1)
+        probs, box = oracle.march_probs(g, list(p.Kinv), E1, 640, 480, ost.sdf, ost.hist, p.box_thresh)
+        m_ref, n_ref, mx, prev, _ = oracle.filter_overlaps(probs, box, mb, 1, num, 0.05, precision=0)
+        assert np.array_equal(m_gpu, m_ref), force
+        assert list(stats.assigned_prev) == list(prev) and stats.num_objs == n_ref, force
+        assert (prev >= 0).sum() >= 3  # real matches were made
+        if force:
+            assert stats.exact_rows == ((1 << mx) - 1) & ~1
+        vol.close()
+
+
+@pytest.mark.parametrize("nshards,chunk,exchange", [(2, 8, "min"), (3, 5, "allgather")])
+def test_sharded_exact_path_equals_single_volume(S, oracle, nshards, chunk, exchange):
+    """Sharded association through the exact path (every row forced onto it): assoc_apply
+    reports NEED_PIXELS, the shards' per-pixel data are summed, assoc_apply_exact decides --
+    masks, matches and counts identical to the single volume."""
+    from semtsdf.shard import LocalShardGroup
+    from semtsdf.synth import SyntheticStream
+    from semtsdf.volume import DeviceBuffer
+
+    semtsdf, L = S
+    st = SyntheticStream(seed=0)
+    frames = [st.frame(k) for k in range(5)]
+    p = semtsdf.default_params(64, KI, 640, 480)
+    p.dim[0], p.dim[1], p.dim[2] = 48, 40, 64
+    semtsdf.place_from_frame(p, frames[0].depth, float(np.mean(frames[0].depth[frames[0].depth > 0])) / 5000.0,
+                             L.PLACE_SFM)
+    vol = semtsdf.Volume(p, 0)
+    shards = []
+    for sidx in range(nshards):
+        q = semtsdf.default_params(64, KI, 640, 480)
+        for fld in ("dim", "vol_start", "vol_end", "voxel", "K", "Kinv"):
+            getattr(q, fld)[:] = getattr(p, fld)[:]
+        q.mu, q.flags = p.mu, p.flags
+        q.z_nshards, q.z_shard, q.z_chunk = nshards, sidx, chunk
+        shards.append(semtsdf.Volume(q, 0))
+        shards[-1].set_instrumentation(events=False, force_exact=True)
+    grp = LocalShardGroup(shards, exchange=exchange)
+    npx = 640 * 480
+    dbuf, rbuf = DeviceBuffer(npx * 2), DeviceBuffer(npx * 3)
+    mbufs = [DeviceBuffer(npx) for _ in shards]
+    exact = 0
+    for k in range(1, 5):
+        fr = frames[k]
+        E = (fr.w2c @ frames[0].c2w).astype(np.float32)
+        m_single = np.ascontiguousarray(fr.mask.copy())
+        stats = vol.parse_frame(fr.depth, fr.rgb, m_single, E)
+        dbuf.upload(fr.depth, grp.stream)
+        rbuf.upload(fr.rgb, grp.stream)
+        for mb in mbufs:
+            mb.upload(fr.mask, grp.stream)
+        if k >= 2:
+            sstats = grp.associate_dev([mb.ptr for mb in mbufs], E, want_stats=True)
+            for ss in sstats:
+                assert list(ss.assigned_prev) == list(stats.assigned_prev)
+                assert ss.num_objs == stats.num_objs and bytes(ss.lut) == bytes(stats.lut)
+                exact += ss.exact_rows != 0
+        for sh, mb in zip(shards, mbufs):
+            sh.integrate_dev(dbuf.ptr, rbuf.ptr, mb.ptr, E, grp.stream)
+            L.check(L.load().semtsdf_shard_note_integrated(sh.handle, L.ptr(mb.ptr), L.ptr(grp.stream)))
+        for mb in mbufs:
+            got = np.zeros(npx, np.uint8)
+            mb.download(got, grp.stream)
+            shards[0].sync()
+            assert np.array_equal(got, m_single.reshape(-1)), f"frame {k}"
+    assert exact == 3 * nshards
+    for sh in shards:
+        sh.close()
+    vol.close()
