@@ -350,8 +350,10 @@ def run_pipeline(semtsdf, L, p, local, n_frames=100, n_warm=5):
     mean_m = tum.mean_depth_m(frames[0].depth)
     ext0_inv = np.linalg.inv(P.parse_pos(traj[0, 1:]))  # frame 0 places the volume (tsdf.cu:173-214)
 
-    def run(overlap, instr=False, fused=False):
+    def run(overlap, instr=False, fused=False, force_exact=False):
         vol = semtsdf.Volume(p, local)
+        if force_exact:  # every association row decided from its exact f32 pixel-order sums
+            vol.set_instrumentation(events=False, force_exact=True)
         vstream = torch.cuda.ExternalStream(vol.stream, device=dev)
         cstream = torch.cuda.Stream(device=dev)
         rstream = torch.cuda.Stream(device=dev) if overlap else vstream
@@ -415,7 +417,7 @@ def run_pipeline(semtsdf, L, p, local, n_frames=100, n_warm=5):
         vol.sync()
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        tm = vol.timing() if instr else None
+        tm = vol.timing()
         if fused:  # the view of the last frame (rendered by the next frame's call), untimed
             s2w, c = semtsdf.orbit_camera(list(p.Kinv), 0.01 * (n_all - 1), mean_m)
             vol.raycast_dev(s2w, c, L.RENDER_LABEL, outs[(n_all - 1) % 2].data_ptr())
@@ -428,9 +430,13 @@ def run_pipeline(semtsdf, L, p, local, n_frames=100, n_warm=5):
     vol_s.close()
     # the reported rate: each frame's call renders the view of the previous frame's state in the
     # launch of its association march (semtsdf_parse_frame_view_dev); same frames, same views
-    vol_f, t_fus, _, img_f, objs_f = run(False, fused=True)
+    vol_f, t_fus, tm_f, img_f, objs_f = run(False, fused=True)
     vol_f.close()
     same_f = bool(torch.equal(img_f.cpu(), ref_img)) and objs_f == objs_s
+    # the cost of the decision's exact path: the same fused frames with every row forced onto it
+    vol_x, t_exact, tm_x, img_x, objs_x = run(False, fused=True, force_exact=True)
+    vol_x.close()
+    same_x = bool(torch.equal(img_x.cpu(), ref_img)) and objs_x == objs_s
     vol_b, _, tm, _, _ = run(False, instr=True)  # the same frames again, with events
     vol_b.close()
     vol, t_ovl, _, img_o, objs_o = run(True)
@@ -460,6 +466,14 @@ def run_pipeline(semtsdf, L, p, local, n_frames=100, n_warm=5):
         "serial_frames_per_s": n_frames / t_ser,
         "serial_ms_per_frame": t_ser * 1e3 / n_frames,
         "fused_equals_serial": same_f,
+        "view_lag_frames": 1,
+        "assoc_decisions": int(tm_f.n_assoc),
+        "assoc_exact_frames": int(tm_f.assoc_exact_frames),
+        "assoc_exact_rows": int(tm_f.assoc_exact_rows),
+        "assoc_exact_note": "decisions (warm-up included) whose certificate left rows to the exact f32 "
+                            "pixel-order path (DESIGN.md §4); all_exact_frames_per_s: every row forced onto it",
+        "all_exact_frames_per_s": n_frames / t_exact,
+        "all_exact_equals_serial": same_x,
         "overlapped_frames_per_s": n_frames / t_ovl,
         "overlapped_equals_serial": same,
         "frames": n_frames, "warmup_frames": n_warm,

@@ -198,7 +198,9 @@ int semtsdf_assoc_probs(semtsdf_vol* v, const float E[16], float* probs, uint8_t
 int semtsdf_filter_overlaps_dev(semtsdf_vol* v, const float* probs_d, const uint8_t* box_d, uint8_t* mask_d,
                                 semtsdf_assoc_stats* stats_host_or_null, void* stream);
 /* The association's f32 logf (fn 0) / expf (fn 1) on the device over n values (device
- * pointers): the host C library's results bit for bit (semtsdf_libm.h), for verification. */
+ * pointers): the host C library's results bit for bit (semtsdf_libm.h), for verification;
+ * fn 2: the device's own logf, which the march's fixed-point sums use (within the
+ * certificate's slack of the host's). */
 int semtsdf_libm_eval(int fn, const float* x_d, float* y_d, size_t n, void* stream);
 
 /* ---- per-frame driver (a7: TSDF::parse_frame/launch_kernel tsdf.cu:171-228,418-504) ----

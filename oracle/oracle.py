@@ -78,6 +78,8 @@ def lib():
         _lib.oracle_project.restype = None
         _lib.oracle_libm_mismatches.argtypes = [C.c_int, P, P, C.c_long, C.c_uint32]
         _lib.oracle_libm_mismatches.restype = C.c_long
+        _lib.oracle_logf_ulp_max.argtypes = [P, C.c_long, C.c_uint32]
+        _lib.oracle_logf_ulp_max.restype = C.c_double
     return _lib
 
 
@@ -196,8 +198,10 @@ def march_probs(g: OGeom, Kinv16, E16, W, H, sdf, hist, box_thresh=0.3):
     return probs, box
 
 
-def filter_overlaps(probs, box, mask, n_obs, num_objs, eps=0.05, precision=1, table=None):
+def filter_overlaps(probs, box, mask, n_obs, num_objs, eps=0.05, precision=0, table=None):
     """Relabels a copy of mask; returns (mask, num_objs, max_obj_now, assigned_prev, assigned_prob).
+    precision 0: the reference's f32 rule (logf terms summed in pixel order, expf of the f32
+    mean, tsdf.cu:312-349), which the device reproduces; 1: double accumulation (tests only).
     table: optional float64 [32, 32] that receives every candidate probability (row = current
     label, column = previous id)."""
     H, W = mask.shape

@@ -337,8 +337,10 @@ void oracle_march_probs(const int32_t* dims, const float* geo, const float* Kinv
 }
 
 /* ---------------------------------------------------------------- filter_overlaps
- * precision 0: the reference's float accumulation in pixel order (logf, expf);
- * precision 1: double accumulation (log, exp) — the decision contract of the device path.
+ * precision 0: the reference's float accumulation in pixel order (logf, expf) -- the rule the
+ *   device reproduces;
+ * precision 1: double accumulation of the same f32 terms, exp in double: a different rule,
+ *   used by the tests to find the cases that f32 rounding decides.
  * mask is relabelled in place; *num_objs is updated.  assigned_prev[i] = previous id
  * matched by current label i (or -1), assigned_prob[i] its probability.
  * Returns max_obj_now. */
@@ -811,4 +813,24 @@ long oracle_libm_mismatches(int fn, const float* x, const float* y, long n, uint
         if (memcmp(&r, &y[i], 4) != 0) ++bad;
     }
     return bad;
+}
+
+/* Largest distance in ulps (of the library result) between y[i] and this C library's logf of
+ * the consecutive float bit patterns u0 + i: bounds the device logf the association march's
+ * fixed-point sums use (the certificate's term slack). */
+double oracle_logf_ulp_max(const float* y, long n, uint32_t u0) {
+    double worst = 0.0;
+    for (long i = 0; i < n; ++i) {
+        const uint32_t u = u0 + (uint32_t)i;
+        float xi;
+        memcpy(&xi, &u, 4);
+        const float r = logf(xi);
+        if (r == 0.0f) {
+            if (y[i] != 0.0f) worst = INFINITY;
+            continue;
+        }
+        const double d = fabs((double)y[i] - (double)r) / (double)(nextafterf(fabsf(r), INFINITY) - fabsf(r));
+        if (d > worst) worst = d;
+    }
+    return worst;
 }

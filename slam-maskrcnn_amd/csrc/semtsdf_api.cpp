@@ -1106,7 +1106,7 @@ int semtsdf_filter_overlaps_dev(semtsdf_vol* v, const float* probs_d, const uint
 }
 
 int semtsdf_libm_eval(int fn, const float* x_d, float* y_d, size_t n, void* stream) {
-    if (fn != 0 && fn != 1) return fail(SEMTSDF_ERR_INVALID, "fn must be 0 (logf) or 1 (expf)");
+    if (fn < 0 || fn > 2) return fail(SEMTSDF_ERR_INVALID, "fn must be 0 (logf), 1 (expf) or 2 (device logf)");
     if (n && (!x_d || !y_d)) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
     HIPC(launch_libm_eval(fn, x_d, y_d, n, (hipStream_t)stream));
     return SEMTSDF_OK;

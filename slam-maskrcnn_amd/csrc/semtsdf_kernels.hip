@@ -2340,14 +2340,14 @@ __device__ __forceinline__ void assoc_accumulate(AssocLds& s, const float* p, un
         atomicAdd(&s.c1[m], 1u);
 #pragma unroll
         for (int j = 1; j < kMaxObjects; ++j) {
-            const float L = glibc::logf(fmaxf(p[j] / n_obs, eps));
+            const float L = logf(fmaxf(p[j] / n_obs, eps));
             atomicAdd(reinterpret_cast<unsigned long long*>(&s.t1[m][j]), (unsigned long long)to_fix(L));
         }
     }
 #pragma unroll
     for (int n = 1; n < kMaxObjects; ++n) {
         if (p[n] > box_thresh) {
-            const float L = glibc::logf(fmaxf(1.0f - p[n] / n_obs, eps));
+            const float L = logf(fmaxf(1.0f - p[n] / n_obs, eps));
             const unsigned long long f = (unsigned long long)to_fix(L);
             atomicAdd(reinterpret_cast<unsigned long long*>(&s.t2[n]), f);
             atomicAdd(&s.c2[n], 1u);
@@ -2364,28 +2364,40 @@ __device__ __forceinline__ void assoc_accumulate(AssocLds& s, const float* p, un
 // to the whole row and the per-pixel work is the few present bins (their to_fix(L) - F0).
 // The row baseline c1[m] * F0 is added when the workgroup flushes its tables; the integer
 // sums are identical.  Requires box_thresh >= 0 (an empty bin is never in the box).
+// px (optional): the pixel's data for the decision's exact path (AssocPixels), written in the
+// same loop: present bins (p != 0) and their counts, box bins (p > box_thresh >= 0 needs p != 0).
 __device__ __forceinline__ void assoc_accumulate_sparse(AssocLds& s, const float* p, unsigned bins, unsigned m,
-                                                        float n_obs, float eps, float box_thresh, long long F0) {
+                                                        float n_obs, float eps, float box_thresh, long long F0,
+                                                        const AssocPixels& px, int npx, int k) {
     const bool lab = m > 0 && m < (unsigned)kMaxObjects;
     if (lab) atomicAdd(&s.c1[m], 1u);
+    unsigned box = 0u;  // bins becomes the present bins (p != 0) as the loop goes
+    bins &= ~1u;
 #pragma unroll
     for (int j = 1; j < kMaxObjects; ++j) {
-        if (!((bins >> j) & 1u) || p[j] == 0.0f) continue;
+        if (!((bins >> j) & 1u)) continue;
+        if (p[j] == 0.0f) {
+            bins &= ~(1u << j);
+            continue;
+        }
+        if (px.bits) px.p[(size_t)j * npx + k] = p[j];
         if (lab) {
-            const long long d = to_fix(glibc::logf(fmaxf(p[j] / n_obs, eps))) - F0;
+            const long long d = to_fix(logf(fmaxf(p[j] / n_obs, eps))) - F0;
             if (d) atomicAdd(reinterpret_cast<unsigned long long*>(&s.t1[m][j]), (unsigned long long)d);
         }
         if (p[j] > box_thresh) {
-            const float L = glibc::logf(fmaxf(1.0f - p[j] / n_obs, eps));
+            const float L = logf(fmaxf(1.0f - p[j] / n_obs, eps));
             const unsigned long long f = (unsigned long long)to_fix(L);
             atomicAdd(reinterpret_cast<unsigned long long*>(&s.t2[j]), f);
             atomicAdd(&s.c2[j], 1u);
+            box |= 1u << j;
             if (lab) {
                 atomicAdd(reinterpret_cast<unsigned long long*>(&s.t3[m][j]), f);
                 atomicAdd(&s.c3[m][j], 1u);
             }
         }
     }
+    if (px.bits) px.bits[k] = make_uint2(bins, box);
 }
 
 // The pixel's data for the decision's exact path (AssocPixels): present and box bins, and the
@@ -2420,7 +2432,7 @@ __device__ __forceinline__ void assoc_tile(const AssocArgs& a, AssocLds& s, int 
     assoc_lds_clear(s);
     __syncthreads();
     const bool sparse = a.box_thresh >= 0.0f && !a.probs_out;  // see assoc_accumulate_sparse
-    const long long F0 = to_fix(glibc::logf(fmaxf(0.0f, a.eps)));  // an empty bin's term
+    const long long F0 = to_fix(logf(fmaxf(0.0f, a.eps)));      // an empty bin's term
 
     const int x = bx * 16 + (tid & 15);
     const int y = by * 16 + (tid >> 4);
@@ -2436,7 +2448,7 @@ __device__ __forceinline__ void assoc_tile(const AssocArgs& a, AssocLds& s, int 
             bins = tri_hist(a.g, a.b, tr, p);
         }
         const int px = y * a.width + x;
-        if (a.px.bits) assoc_pixel_out(a.px, a.width * a.height, px, p, bins, a.box_thresh);
+        if (a.px.bits && !sparse) assoc_pixel_out(a.px, a.width * a.height, px, p, bins, a.box_thresh);
         if (a.probs_out) {
 #pragma unroll
             for (int k = 0; k < kMaxObjects; ++k) {
@@ -2446,7 +2458,8 @@ __device__ __forceinline__ void assoc_tile(const AssocArgs& a, AssocLds& s, int 
         }
         if (a.debug != 1) {
             if (sparse)
-                assoc_accumulate_sparse(s, p, bins, a.mask[px], a.n_obs, a.eps, a.box_thresh, F0);
+                assoc_accumulate_sparse(s, p, bins, a.mask[px], a.n_obs, a.eps, a.box_thresh, F0, a.px,
+                                        a.width * a.height, px);
             else
                 assoc_accumulate(s, p, a.mask[px], a.n_obs, a.eps, a.box_thresh);
         }
@@ -2677,7 +2690,11 @@ __device__ float exact_row_sum(int i, int j, const DecideArgs& a, float c0, Scan
 }
 
 // Certified interval [lo, hi] of the reference's f32 exp(A/C) from the fixed-point sums, and
-// the point estimate mid (see above).  A fixed = the 2^-28 fixed-point sum, n = count.
+// the point estimate mid (see above).  A fixed = the 2^-28 fixed-point sum, n = count.  Each
+// fixed-point term differs from the reference's glibc logf term by at most kTermSlack: half a
+// unit of 2^-28 plus the device logf's distance to glibc's (<= 2 ulp over [eps, 1],
+// tests/test_gpu_assoc_exact.py; 4 ulp at |t| < 4 = 2^-20 allowed).
+constexpr double kTermSlack = 0x1p-29 + 0x1p-20;
 __device__ __forceinline__ void prob_interval(long long A, long long n, double* lo, double* hi, double* mid) {
     if (n <= 0) { *lo = *hi = *mid = 0.0; return; }
     const double dn = (double)n;
@@ -2686,8 +2703,8 @@ __device__ __forceinline__ void prob_interval(long long A, long long n, double* 
     const double g = (dn - 1.0) * 0x1p-24;
     if (g >= 0.5) { *lo = 0.0; *hi = 2.0; return; }  // no certificate: the exact path decides
     const double gam = g / (1.0 - g) * (1.0 + 0x1p-40);
-    const double slo = S - dn * 0x1p-29 * (1.0 + 0x1p-40);
-    const double shi = fmin(S + dn * 0x1p-29 * (1.0 + 0x1p-40), 0.0);
+    const double slo = S - dn * kTermSlack * (1.0 + 0x1p-40);
+    const double shi = fmin(S + dn * kTermSlack * (1.0 + 0x1p-40), 0.0);
     const double qlo = slo * (1.0 + gam) / dn * (1.0 + 0x1p-24 + 0x1p-40) - 0x1p-60;
     const double qhi = shi * (1.0 - gam) / dn * (1.0 - 0x1p-24 - 0x1p-40) + 0x1p-60;
     *lo = exp(qlo) * (1.0 - 0x1p-23 - 0x1p-40);
@@ -2799,15 +2816,27 @@ __global__ __launch_bounds__(256) void k_assoc_decide(DecideArgs a) {
         for (int i = 1; i < max_now; ++i) {
             if (!((F >> i) & 1u)) continue;
             const float A = exact_row_sum(i, j, a, c0, L.scan);
-            if (tid == 0) a.X->A[i][j] = A;
+            // write-through (sc1) store: the deciding workgroup may sit on another XCD
+            if (tid == 0) __hip_atomic_store(&a.X->A[i][j], A, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    // ---- the last workgroup decides ----
-    __threadfence();
-    if (tid == 0) L.last = atomicAdd(&a.X->counter, 1u) == gridDim.x - 1u;
+    // ---- the last workgroup decides (in-launch hand-off: every storing wave drains its stores,
+    // one release + counter ticket per workgroup, one acquire in the last arriver) ----
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned ticket = __hip_atomic_fetch_add(&a.X->counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        L.last = ticket == gridDim.x - 1u;
+    }
     __syncthreads();
     if (!L.last) return;
-    __threadfence();
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
     AssocDecision* D = a.D;
     const unsigned Fx = have_px ? F : 0u;
     for (int k = tid; k < kMaxObjects * kMaxObjects; k += 256) {
@@ -2880,7 +2909,7 @@ __global__ __launch_bounds__(256) void k_assoc_decide(DecideArgs a) {
             a.X->frames += 1u;
             a.X->rows += (unsigned)__popc(Fx);
         }
-        a.X->counter = 0u;
+        __hip_atomic_store(&a.X->counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // every read of T is above (the last barrier orders them): clear it for the next frame
     uint2* w = reinterpret_cast<uint2*>(T);
@@ -2968,7 +2997,7 @@ hipError_t launch_assoc_from_probs(const float* probs, const uint8_t* box, const
 
 __global__ __launch_bounds__(256) void k_libm_eval(int fn, const float* __restrict__ x, float* __restrict__ y, size_t n) {
     for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
-        y[i] = fn == 0 ? glibc::logf(x[i]) : glibc::expf(x[i]);
+        y[i] = fn == 0 ? glibc::logf(x[i]) : fn == 1 ? glibc::expf(x[i]) : logf(x[i]);  // 2: the march's logf
 }
 
 hipError_t launch_libm_eval(int fn, const float* x, float* y, size_t n, hipStream_t s) {
@@ -3131,7 +3160,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_MAR
 // tiles of each fill the other's tail.  Workgroup b: tiles alternate (association, render)
 // while both have tiles left, then the rest of the larger one.
 template <bool OCT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_MARCH_WPE))) void k_march_fused(
+#ifndef SEMTSDF_FUSED_WPE
+#define SEMTSDF_FUSED_WPE 4  // 4 waves per SIMD: at most 128 VGPRs (the association's per-pixel output put it at 131)
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_FUSED_WPE))) void k_march_fused(
     AssocArgs aa, RenderArgs ra, int na, int nr) {
     __shared__ AssocLds s;
     const int b = (int)blockIdx.x, m = min(na, nr);

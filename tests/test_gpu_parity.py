@@ -142,7 +142,7 @@ def test_association_probs_and_relabel(S, oracle, stream):
             num = int(m_ref.max()) + 1
         else:
             m_ref, num, _, prev, _ = oracle.filter_overlaps(probs_o, box_o, m_ref, k - 1, num, p.prior_mrcnn_err_rate,
-                                                            precision=1)
+                                                            precision=0)
             assert np.array_equal(np.array(stats.assigned_prev[:]), prev)
             assert stats.num_objs == num
         assert np.array_equal(m_gpu, m_ref), f"frame {k}"
@@ -887,7 +887,7 @@ def test_parse_frame_ragged_image_device_equals_host_and_oracle(S, oracle, strea
             num = int(m_ref.max()) + 1
         else:
             probs, box = oracle.march_probs(g, list(p.Kinv), E, Wr, Hr, ost.sdf, ost.hist, p.box_thresh)
-            m_ref, num, _, _, _ = oracle.filter_overlaps(probs, box, m_ref, k - 1, num, p.prior_mrcnn_err_rate, 1)
+            m_ref, num, _, _, _ = oracle.filter_overlaps(probs, box, m_ref, k - 1, num, p.prior_mrcnn_err_rate, 0)
         oracle.integrate(g, ost, list(p.K), E, d, c, m_ref, flags=0x3)
         assert np.array_equal(mh, m_ref), f"host mask, frame {k}"
         assert np.array_equal(md.cpu().numpy().reshape(Hr, Wr), m_ref), f"device mask, frame {k}"
