@@ -409,9 +409,16 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
         HIPC(hipEventRecord(F.prep_done, ps));
         HIPC(hipStreamWaitEvent(s, F.prep_done, 0));
     }
-    if (relabel_after) {
+    // the relabel of a frame whose prepass ran beside its association: by the integrate
+    // itself (records mapped as they are read, the mask at the kernel's end; one launch and the
+    // stream gap in front of it fewer) or, with SEMTSDF_RELABEL_KERNEL=1, by k_relabel_records
+    static const bool relabel_kernel = getenv("SEMTSDF_RELABEL_KERNEL") && atoi(getenv("SEMTSDF_RELABEL_KERNEL"));
+    if (relabel_after && relabel_kernel) {
         HIPC(launch_relabel_records(const_cast<uint8_t*>(mask_d), v->p.width, v->p.height, F.pyr, v->decision_d, s));
         v->pending_lut = nullptr;
+    } else if (relabel_after) {
+        a.lut = &v->decision_d->lut[0];
+        a.relabel_mask = const_cast<uint8_t*>(mask_d);
     }
     // the volume's writer: after the last empty-space map update
     if (int rc = after_bmin(v, s)) return rc;
@@ -435,6 +442,7 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
         HIPC(hipMemsetAsync(a.wtrace, 0, kWtSlots * kWaveTraceWords * 8, s));
     }
     HIPC(launch_integrate(a, s, ep.a, ep.b));
+    if (a.lut) v->pending_lut = nullptr;  // consumed by the integrate
     if (wt) {
         std::vector<unsigned long long> h(kWtSlots * kWaveTraceWords);
         HIPC(hipMemcpyAsync(h.data(), a.wtrace, h.size() * 8, hipMemcpyDeviceToHost, s));

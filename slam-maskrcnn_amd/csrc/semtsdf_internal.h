@@ -139,6 +139,9 @@ struct IntegrateArgs {
     unsigned long long* wtrace;    // instrumentation (build with SEMTSDF_WAVE_TRACE=1, run with
                                    // SEMTSDF_WAVE_TRACE=<file>): per wave kWaveTraceWords timestamps
     unsigned wtrace_slots;         // waves wtrace holds (waves past it are not traced)
+    const uint8_t* lut;            // deferred relabel of an association decision (256 bytes, device): the
+                                   // pixel records carry the frame's raw labels; nullptr: none
+    uint8_t* relabel_mask;         // the frame's mask, relabelled in place through lut by the kernel (nullable)
 };
 constexpr int kWaveTraceWords = 8;
 

@@ -1080,9 +1080,18 @@ __device__ __forceinline__ void stage_project(const IntegrateArgs& a, const Unit
     }
 }
 
+// The deferred relabel of a frame whose prepass ran beside its association (IntegrateArgs::lut):
+// label byte of a pixel record -> the decision's new label, from the 256-byte table held one
+// dword per lane (lutv, lane l = labels 4l..4l+3; every lane of the wave active).
+__device__ __forceinline__ uint32_t relabel_rec(uint32_t rec, unsigned lutv) {
+    const unsigned raw = rec >> 24;
+    const unsigned w = (unsigned)__shfl((int)lutv, (int)(raw >> 2), 64);
+    return (rec & 0x00FFFFFFu) | (((w >> (8u * (raw & 3u))) & 0xFFu) << 24);
+}
+
 template <bool SEM, bool GATE, bool VOTE, bool COUNT, bool FREE>
 __device__ __forceinline__ void stage_classify(const IntegrateArgs& a, const Proj& P, Cls& C, bool count,
-                                               unsigned& n_touch, unsigned& n_gate) {
+                                               unsigned& n_touch, unsigned& n_gate, unsigned lutv) {
     const VolGeom& g = a.g;
     if (FREE) {  // free unit (unit_cull == 2): a voxel with depth is touched with f == 1, never gated
         unsigned tm = 0;
@@ -1115,6 +1124,10 @@ __device__ __forceinline__ void stage_classify(const IntegrateArgs& a, const Pro
         tmask |= (t ? 1u : 0u) << k;
         C.pix[k] = P.rec[k].y;
         if (VOTE) C.img[k] = P.lin[k];
+    }
+    if (SEM && a.lut) {  // uniform: records of a deferred relabel carry raw labels
+#pragma unroll
+        for (int k = 0; k < 4; ++k) C.pix[k] = relabel_rec(C.pix[k], lutv);
     }
     C.sflag = P.sflag;
     if (dslow || !a.fastdiv) {  // rare: tiny differences, or mu outside the reciprocal range
@@ -1151,16 +1164,18 @@ __device__ __forceinline__ void stage_classify(const IntegrateArgs& a, const Pro
 }
 
 #ifndef SEMTSDF_FULLROW
-#define SEMTSDF_FULLROW 1
+#define SEMTSDF_FULLROW 0
 #endif
-// The steady flag of a line is decided from the values of all 8 lanes of the line after the
-// update, so lanes of a line must not read the dummy line when another lane of it updates
-// (a per-lane build measured 2.5 % faster and flagged unsteady lines steady: the sharded
-// GPU test caught it, profiles/r03/s2/ab_full_row.txt).
-static_assert(SEMTSDF_FULLROW || !SEMTSDF_STEADY, "steady-line flags need whole-line state traffic");
-// Whole-line state traffic: a 128-B line of a per-voxel array is the 8 lanes of one
-// z-quad (lane % 8); when any of them updates, all 8 load and store it (unchanged values
-// included), so every line written back is fully dirty.
+// State traffic per lane (SEMTSDF_FULLROW 0): a lane loads and stores its 16-B vectors only
+// when it updates (sdf/weight: a touched voxel; colour: a gated one); a 128-B line of a
+// per-voxel array is the 8 lanes of one z-quad (lane % 8).  The line's steady flag is then
+// decided from the lanes that loaded their values plus what the old flag says of the others:
+// an untouched lane of a steady line still holds sdf 1.0f and a weight < 2^23; of a line not
+// known steady, nothing (it stays 0, "unknown").  (r03's per-lane build decided the flag from
+// every lane's values, the dummy line's included, and flagged unsteady lines steady:
+// profiles/r03/s2/gputest_full_row_0_failure.txt.)  SEMTSDF_FULLROW 1: whole-line traffic
+// (all 8 lanes load and store when any of them updates; every line written back fully dirty).
+static_assert(!SEMTSDF_LAZY_WEIGHT || SEMTSDF_FULLROW, "lazy weights need whole-line state traffic");
 constexpr uint64_t line_lanes() {  // lanes of one line of slot 0, z-quad 0: zq + LZQ y
     uint64_t m = 0;
     for (int y = 0; y < UY; ++y) m |= 1ull << (LZQ * y);
@@ -1236,7 +1251,8 @@ __device__ __forceinline__ void stage_load(const IntegrateArgs& a, const UnitPos
     bool fone = true;
 #pragma unroll
     for (int k = 0; k < 4; ++k) fone &= (((C.tmask >> k) & 1u) == 0u) | (C.fv[k] == 1.0f);
-    const bool skip = SEMTSDF_STEADY && tile_line_all((C.sflag != 0u) & fone);
+    // (whole-line traffic: the whole line skips together; per-lane: each lane for itself)
+    const bool skip = SEMTSDF_STEADY && (SEMTSDF_FULLROW ? tile_line_all((C.sflag != 0u) & fone) : ((C.sflag != 0u) & fone));
     // lazy: steady, every voxel of the line touched (f == 1), pending count below the cap
     const bool lazy = SEMTSDF_STEADY && SEMTSDF_LAZY_WEIGHT && !VOTE && a.free_ok &&
                       tile_line_all((C.sflag != 0u) & (C.sflag < kFlagMax) & fone & (C.tmask == 15u));
@@ -1384,7 +1400,10 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
     const unsigned tmask = M.meta & 15u, gmask = (M.meta >> 4) & 15u, hmode = (M.meta >> 8) & 3u,
                    hlab = M.meta >> 16;
     const bool trow = tile_line_any(tmask != 0u), grow = tile_line_any(gmask != 0u);
-    if (!trow) return;
+    // the lines with an update stay active together (the flag below is a ballot over a line)
+    const bool line = SEMTSDF_FULLROW ? trow : ((__ballot(tmask != 0u) >> ((int)__lane_id() % LZQ +
+                                                 lane_slot((int)__lane_id()) * kUnitLanes)) & kLineLanes) != 0ull;
+    if (!line) return;
     const uint64_t v = unit_tile(g, up) + coff;
     if (a.b.bdirty) {
         // a brick of the empty-space map changes only where a voxel crossed the threshold:
@@ -1406,13 +1425,15 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
         }
     }
     if (COUNT && O.lazy) n_lazy += 4u;
-    if (!(kProbes && a.debug == 10) && !O.lazy) {  // 10: timing probe, loads but no sdf/weight stores
+    if (!(kProbes && a.debug == 10) && !O.lazy && trow) {  // 10: timing probe, loads but no sdf/weight stores
         if (!O.skip) st_state(a.b.sdf + v, O.s4);
         st_state(a.b.wt + v, O.w4);
     }
     if (SEMTSDF_STEADY) {  // the line's flag byte after this update (one lane per line writes)
-        const bool one = (O.s4.x == 1.0f) & (O.s4.y == 1.0f) & (O.s4.z == 1.0f) & (O.s4.w == 1.0f) &
-                         (O.w4.x < (1 << 23)) & (O.w4.y < (1 << 23)) & (O.w4.z < (1 << 23)) & (O.w4.w < (1 << 23));
+        const bool vals = (O.s4.x == 1.0f) & (O.s4.y == 1.0f) & (O.s4.z == 1.0f) & (O.s4.w == 1.0f) &
+                          (O.w4.x < (1 << 23)) & (O.w4.y < (1 << 23)) & (O.w4.z < (1 << 23)) & (O.w4.w < (1 << 23));
+        // a lane that did not load its values (per-lane traffic) keeps what the old flag says
+        const bool one = trow ? vals : (O.oflag != 0u);
         // a lazy line counts one more pending increment; any other update stored the weights
         // with the pending count folded in: steady (1) or not (0)
         const unsigned nb = O.lazy ? O.oflag + 1u : (tile_line_all(one) ? 1u : 0u);
@@ -1535,6 +1556,7 @@ struct Pipe {
     Ld L;
     Out O;
     bool primed = false;
+    unsigned lutv = 0;  // deferred relabel table, one dword per lane (IntegrateArgs::lut)
 };
 
 // Unit-kind of a list: 0 general, 1 free (projected), 2 full free (no projection).
@@ -1554,7 +1576,7 @@ __device__ __forceinline__ void list_prime(const IntegrateArgs& a, const UnitGri
     group_entries(v, v.i, seg_cap, e);
     S.cur = lane_pos(ug, e);
     stage_project<SHARD, PIN, FREE, FULL, VOTE>(a, S.cur, lane, S.P);
-    stage_classify<SEM, GATE, VOTE, COUNT, FREE>(a, S.P, S.C, true, n_touch, n_gate);
+    stage_classify<SEM, GATE, VOTE, COUNT, FREE>(a, S.P, S.C, true, n_touch, n_gate, S.lutv);
     stage_load<SEM, CI32, VOTE, FREE>(a, S.cur, coff, S.C, S.L);
     S.primed = true;
 }
@@ -1588,7 +1610,7 @@ __device__ __forceinline__ void integrate_list(const IntegrateArgs& a, const Uni
         stage_project<SHARD, PIN, FREE, FULL, VOTE>(a, nxt, lane, S.P);
         stage_compute<SEM, GATE, CI32, VOTE, FREE>(a, s_rcp, S.C, S.L, S.O);
         const StoreMeta Mc = store_meta(S.C);
-        stage_classify<SEM, GATE, VOTE, COUNT, FREE>(a, S.P, S.C, true, n_touch, n_gate);
+        stage_classify<SEM, GATE, VOTE, COUNT, FREE>(a, S.P, S.C, true, n_touch, n_gate, S.lutv);
         stage_store<SEM, CI32, VOTE, FREE, COUNT>(a, S.cur, coff, Mc, S.O, n_lazy);
         stage_load<SEM, CI32, VOTE, FREE>(a, nxt, coff, S.C, S.L);
         S.cur = nxt;
@@ -1600,7 +1622,7 @@ __device__ __forceinline__ void integrate_list(const IntegrateArgs& a, const Uni
         stage_project<SHARD, PIN, NFREE, NFULL, VOTE>(a, nxt, lane, S.P);
         stage_compute<SEM, GATE, CI32, VOTE, FREE>(a, s_rcp, S.C, S.L, S.O);
         const StoreMeta Mc = store_meta(S.C);
-        stage_classify<SEM, GATE, VOTE, COUNT, NFREE>(a, S.P, S.C, true, n_touch, n_gate);
+        stage_classify<SEM, GATE, VOTE, COUNT, NFREE>(a, S.P, S.C, true, n_touch, n_gate, S.lutv);
         stage_store<SEM, CI32, VOTE, FREE, COUNT>(a, S.cur, coff, Mc, S.O, n_lazy);
         stage_load<SEM, CI32, VOTE, NFREE>(a, nxt, coff, S.C, S.L);
         S.cur = nxt;
@@ -1643,6 +1665,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
     unsigned n_touch = 0, n_gate = 0, n_lazy = 0;
     unsigned nlive = 0;
     Pipe S;
+    if (SEM && a.lut) S.lutv = reinterpret_cast<const uint32_t*>(a.lut)[lane];
     const unsigned* cnt = a.list_count;
     const unsigned* lst = a.unit_list;
     const size_t lstride = (size_t)kListSegs * seg_cap;
@@ -1689,12 +1712,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
                                                                         n_touch, n_gate, n_lazy);
         n0 = v0.total;
     }
+    if (SEM && a.lut && a.relabel_mask) {  // the frame's mask through the same table, in place
+        const unsigned npx = (unsigned)(a.width * a.height);
+        const unsigned gid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
+        uint32_t* m4 = reinterpret_cast<uint32_t*>(a.relabel_mask);
+        const bool al = ((uintptr_t)a.relabel_mask & 3u) == 0u;
+        const unsigned n4 = al ? npx >> 2 : 0u;
+        for (unsigned base = 0; base < n4; base += nth) {  // uniform trip count: every lane shuffles
+            const unsigned i = base + gid;
+            const uint32_t v = i < n4 ? m4[i] : 0u;
+            uint32_t o = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) o |= (relabel_rec(v << (24 - 8 * k), S.lutv) >> 24) << (8 * k);
+            if (i < n4) m4[i] = o;
+        }
+        for (unsigned base = n4 * 4; base < npx; base += nth) {  // unaligned mask or the tail bytes
+            const unsigned i = base + gid;
+            const uint32_t v = i < npx ? (uint32_t)a.relabel_mask[i] : 0u;
+            const uint32_t o = relabel_rec(v << 24, S.lutv) >> 24;
+            if (i < npx) a.relabel_mask[i] = (uint8_t)o;
+        }
+    }
     if (SEMTSDF_WAVE_TRACE && a.wtrace && wave < a.wtrace_slots) {
         tr[4] = wall_clock64();
         trn |= groups_of(n0, rot0) << 40;
         if (lane < 8) {
             const unsigned long long hw = (unsigned long long)__smid() | ((unsigned long long)blockIdx.x << 32);
-            const unsigned long long v = lane < 5 ? tr[lane < 5 ? lane : 0] : lane == 5 ? hw : lane == 6 ? trn : 0ull;
+            // word 7: HW_ID (wave id bits 3:0, SIMD bits 5:4, CU bits 11:8, ...) for per-SIMD analyses
+            const unsigned hwid = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
+            const unsigned long long v = lane < 5 ? tr[lane < 5 ? lane : 0] : lane == 5 ? hw : lane == 6 ? trn : (unsigned long long)hwid;
             a.wtrace[(size_t)wave * kWaveTraceWords + lane] = v;
         }
     }

@@ -71,6 +71,26 @@ def main():
         n = len(end)
         print("  waves done by: " + " ".join(f"{q}%={end[min(n - 1, int(n * q / 100))]:.1f}"
                                             for q in (25, 50, 75, 90, 95, 99)))
+        hwid = (r[:, 7] & 0xFFFFFFFF).astype(np.int64)
+        if hwid.any():  # word 7: HW_ID (SIMD bits 5:4): does a wave's age on its SIMD set its pace?
+            simd = (hwid >> 4) & 3
+            key = cu * 4 + simd
+            uk, kinv = np.unique(key, return_inverse=True)
+            rank = np.zeros(len(r), np.int64)
+            for k in range(len(uk)):
+                idx = np.flatnonzero(kinv == k)
+                rank[idx[np.argsort(t[idx, 0], kind="stable")]] = np.arange(idx.size)
+            dur = t[:, 4] - t[:, 0]
+            print(f"  waves per SIMD: {np.bincount(np.bincount(kinv)).nonzero()[0].tolist()}; by age rank on the "
+                  "SIMD (0 = entered first): " + " ".join(
+                      f"r{q}: n={int((rank == q).sum())} dur={dur[rank == q].mean():.1f} end={t[rank == q, 4].mean():.1f}"
+                      for q in range(int(rank.max()) + 1)))
+            per_simd_max = np.zeros(len(uk))
+            np.maximum.at(per_simd_max, kinv, t[:, 4])
+            per_simd_mean = np.bincount(kinv, weights=t[:, 4]) / np.bincount(kinv)
+            print(f"  per SIMD: mean end p0={per_simd_mean.min():.1f} p50={np.median(per_simd_mean):.1f} "
+                  f"max={per_simd_mean.max():.1f}; spread within a SIMD (max - mean) p50="
+                  f"{np.median(per_simd_max - per_simd_mean):.1f} max={np.max(per_simd_max - per_simd_mean):.1f}")
 
 
 if __name__ == "__main__":
