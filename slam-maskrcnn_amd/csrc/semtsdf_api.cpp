@@ -1417,6 +1417,7 @@ int semtsdf_shard_assoc_pixels(semtsdf_vol* v, const void* gathered_d, int32_t* 
     HIPC(hipSetDevice(v->device));
     hipStream_t s = pick(v, stream);
     ShardRayArgs a = shard_args(v);
+    a.kind = SEMTSDF_RAY_ASSOC;  // the protocol's kind (assoc_partial has closed it)
     a.gathered = (const int2*)gathered_d;
     HIPC(launch_shard_assoc_pixels(a, px_d, s));
     return SEMTSDF_OK;

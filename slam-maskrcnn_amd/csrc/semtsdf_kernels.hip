@@ -1581,6 +1581,30 @@ __device__ __forceinline__ void list_prime(const IntegrateArgs& a, const UnitGri
     S.primed = true;
 }
 
+// Issue priority rotation of the persistent waves.  The 4 waves sharing a SIMD (one from each of
+// the CU's 4 workgroups) are arbitrated by priority, then age: at equal priority the oldest wave
+// issues first, and with equal static shares the waves end in age order, the youngest ≈ 40 %
+// after the oldest (per-wave trace, profiles/r04/wave_trace_age.txt), the SIMD running its
+// tail with fewer and fewer waves.  Each wave rotates its priority every group, offset by its
+// workgroup's dispatch round (blockIdx / CUs: blocks are dealt to the CUs in rounds), so at
+// any time the 4 waves of a SIMD hold distinct priorities and each holds the top one a
+// quarter of the time.
+#ifndef SEMTSDF_PRIO_ROTATE
+#define SEMTSDF_PRIO_ROTATE 1
+#endif
+__device__ __forceinline__ void rotate_prio(unsigned p) {
+    if (!SEMTSDF_PRIO_ROTATE) return;
+    switch (p & 3u) {  // s_setprio takes an immediate
+        case 0: __builtin_amdgcn_s_setprio(0); break;
+        case 1: __builtin_amdgcn_s_setprio(1); break;
+        case 2: __builtin_amdgcn_s_setprio(2); break;
+        default: __builtin_amdgcn_s_setprio(3); break;
+    }
+}
+__device__ __forceinline__ unsigned dispatch_round() {
+    return __builtin_amdgcn_readfirstlane((blockIdx.x * 4u) / gridDim.x);
+}
+
 // One list (kind KIND) by one persistent wave, software-pipelined.  The wave's last unit of
 // the list is computed and stored under the project / classify / load of its first unit of
 // the next list (kind NKIND, `nx`; NKIND < 0: none), which then starts primed: the pipeline
@@ -1615,6 +1639,7 @@ __device__ __forceinline__ void integrate_list(const IntegrateArgs& a, const Uni
         stage_load<SEM, CI32, VOTE, FREE>(a, nxt, coff, S.C, S.L);
         S.cur = nxt;
         v.i += nwaves;
+        rotate_prio(dispatch_round() + v.i / nwaves);
     }
     // the wave's last unit of this list
     if (NKIND >= 0 && SEMTSDF_CHAIN && chain) {
@@ -2612,127 +2637,157 @@ __device__ __forceinline__ int wg_min(int v, ScanLds& L) {
     return r;
 }
 
-// The reference's A[i][j] (tsdf.cu:312-334) for one current label i and previous id j: the f32
-// sum, in pixel order, of logf(max(p/n, eps)) over pixels labelled i and logf(max(1 - p/n, eps))
-// over the other pixels whose box bit j is set (every pixel adds at most one term).  The
-// sequential additions s <- RN(s + x) are evaluated in chunks of kScanChunk pixels: while s
+// One chunk of the reference's sequential f32 additions s <- RN(s + x) (tsdf.cu:318,329) for one
+// row: x[e] are the chunk's terms of this lane (pixel base + 8 tid + e, 0 = no term).  While s
 // stays in one binade [2^e, 2^(e+1)) (all terms <= 0, |s| grows), its grid is the multiples of
-// u = 2^(e-23) and RN(s + x) = s + round_u(x) exactly, so a chunk's steps are an integer prefix
-// sum of round_u(x) / u.  A step that would reach the next binade, a tie (x an odd multiple of
-// u/2, where the parity of s decides), a positive term or s == 0 is taken as the f32 addition
-// itself, and the chunk resumes after it with the new binade.
-__device__ float exact_row_sum(int i, int j, const DecideArgs& a, float c0, ScanLds& L) {
+// u = 2^(e-23) and RN(s + x) = s + round_u(x) exactly, so the chunk's steps are an integer prefix
+// sum of round_u(x) / u (a workgroup scan).  A step that would reach the next binade, a tie (x an
+// odd multiple of u/2, where the parity of s decides), a positive term, s == 0 or a subnormal s
+// is taken as the f32 addition itself, and the chunk resumes after it with the new binade.
+// Returns the new s (workgroup-uniform).
+__device__ float scan_chunk(float s, const float* x, ScanLds& L) {
+    const int tid = threadIdx.x;
+    int pos = 0;  // chunk elements before pos are done
+    for (;;) {
+        const unsigned sb = glibc::f2u(s);
+        if (s == 0.0f || (sb >> 31) == 0u || ((sb >> 23) & 0xFFu) == 0u) {
+            // s == 0 (the first nonzero term is the sum), s > 0 or subnormal (not reached by
+            // same-sign terms of the association): one addition at a time
+            int f = kScanChunk;
+#pragma unroll
+            for (int e = 0; e < kScanPer; ++e) {
+                const int idx = tid * kScanPer + e;
+                if (idx >= pos && x[e] != 0.0f && idx < f) f = idx;
+            }
+            f = wg_min(f, L);
+            if (f == kScanChunk) return s;
+            if (f >= tid * kScanPer && f < (tid + 1) * kScanPer) {
+#pragma unroll
+                for (int e = 0; e < kScanPer; ++e)
+                    if (tid * kScanPer + e == f) L.xv = x[e];
+            }
+            __syncthreads();
+            s = s + L.xv;
+            __syncthreads();
+            pos = f + 1;
+            continue;
+        }
+        const int uexp = (int)((sb >> 23) & 0xFFu) - 150;             // u = 2^uexp
+        const long long S0 = (long long)((sb & 0x7FFFFFu) | 0x800000u);  // |s| / u
+        long long r[kScanPer];
+        bool viol[kScanPer];
+        long long lsum = 0;
+#pragma unroll
+        for (int e = 0; e < kScanPer; ++e) {
+            const int idx = tid * kScanPer + e;
+            r[e] = 0;
+            viol[e] = false;
+            if (idx >= pos && x[e] != 0.0f) {
+                if (x[e] > 0.0f) {
+                    viol[e] = true;
+                } else {
+                    const double v = ldexp(-(double)x[e], -uexp);  // |x| / u, exact
+                    if (v >= 0x1p25) {
+                        r[e] = 1ll << 25;
+                        viol[e] = true;
+                    } else {
+                        const double fl = floor(v), fr = v - fl;
+                        r[e] = (long long)fl + (fr > 0.5 ? 1 : 0);
+                        viol[e] = fr == 0.5;
+                    }
+                }
+            }
+            lsum += r[e];
+        }
+        long long tot;
+        const long long ex = wg_exscan(lsum, L, &tot);
+        int f = kScanChunk;
+        long long run = ex;
+#pragma unroll
+        for (int e = 0; e < kScanPer; ++e) {
+            const int idx = tid * kScanPer + e;
+            run += r[e];
+            if ((viol[e] || S0 + run >= (1ll << 24)) && idx >= pos && idx < f) f = idx;
+        }
+        f = wg_min(f, L);
+        if (f == kScanChunk)  // the rest of the chunk stays in this binade
+            return -(float)ldexp((double)(S0 + tot), uexp);
+        if (f >= tid * kScanPer && f < (tid + 1) * kScanPer) {
+            long long before = ex;
+#pragma unroll
+            for (int e = 0; e < kScanPer; ++e) {
+                if (tid * kScanPer + e == f) L.xv = x[e];
+                if (tid * kScanPer + e < f) before += r[e];
+            }
+            L.before = before;
+        }
+        __syncthreads();
+        s = -(float)ldexp((double)(S0 + L.before), uexp);  // exact: the steps before f
+        s = s + L.xv;                                        // step f as the f32 addition
+        __syncthreads();
+        pos = f + 1;
+        if (pos >= kScanChunk) return s;
+    }
+}
+
+// The reference's A[i][j] (tsdf.cu:312-334) of every flagged current label i (rows) for previous
+// id j: the f32 sum, in pixel order, of logf(max(p/n, eps)) over pixels labelled i and
+// logf(max(1 - p/n, eps)) over the other pixels whose box bit j is set (every pixel adds at most
+// one term to an entry).  One pass over the pixels serves all rows: a chunk's per-pixel data
+// (label, bits, count of bin j) is loaded once, one chunk ahead of its use, and each row scans
+// the chunk with its own running sum (s_rows, LDS).
+__device__ void exact_rows_sum(unsigned rows, int j, const DecideArgs& a, float c0, ScanLds& L, float* s_rows) {
     const int tid = threadIdx.x;
     const float* pj = a.px.p + (size_t)j * a.npx;
-    float s = 0.0f;
-    for (int base = 0; base < a.npx; base += kScanChunk) {
-        float x[kScanPer];
-        bool any = false;
+    if (tid < kMaxObjects) s_rows[tid] = 0.0f;
+    __syncthreads();
+    unsigned m_n[kScanPer];
+    uint2 b_n[kScanPer];
+    float p_n[kScanPer];
+    auto load = [&](int base) {
 #pragma unroll
         for (int e = 0; e < kScanPer; ++e) {
             const int k = base + tid * kScanPer + e;
-            float t = 0.0f;
-            if (k < a.npx) {
-                const unsigned m = a.mask[k];
-                const uint2 b = a.px.bits[k];
-                const bool pres = (b.x >> j) & 1u;
-                if (m == (unsigned)i) {
-                    const float p = pres ? pj[k] : 0.0f;
-                    t = p == 0.0f ? c0 : glibc::logf(fmaxf(p / a.n_obs, a.eps));
-                } else if ((b.y >> j) & 1u) {
-                    const float p = pres ? pj[k] : 0.0f;
-                    t = glibc::logf(fmaxf(1.0f - p / a.n_obs, a.eps));
-                }
-            }
-            x[e] = t;
-            any |= t != 0.0f;
+            const bool in = k < a.npx;
+            m_n[e] = in ? a.mask[k] : 0u;
+            b_n[e] = in ? a.px.bits[k] : make_uint2(0u, 0u);
+            p_n[e] = in ? pj[k] : 0.0f;  // stale unless the bin is present: masked below
         }
-        if (!__syncthreads_or(any)) continue;
-        int pos = 0;  // chunk elements before pos are done
-        for (;;) {
-            const unsigned sb = glibc::f2u(s);
-            if (s == 0.0f || (sb >> 31) == 0u || ((sb >> 23) & 0xFFu) == 0u) {
-                // s == 0 (the first nonzero term is the sum), s > 0 or subnormal (not reached by
-                // same-sign terms of the association): one addition at a time
-                int f = kScanChunk;
+    };
+    load(0);
+    for (int base = 0; base < a.npx; base += kScanChunk) {
+        unsigned m[kScanPer];
+        float t1[kScanPer], t2[kScanPer];
+        bool box[kScanPer];
 #pragma unroll
-                for (int e = 0; e < kScanPer; ++e) {
-                    const int idx = tid * kScanPer + e;
-                    if (idx >= pos && x[e] != 0.0f && idx < f) f = idx;
-                }
-                f = wg_min(f, L);
-                if (f == kScanChunk) break;
-                if (f >= tid * kScanPer && f < (tid + 1) * kScanPer) {
-#pragma unroll
-                    for (int e = 0; e < kScanPer; ++e)
-                        if (tid * kScanPer + e == f) L.xv = x[e];
-                }
-                __syncthreads();
-                s = s + L.xv;
-                __syncthreads();
-                pos = f + 1;
-                continue;
-            }
-            const int uexp = (int)((sb >> 23) & 0xFFu) - 150;             // u = 2^uexp
-            const long long S0 = (long long)((sb & 0x7FFFFFu) | 0x800000u);  // |s| / u
-            long long r[kScanPer];
-            bool viol[kScanPer];
-            long long lsum = 0;
+        for (int e = 0; e < kScanPer; ++e) {
+            m[e] = m_n[e];
+            const bool pres = (b_n[e].x >> j) & 1u;
+            box[e] = (b_n[e].y >> j) & 1u;
+            const float p = pres ? p_n[e] : 0.0f;
+            // t1 for the pixel's own label (a flagged row), t2 for every other row (box bit j)
+            t1[e] = (m[e] < (unsigned)kMaxObjects && ((rows >> m[e]) & 1u))
+                        ? (p == 0.0f ? c0 : glibc::logf(fmaxf(p / a.n_obs, a.eps)))
+                        : 0.0f;
+            t2[e] = box[e] ? glibc::logf(fmaxf(1.0f - p / a.n_obs, a.eps)) : 0.0f;
+        }
+        if (base + kScanChunk < a.npx) load(base + kScanChunk);  // the next chunk, in flight meanwhile
+        for (unsigned rr = rows; rr; rr &= rr - 1u) {
+            const unsigned i = (unsigned)(__ffs((int)rr) - 1);
+            float x[kScanPer];
+            bool any = false;
 #pragma unroll
             for (int e = 0; e < kScanPer; ++e) {
-                const int idx = tid * kScanPer + e;
-                r[e] = 0;
-                viol[e] = false;
-                if (idx >= pos && x[e] != 0.0f) {
-                    if (x[e] > 0.0f) {
-                        viol[e] = true;
-                    } else {
-                        const double v = ldexp(-(double)x[e], -uexp);  // |x| / u, exact
-                        if (v >= 0x1p25) {
-                            r[e] = 1ll << 25;
-                            viol[e] = true;
-                        } else {
-                            const double fl = floor(v), fr = v - fl;
-                            r[e] = (long long)fl + (fr > 0.5 ? 1 : 0);
-                            viol[e] = fr == 0.5;
-                        }
-                    }
-                }
-                lsum += r[e];
+                x[e] = m[e] == i ? t1[e] : t2[e];
+                any |= x[e] != 0.0f;
             }
-            long long tot;
-            const long long ex = wg_exscan(lsum, L, &tot);
-            int f = kScanChunk;
-            long long run = ex;
-#pragma unroll
-            for (int e = 0; e < kScanPer; ++e) {
-                const int idx = tid * kScanPer + e;
-                run += r[e];
-                if ((viol[e] || S0 + run >= (1ll << 24)) && idx >= pos && idx < f) f = idx;
-            }
-            f = wg_min(f, L);
-            if (f == kScanChunk) {  // the rest of the chunk stays in this binade
-                s = -(float)ldexp((double)(S0 + tot), uexp);
-                break;
-            }
-            if (f >= tid * kScanPer && f < (tid + 1) * kScanPer) {
-                long long before = ex;
-#pragma unroll
-                for (int e = 0; e < kScanPer; ++e) {
-                    if (tid * kScanPer + e == f) L.xv = x[e];
-                    if (tid * kScanPer + e < f) before += r[e];
-                }
-                L.before = before;
-            }
+            if (!__syncthreads_or(any)) continue;
+            const float s = scan_chunk(s_rows[i], x, L);
+            __syncthreads();  // every lane has read s_rows[i]
+            if (tid == 0) s_rows[i] = s;
             __syncthreads();
-            s = -(float)ldexp((double)(S0 + L.before), uexp);  // exact: the steps before f
-            s = s + L.xv;                                        // step f as the f32 addition
-            __syncthreads();
-            pos = f + 1;
-            if (pos >= kScanChunk) break;
         }
     }
-    return s;
 }
 
 // Certified interval [lo, hi] of the reference's f32 exp(A/C) from the fixed-point sums, and
@@ -2772,6 +2827,7 @@ struct DecideLds {
     unsigned first[256];
     int newcount;
     ScanLds scan;
+    float srow[kMaxObjects];  // exact path: the running f32 sum of each flagged row
 };
 
 __global__ __launch_bounds__(256) void k_assoc_decide(DecideArgs a) {
@@ -2855,16 +2911,15 @@ __global__ __launch_bounds__(256) void k_assoc_decide(DecideArgs a) {
         return;
     }
     const bool have_px = a.px.bits != nullptr;
-    // ---- exact sums: column j = blockIdx.x of every flagged row ----
+    // ---- exact sums: column j = blockIdx.x of every flagged row, one pass over the pixels ----
     if (F && have_px && blockIdx.x >= 1) {
         const int j = (int)blockIdx.x;
         const float c0 = glibc::logf(fmaxf(0.0f, a.eps));
-        for (int i = 1; i < max_now; ++i) {
-            if (!((F >> i) & 1u)) continue;
-            const float A = exact_row_sum(i, j, a, c0, L.scan);
-            // write-through (sc1) store: the deciding workgroup may sit on another XCD
-            if (tid == 0) __hip_atomic_store(&a.X->A[i][j], A, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        const unsigned rows = F & (max_now >= 32 ? 0xFFFFFFFFu : ((1u << max_now) - 1u)) & ~1u;
+        exact_rows_sum(rows, j, a, c0, L.scan, L.srow);
+        // write-through (sc1) stores: the deciding workgroup may sit on another XCD
+        if (tid < kMaxObjects && ((rows >> tid) & 1u))
+            __hip_atomic_store(&a.X->A[tid][j], L.srow[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // ---- the last workgroup decides (in-launch hand-off: every storing wave drains its stores,
     // one release + counter ticket per workgroup, one acquire in the last arriver) ----

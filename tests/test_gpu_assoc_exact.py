@@ -397,3 +397,79 @@ def test_sharded_exact_path_equals_single_volume(S, oracle, nshards, chunk, exch
     for sh in shards:
         sh.close()
     vol.close()
+
+
+def test_sharded_pixel_export_equals_single_volume_probs(S, oracle):
+    """The shards' per-pixel association data, summed over the group (the exchange of the
+    sharded exact path), equals the single volume's probabilities and box bits at every pixel
+    (semtsdf_assoc_probs: the reference's back_proj_kernel output, tsdf.cu:72-135)."""
+    import ctypes as C
+
+    from semtsdf.shard import LocalShardGroup, _sum_int32_dev
+    from semtsdf.synth import SyntheticStream
+    from semtsdf.volume import DeviceBuffer
+
+    semtsdf, L = S
+    lib = L.load()
+    st = SyntheticStream(seed=0)
+    frames = [st.frame(k) for k in range(4)]
+    p = semtsdf.default_params(64, KI, 640, 480)
+    p.dim[0], p.dim[1], p.dim[2] = 48, 40, 64
+    semtsdf.place_from_frame(p, frames[0].depth, float(np.mean(frames[0].depth[frames[0].depth > 0])) / 5000.0,
+                             L.PLACE_SFM)
+    vol = semtsdf.Volume(p, 0)
+    shards = []
+    for sidx in range(2):
+        q = semtsdf.default_params(64, KI, 640, 480)
+        for fld in ("dim", "vol_start", "vol_end", "voxel", "K", "Kinv"):
+            getattr(q, fld)[:] = getattr(p, fld)[:]
+        q.mu, q.flags = p.mu, p.flags
+        q.z_nshards, q.z_shard, q.z_chunk = 2, sidx, 8
+        shards.append(semtsdf.Volume(q, 0))
+    grp = LocalShardGroup(shards, exchange="min")
+    npx = 640 * 480
+    dbuf, rbuf = DeviceBuffer(npx * 2), DeviceBuffer(npx * 3)
+    mbufs = [DeviceBuffer(npx) for _ in shards]
+    for k in range(1, 3):  # integrate two frames everywhere (no association)
+        fr = frames[k]
+        E = (fr.w2c @ frames[0].c2w).astype(np.float32)
+        vol.integrate(fr.depth, fr.rgb, np.ascontiguousarray(fr.mask), E)
+        dbuf.upload(fr.depth, grp.stream)
+        rbuf.upload(fr.rgb, grp.stream)
+        for sh, mb in zip(shards, mbufs):
+            mb.upload(fr.mask, grp.stream)
+            sh.integrate_dev(dbuf.ptr, rbuf.ptr, mb.ptr, E, grp.stream)
+            L.check(lib.semtsdf_shard_note_integrated(sh.handle, L.ptr(mb.ptr), L.ptr(grp.stream)))
+    vol.set_state(2, 8)
+    fr = frames[3]
+    E = (fr.w2c @ frames[0].c2w).astype(np.float32)
+    probs, box = vol.assoc_probs(E)
+    g = grp._protocol(L.RAY_ASSOC, E, None)
+    for sh, mb, pb in zip(shards, mbufs, grp.partial):
+        mb.upload(fr.mask, grp.stream)
+        L.check(lib.semtsdf_shard_assoc_partial(sh.handle, C.c_void_p(g), C.c_void_p(mb.ptr), C.c_void_p(pb.ptr),
+                                                grp._s()))
+    nw = npx * L.ASSOC_PIXEL_WORDS
+    parts = [DeviceBuffer(4 * nw) for _ in shards]
+    for sh, pb in zip(shards, parts):
+        L.check(lib.semtsdf_shard_assoc_pixels(sh.handle, C.c_void_p(g), C.c_void_p(pb.ptr), grp._s()))
+    px = DeviceBuffer(4 * nw)
+    _sum_int32_dev([pb.ptr for pb in parts], px.ptr, nw, grp.stream)
+    out = np.zeros(nw, np.int32)
+    px.download(out, grp.stream)
+    shards[0].sync()
+    bits = out[:2 * npx].view(np.uint32).reshape(npx, 2)
+    pl = out[2 * npx:].view(np.float32).reshape(32, npx)
+    pr = probs.reshape(npx, 32)
+    bx = box.reshape(npx, 32)
+    jbit = (1 << np.arange(32, dtype=np.uint64))
+    pres_ref = ((pr != 0) * jbit).sum(axis=1).astype(np.uint64) & ~np.uint64(1)
+    box_ref = ((bx != 0) * jbit).sum(axis=1).astype(np.uint64) & ~np.uint64(1)
+    assert np.array_equal(bits[:, 0].astype(np.uint64), pres_ref), int((bits[:, 0] != pres_ref).sum())
+    assert np.array_equal(bits[:, 1].astype(np.uint64), box_ref), int((bits[:, 1] != box_ref).sum())
+    m = pr[:, 1:] != 0
+    assert np.array_equal(pl[1:].T[m].view(np.uint32), pr[:, 1:][m].view(np.uint32))
+    assert m.sum() > 1000
+    for sh in shards:
+        sh.close()
+    vol.close()
