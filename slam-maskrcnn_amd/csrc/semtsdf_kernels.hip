@@ -2183,6 +2183,9 @@ struct MarchStats {
 #define SEMTSDF_MARCH_SPEC 5
 #endif
 constexpr int kMarchSpec = SEMTSDF_MARCH_SPEC;  // speculative samples per evaluated sample
+#ifndef SEMTSDF_MARCH_PRIO
+#define SEMTSDF_MARCH_PRIO 12u  // iterations after which a marching wave's priority rises (0: off)
+#endif
 
 template <bool OCT>
 __device__ bool march_ray(const VolGeom& g, const VolBufs& b, float ox, float oy, float oz, float dx, float dy,
@@ -2212,8 +2215,17 @@ __device__ bool march_ray(const VolGeom& g, const VolBufs& b, float ox, float oy
     // One memory access (a brick lookup or a sample) per iteration; in between, each lane
     // runs through the samples of its current skippable brick with arithmetic only, so the
     // lanes of a wave do not wait for each other's memory round trips sample by sample.
+    unsigned iters = 0;
     while (t < tfar) {
         if (st) st->iters++;
+        // a wave still marching after many iterations holds the kernel's tail: raise its
+        // issue priority (age arbitration would otherwise favour the older, shorter waves)
+        if (SEMTSDF_MARCH_PRIO) {
+            const unsigned wi = __builtin_amdgcn_readfirstlane(++iters);
+            if (wi == SEMTSDF_MARCH_PRIO) __builtin_amdgcn_s_setprio(1);
+            else if (wi == 2u * SEMTSDF_MARCH_PRIO) __builtin_amdgcn_s_setprio(2);
+            else if (wi == 4u * SEMTSDF_MARCH_PRIO) __builtin_amdgcn_s_setprio(3);
+        }
         if (box && cur.skip && in_skip_box(cur, rv, t)) {
             // the same additions as sample-by-sample stepping (the hit position depends on
             // them), tested against the box's exit parameter, then exactly near the exit
