@@ -309,6 +309,20 @@ int semtsdf_download_slab(semtsdf_vol* v, int x0, int x1, float* sdf, int32_t* w
 int semtsdf_upload(semtsdf_vol* v, const float* sdf, const int32_t* wt, const void* color,
                    const uint32_t* hist, const int32_t* cls, const int32_t* cls_cnt);
 
+/* ---- surface export (no reference counterpart) -------------------------
+ * Every stored voxel of this handle (a shard: its owned planes) with weight >= min_weight and
+ * |sdf| < sdf_max (sdf in the volume's normalised units, f = diff / mu), in the reference's flat
+ * order (x-major, z fastest; global indices), with its colour (int32 colours clamped to [0, 255])
+ * and instance label (the argmax of its histogram, first maximum; 0 without a count).  out may
+ * be NULL (count only); otherwise it receives min(count, capacity) points.  Synchronises. */
+typedef struct semtsdf_surface_point {
+    uint32_t x, y, z; /* voxel index; position = vol_start + index * voxel (tsdf.cu:30) */
+    float sdf;
+    uint8_t r, g, b, label;
+} semtsdf_surface_point;
+int semtsdf_export_surface(semtsdf_vol* v, float sdf_max, int32_t min_weight, semtsdf_surface_point* out,
+                           uint64_t capacity, uint64_t* count);
+
 /* ---- measurement ------------------------------------------------------------------------ */
 /* enable bit0: record HIP events around kernels; bit1: count touched/gated voxels; bit2: every
  * association row takes the exact f32 path (tests and its cost measurement). */

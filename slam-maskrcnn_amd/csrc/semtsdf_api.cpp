@@ -1847,6 +1847,53 @@ int semtsdf_upload(semtsdf_vol* v, const float* sdf, const int32_t* wt, const vo
     return SEMTSDF_OK;
 }
 
+int semtsdf_export_surface(semtsdf_vol* v, float sdf_max, int32_t min_weight, semtsdf_surface_point* out,
+                           uint64_t capacity, uint64_t* count) {
+    static_assert(sizeof(semtsdf_surface_point) == sizeof(SurfacePoint), "surface point layout");
+    if (!v || !count) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    if (!(sdf_max > 0.0f)) return fail(SEMTSDF_ERR_INVALID, "sdf_max must be > 0");
+    HIPC(hipSetDevice(v->device));
+    hipStream_t s = v->stream;
+    if (int rc = after_bmin(v, s)) return rc;
+    HIPC(launch_flush_lazy(v->g, v->b, s));  // pending weight increments (lazy-weight builds)
+    unsigned long long* cnt_d = nullptr;
+    HIPC(hipMalloc((void**)&cnt_d, sizeof(unsigned long long)));
+    SurfacePoint* pts_d = nullptr;
+    auto cleanup = [&]() {
+        if (cnt_d) (void)hipFree(cnt_d);
+        if (pts_d) (void)hipFree(pts_d);
+    };
+    auto run = [&](SurfacePoint* o, uint64_t cap, unsigned long long* n) -> hipError_t {
+        hipError_t e = hipMemsetAsync(cnt_d, 0, sizeof(unsigned long long), s);
+        if (e == hipSuccess) e = launch_export_surface(v->g, v->b, sdf_max, min_weight, v->color_wide ? 1 : 0,
+                                                       (v->p.flags & SEMTSDF_F_SEMANTIC) ? 1 : 0, o, cap, cnt_d, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(n, cnt_d, sizeof(*n), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        return e;
+    };
+    unsigned long long n = 0;
+    hipError_t e = run(nullptr, 0, &n);
+    if (e != hipSuccess) { cleanup(); return fail(SEMTSDF_ERR_HIP, "surface count: %s", hipGetErrorString(e)); }
+    *count = n;
+    if (!out || n == 0 || capacity == 0) { cleanup(); return SEMTSDF_OK; }
+    e = hipMalloc((void**)&pts_d, n * sizeof(SurfacePoint));
+    if (e != hipSuccess) { cleanup(); return fail(SEMTSDF_ERR_OOM, "surface export: %s", hipGetErrorString(e)); }
+    unsigned long long n2 = 0;
+    e = run(pts_d, n, &n2);
+    std::vector<SurfacePoint> h(n);
+    if (e == hipSuccess) e = hipMemcpy(h.data(), pts_d, n * sizeof(SurfacePoint), hipMemcpyDeviceToHost);
+    cleanup();
+    if (e != hipSuccess) return fail(SEMTSDF_ERR_HIP, "surface export: %s", hipGetErrorString(e));
+    if (n2 != n) return fail(SEMTSDF_ERR_STATE, "surface export: count changed (%llu, %llu)", n, n2);
+    // the reference's flat order (x-major, z fastest)
+    std::sort(h.begin(), h.end(), [](const SurfacePoint& a, const SurfacePoint& b) {
+        return a.x != b.x ? a.x < b.x : a.y != b.y ? a.y < b.y : a.z < b.z;
+    });
+    const uint64_t m = n < capacity ? n : capacity;
+    memcpy(out, h.data(), m * sizeof(SurfacePoint));
+    return SEMTSDF_OK;
+}
+
 int semtsdf_set_instrumentation(semtsdf_vol* v, int enable) {
     if (!v) return fail(SEMTSDF_ERR_INVALID, "NULL handle");
     v->instr = enable;

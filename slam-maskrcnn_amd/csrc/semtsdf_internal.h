@@ -331,5 +331,12 @@ hipError_t launch_hist_chunk_to_vm(const uint32_t* bm, uint32_t* vm, const VolGe
 hipError_t launch_hist_chunk_to_bm(const uint32_t* vm, uint32_t* bm, const VolGeom& g, uint64_t v0, uint64_t nv,
                                    hipStream_t s);
 hipError_t launch_hist_mask(const VolGeom& g, const VolBufs& b, hipStream_t s);  // hmask from hist
+struct SurfacePoint {  // one exported surface voxel (semtsdf_surface_point)
+    uint32_t x, y, z;  // global voxel index
+    float sdf;
+    uint32_t rgbl;     // r | g << 8 | b << 16 | label << 24
+};
+hipError_t launch_export_surface(const VolGeom& g, const VolBufs& b, float sdf_max, int min_w, int color_wide,
+                                 int semantic, SurfacePoint* out, uint64_t cap, unsigned long long* count, hipStream_t s);
 
 }  // namespace semtsdf

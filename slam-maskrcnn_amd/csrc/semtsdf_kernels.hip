@@ -4107,4 +4107,67 @@ hipError_t launch_masks_to_labels(const uint8_t* masks, int npx, int n, int min_
 size_t mask_scratch_bytes() { return sizeof(MaskScratch); }
 size_t mask_scratch_kept_offset() { return offsetof(MaskScratch, n_kept); }
 
+
+
+// ------------------------------------------------------------------------------------
+// Surface export (optional in the reference: the volume layout of
+// src/TSDF_Python/tsdf.py:48-52): every stored, owned voxel with weight >= min_w and |sdf| <
+// sdf_max, with its colour and instance label (the argmax of its histogram, first maximum,
+// as the label render's viewer.cu:66-79 rule applied to the voxel itself; 0 when empty).
+// Unordered appends (the host sorts by the reference index); a counting pass when out is null.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_export_surface(VolGeom g, VolBufs b, float sdf_max, int min_w, int color_wide,
+                                                        int semantic, SurfacePoint* __restrict__ out, uint64_t cap,
+                                                        unsigned long long* __restrict__ count) {
+    const uint64_t n = (uint64_t)g.dimx * (uint64_t)g.dimy * (uint64_t)g.lz;
+    for (uint64_t v = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t row = v / (uint64_t)g.lz;
+        const int l = (int)(v - row * (uint64_t)g.lz);
+        const int x = (int)(row / (uint64_t)g.dimy), y = (int)(row - (uint64_t)x * g.dimy);
+        if (g.nshards > 1 && (l % (g.chunk + g.halo)) >= g.chunk) continue;  // halo plane: its owner exports it
+        const int gz = local_to_global_z(g, l);
+        if (gz >= g.dimz) continue;
+        const uint32_t t = tile_index(g, x, y, l);
+        const int w = b.wt[t];
+        const float s = b.sdf[t];
+        if (w < min_w || !(fabsf(s) < sdf_max)) continue;
+        unsigned r, gg, bb;
+        if (color_wide) {
+            const int4 c = reinterpret_cast<const int4*>(b.color)[t];
+            r = (unsigned)min(max(c.x, 0), 255); gg = (unsigned)min(max(c.y, 0), 255); bb = (unsigned)min(max(c.z, 0), 255);
+        } else {
+            const unsigned c = reinterpret_cast<const uint32_t*>(b.color)[t];
+            r = c & 0xFFu; gg = (c >> 8) & 0xFFu; bb = (c >> 16) & 0xFFu;
+        }
+        unsigned lab = 0, best = 0;
+        if (semantic) {
+            unsigned bins = b.hmask[t];
+            while (bins) {
+                const int k = __ffs((int)bins) - 1;
+                bins &= bins - 1u;
+                const unsigned c = b.hist[(uint64_t)k * g.nvox + t];
+                if (c > best) { best = c; lab = (unsigned)k; }
+            }
+        }
+        const unsigned long long i = atomicAdd(count, 1ull);
+        if (out && i < cap) {
+            SurfacePoint p;
+            p.x = (uint32_t)x; p.y = (uint32_t)y; p.z = (uint32_t)gz;
+            p.sdf = s;
+            p.rgbl = r | (gg << 8) | (bb << 16) | (lab << 24);
+            out[i] = p;
+        }
+    }
+}
+
+hipError_t launch_export_surface(const VolGeom& g, const VolBufs& b, float sdf_max, int min_w, int color_wide,
+                                 int semantic, SurfacePoint* out, uint64_t cap, unsigned long long* count, hipStream_t s) {
+    const uint64_t n = (uint64_t)g.dimx * g.dimy * g.lz;
+    if (n == 0) return hipSuccess;
+    const uint64_t blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(k_export_surface, dim3((unsigned)(blocks < 65536 ? blocks : 65536)), dim3(256), 0, s, g, b, sdf_max,
+                       min_w, color_wide, semantic, out, cap, count);
+    return hipGetLastError();
+}
+
 }  // namespace semtsdf

@@ -97,6 +97,11 @@ class AssocStats(C.Structure):
     ]
 
 
+class SurfacePoint(C.Structure):
+    _fields_ = [("x", C.c_uint32), ("y", C.c_uint32), ("z", C.c_uint32), ("sdf", C.c_float),
+                ("r", C.c_uint8), ("g", C.c_uint8), ("b", C.c_uint8), ("label", C.c_uint8)]
+
+
 class Timing(C.Structure):
     _fields_ = [
         ("integrate_ms", C.c_double),
@@ -176,6 +181,7 @@ SIGNATURES = {
     "semtsdf_download": (_I, [_P, _P, _P, _P, _P, _P, _P]),
     "semtsdf_download_slab": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P]),
     "semtsdf_upload": (_I, [_P, _P, _P, _P, _P, _P, _P]),
+    "semtsdf_export_surface": (_I, [_P, _F, C.c_int32, _P, C.c_uint64, C.POINTER(C.c_uint64)]),
     "semtsdf_set_instrumentation": (_I, [_P, _I]),
     "semtsdf_get_timing": (_I, [_P, C.POINTER(Timing)]),
     "semtsdf_reset_timing": (_I, [_P]),
