@@ -2184,7 +2184,7 @@ struct MarchStats {
 #endif
 constexpr int kMarchSpec = SEMTSDF_MARCH_SPEC;  // speculative samples per evaluated sample
 #ifndef SEMTSDF_MARCH_PRIO
-#define SEMTSDF_MARCH_PRIO 12u  // iterations after which a marching wave's priority rises (0: off)
+#define SEMTSDF_MARCH_PRIO 0u  // iterations after which a marching wave's priority rises (0: off; 8-20 measured 0.5-1.5 % slower, profiles/r04/ab_march_priority.txt)
 #endif
 
 template <bool OCT>
