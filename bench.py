@@ -649,6 +649,11 @@ def run_c2(semtsdf, L, local, frames, f0, K=30, warmup=3, traffic_json=None):
     dbuf.free()
     rbuf.free()
     c2_traffic, c2_src = read_traffic(traffic_json, D, 1)
+    # line-granular floor of the state traffic: every 128-B line holding a touched voxel is read
+    # and written whole in each of the three state arrays (sdf, weight, colour u8x4), plus the
+    # 8-B pixel records read once
+    lines = tc.touched_lines / K
+    floor = 128.0 * 6 * lines + 8.0 * NPX
     return {
         "workload": "C2: 256^3 TSDF + colour (sdf f32, weight i32, colour i32x3, NumPy rule: colour ungated), "
                     "synthetic 640x480 stream, ground-truth poses",
@@ -663,6 +668,11 @@ def run_c2(semtsdf, L, local, frames, f0, K=30, warmup=3, traffic_json=None):
                      "traffic": c2_traffic, "traffic_source": c2_src,
                      "algorithmic_bytes_per_launch": int(b), "bytes_rule": "22 N_touch + 5 W H (SURVEY §8d)"},
         "touched_mvox_per_s": round(touched / (kern_ms * 1e-3) / 1e6, 1),
+        "touched_lines_per_frame": int(lines),
+        "line_floor_bytes_per_launch": int(floor),
+        "line_floor_rule": "128 B x 3 arrays (sdf, weight, colour u8x4) x read+write per 128-B sdf line holding a "
+                           "touched voxel (tiles of 8 y x 4 z voxels) + 8 B pixel record per pixel",
+        "traffic_over_line_floor": round(c2_traffic / floor, 3) if c2_traffic else None,
     }
 
 
@@ -1024,6 +1034,7 @@ def main():
         "full_free_units_per_frame": int(full_units),
         "lazy_weight_voxels_per_frame": int(lazy),
         "touched_mvox_per_s": round(touched / (kern_ms * 1e-3) / 1e6, 1),
+        "touched_lines_per_frame": int(tc.touched_lines / args.steps),
         "roofline": {
             "bound": "hbm",
             "achieved": round(achieved, 1),

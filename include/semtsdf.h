@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SEMTSDF_ABI_VERSION 9
+#define SEMTSDF_ABI_VERSION 10
 #define SEMTSDF_MAX_OBJECTS 32 /* tsdf.cuh:4 */
 
 /* ---- status codes ------------------------------------------------------------ */
@@ -120,6 +120,8 @@ typedef struct semtsdf_timing {
                              instead of a weight store (count mode only) */
     uint64_t assoc_exact_frames; /* association decisions that took the exact f32 path (always counted) */
     uint64_t assoc_exact_rows;   /* rows decided on it, summed over those decisions */
+    uint64_t touched_lines;      /* 128-B lines of the sdf array (8 y x 4 z voxels of a tile) holding a
+                                    touched voxel: the line-granular floor of the state traffic (count mode only) */
 } semtsdf_timing;
 
 /* ---- library ------------------------------------------------------------------------ */
@@ -323,9 +325,16 @@ typedef struct semtsdf_surface_point {
 int semtsdf_export_surface(semtsdf_vol* v, float sdf_max, int32_t min_weight, semtsdf_surface_point* out,
                            uint64_t capacity, uint64_t* count);
 
+/* ---- empty-space maps (tests) ------------------------------------------------------------
+ * The octant distance map of the current volume state, one word per 8^3 brick (x-major, z
+ * fastest): byte o = the octant-o distance in bricks (0: the brick is not skippable).  count =
+ * the number of bricks (0: the handle has no octant maps); out may be NULL.  Synchronises. */
+int semtsdf_map_words(semtsdf_vol* v, uint64_t* out, uint64_t capacity, uint64_t* count);
+
 /* ---- measurement ------------------------------------------------------------------------ */
 /* enable bit0: record HIP events around kernels; bit1: count touched/gated voxels; bit2: every
- * association row takes the exact f32 path (tests and its cost measurement). */
+ * association row takes the exact f32 path (tests and its cost measurement); bit3: the octant
+ * maps by the global-memory passes instead of the LDS line passes (tests: same maps). */
 int semtsdf_set_instrumentation(semtsdf_vol* v, int enable);
 int semtsdf_get_timing(semtsdf_vol* v, semtsdf_timing* out); /* synchronises the stream */
 int semtsdf_reset_timing(semtsdf_vol* v);

@@ -25,6 +25,13 @@
 
 using namespace semtsdf;
 
+#ifndef SEMTSDF_EVENT_FLAGS_DEFAULT
+#define SEMTSDF_EVENT_FLAGS_DEFAULT 0  // order_event_flags(): 0 system-scope release, 1 device scope (A/B)
+#endif
+#ifndef SEMTSDF_MARCH_LPT_DEFAULT
+#define SEMTSDF_MARCH_LPT_DEFAULT 1  // env SEMTSDF_MARCH_LPT=0/1 overrides (A/B)
+#endif
+
 namespace {
 
 thread_local std::string g_err;
@@ -129,6 +136,11 @@ struct semtsdf_vol {
                                    // is left before a colour mean could take the int32 wrap (w >= 2^23)
     const uint8_t* pending_lut = nullptr;  // relabel table the next integrate's prepass applies
     unsigned long long* wtrace_d = nullptr;  // instrumentation: per-wave trace slots (kWtSlots, allocated once)
+    // launch order of the fused view + association march (AssocArgs::tile_*): per-tile durations
+    // of the last launch and the order the decision computed from them for tile_n tiles
+    unsigned* tile_cost_d = nullptr;
+    unsigned* tile_perm_d = nullptr;
+    int tile_cap = 0, tile_n = 0;
     bool tables_clean = false;     // tables_d holds the cleared state (left by k_assoc_decide)
     // instrumentation
     int instr = 0;
@@ -138,6 +150,15 @@ struct semtsdf_vol {
 };
 
 namespace {
+
+// Flags of the events that order this device's own streams (prepass, map update, frame sets):
+// no timing and, by default, a device-scope release (the consumers are kernels of the same
+// device, never the host).  SEMTSDF_EVENT_FLAGS=0 selects the default system-scope release.
+unsigned order_event_flags() {
+    static const char* e = getenv("SEMTSDF_EVENT_FLAGS");
+    static const int mode = e ? atoi(e) : SEMTSDF_EVENT_FLAGS_DEFAULT;
+    return hipEventDisableTiming | (mode == 1 ? hipEventReleaseToDevice : 0u) | (mode == 2 ? hipEventDisableSystemFence : 0u);
+}
 
 size_t npx(const semtsdf_vol* v) { return (size_t)v->p.width * (size_t)v->p.height; }
 
@@ -159,7 +180,7 @@ void free_all(semtsdf_vol* v) {
                     v->fs[1].pyr.l0, v->fs[1].pyr.l1, v->tables_d, v->decision_d,
                     v->num_objs_d, v->probs_d, v->box_d, v->palette_d, v->render_d, v->render_t_d,
                     v->counters_d, v->ray_state_d, v->fs[0].unit_list, v->fs[0].list_count, v->fs[1].unit_list,
-                    v->fs[1].list_count, v->rcp_table_d, v->wtrace_d, v->exact_d, v->px.bits, v->px.p};
+                    v->fs[1].list_count, v->rcp_table_d, v->wtrace_d, v->exact_d, v->px.bits, v->px.p, v->tile_cost_d, v->tile_perm_d};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (v->decision_h) (void)hipHostFree(v->decision_h);
@@ -193,7 +214,7 @@ int check_params(const semtsdf_params* p) {
                         p->dim[1], p->dim[2]);
     }
     if (!(p->mu > 0.0f)) return fail(SEMTSDF_ERR_INVALID, "mu=%g must be > 0", p->mu);
-    if (p->width <= 0 || p->height <= 0 || (int64_t)p->width * p->height > (1 << 28))
+    if (p->width <= 0 || p->height <= 0 || p->width > 65535 || p->height > 65535 || (int64_t)p->width * p->height > (1 << 28))
         return fail(SEMTSDF_ERR_INVALID, "bad frame size %dx%d", p->width, p->height);
     if (!(p->depth_scale > 0.0f)) return fail(SEMTSDF_ERR_INVALID, "depth_scale must be > 0");
     if ((p->flags & SEMTSDF_F_VOTE) && (p->flags & SEMTSDF_F_SEMANTIC))
@@ -310,8 +331,8 @@ int ensure_prep_stream(semtsdf_vol* v) {
     if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
     HIPC(hipStreamCreateWithPriority(&v->prep_stream, hipStreamNonBlocking, hi));
     for (auto& f : v->fs) {
-        HIPC(hipEventCreateWithFlags(&f.prep_done, hipEventDisableTiming));
-        HIPC(hipEventCreateWithFlags(&f.set_free, hipEventDisableTiming));
+        HIPC(hipEventCreateWithFlags(&f.prep_done, order_event_flags()));
+        HIPC(hipEventCreateWithFlags(&f.set_free, order_event_flags()));
     }
     return SEMTSDF_OK;
 }
@@ -488,7 +509,7 @@ int order_after_map(semtsdf_vol* v, hipStream_t s) {
     if (!v->map_set || v->map_stream == s) return SEMTSDF_OK;
     v->multi_stream = true;
     if (!v->bmin_ev_set) {
-        if (!v->bmin_ev) HIPC(hipEventCreateWithFlags(&v->bmin_ev, hipEventDisableTiming));
+        if (!v->bmin_ev) HIPC(hipEventCreateWithFlags(&v->bmin_ev, order_event_flags()));
         HIPC(hipEventRecord(v->bmin_ev, v->map_stream));  // everything queued there so far
         v->bmin_ev_set = true;
     }
@@ -504,14 +525,15 @@ int ensure_bmin(semtsdf_vol* v, hipStream_t s) {
     if (int rc = order_after_map(v, s)) return rc;
     if (!v->bmin_dirty && !v->bmin_stale) return SEMTSDF_OK;
     // stale (reset/upload): every brick; dirty (integrate): the bricks the cull marked
-    HIPC(launch_brick_min(v->g, v->b, v->bmin_stale, s));
+    static const char* mg = getenv("SEMTSDF_MAP_GLOBAL");  // A/B: the global-memory map passes
+    HIPC(launch_brick_min(v->g, v->b, v->bmin_stale, s, (v->instr & 8) != 0 || (mg && atoi(mg) != 0)));
     v->map_stream = s;
     v->map_set = true;
     v->bmin_ev_set = false;
     // on a stream other than the volume's own, record now: that stream may be gone (a
     // caller's temporary render stream) by the time another stream needs the ordering
     if (v->multi_stream || s != v->stream) {
-        if (!v->bmin_ev) HIPC(hipEventCreateWithFlags(&v->bmin_ev, hipEventDisableTiming));
+        if (!v->bmin_ev) HIPC(hipEventCreateWithFlags(&v->bmin_ev, order_event_flags()));
         HIPC(hipEventRecord(v->bmin_ev, s));
         v->bmin_ev_set = true;
     }
@@ -579,15 +601,41 @@ int associate_impl(semtsdf_vol* v, uint8_t* mask_d, const float E[16], hipStream
         static const char* dbg = getenv("SEMTSDF_DEBUG_ASSOC");  // timing probes only
         a.debug = dbg ? atoi(dbg) : 0;
     }
+    int order_n = 0;  // the decision orders the fused march's next launch (largest tiles first)
     if (view) {
         RenderArgs r = *view;
         r.b = v->b;  // the map buffers as ensure_bmin left them
+        static const char* lpt = getenv("SEMTSDF_MARCH_LPT");
+        if (lpt ? atoi(lpt) != 0 : SEMTSDF_MARCH_LPT_DEFAULT) {
+            const int n = ((a.width + 15) / 16) * ((a.height + 15) / 16) + ((r.width + 15) / 16) * ((r.height + 15) / 16);
+            if (n > v->tile_cap) {
+                for (unsigned** q : {&v->tile_cost_d, &v->tile_perm_d})
+                    if (*q) { (void)hipFree(*q); v->device_bytes -= (size_t)v->tile_cap * sizeof(unsigned); *q = nullptr; }
+                v->tile_cap = 0;
+                v->tile_n = 0;
+                if (int rc = dev_alloc(v, (void**)&v->tile_cost_d, (size_t)n * sizeof(unsigned))) return rc;
+                if (int rc = dev_alloc(v, (void**)&v->tile_perm_d, (size_t)n * sizeof(unsigned))) return rc;
+                v->tile_cap = n;
+            }
+            a.tile_cost = v->tile_cost_d;
+            a.tile_perm = v->tile_n == n ? v->tile_perm_d : nullptr;  // sizes changed: identity
+            order_n = n;
+        }
         HIPC(launch_march_fused(a, r, s));
         v->n_render++;
     } else {
         HIPC(launch_assoc_march(a, s));
     }
-    HIPC(launch_assoc_decide(decide_args(v, mask_d, v->px), s));
+    {
+        DecideArgs d = decide_args(v, mask_d, v->px);
+        if (order_n) {
+            d.tile_cost = v->tile_cost_d;
+            d.tile_perm = v->tile_perm_d;
+            d.tile_n = order_n;
+            v->tile_n = order_n;
+        }
+        HIPC(launch_assoc_decide(d, s));
+    }
     v->tables_clean = true;  // the decide kernel clears them
     if (defer_relabel)
         v->pending_lut = &v->decision_d->lut[0];
@@ -921,8 +969,17 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
         const size_t nrec = (size_t)pyr.zero + 1;
         if ((rc = dev_alloc(v, (void**)&pyr.px, nrec * 8))) return bail(rc);
         if (hipMemset(pyr.px, 0, nrec * 8) != hipSuccess) return bail(fail(SEMTSDF_ERR_HIP, "memset failed"));
-        if ((rc = dev_alloc(v, (void**)&pyr.l0, (size_t)pyr.w1 * 4 * pyr.h1 * 4 * sizeof(uint2)))) return bail(rc);
-        if ((rc = dev_alloc(v, (void**)&pyr.l1, (size_t)pyr.w1 * pyr.h1 * sizeof(uint2)))) return bail(rc);
+        pyr.p0 = (pyr.w0 + 4 + 3) & ~3;
+        pyr.p1 = (pyr.w1 + 4 + 3) & ~3;
+        {  // depth words (padded rows, padding zero) then zero flags, per level
+            const size_t n0 = (size_t)pyr.h0 * (pyr.p0 + pyr.w0), n1 = (size_t)pyr.h1 * (pyr.p1 + pyr.w1);
+            if ((rc = dev_alloc(v, (void**)&pyr.l0, n0 * sizeof(unsigned)))) return bail(rc);
+            if ((rc = dev_alloc(v, (void**)&pyr.l1, n1 * sizeof(unsigned)))) return bail(rc);
+            if (hipMemset(pyr.l0, 0, n0 * sizeof(unsigned)) != hipSuccess || hipMemset(pyr.l1, 0, n1 * sizeof(unsigned)) != hipSuccess)
+                return bail(fail(SEMTSDF_ERR_HIP, "memset failed"));
+            pyr.z0 = pyr.l0 + (size_t)pyr.h0 * pyr.p0;
+            pyr.z1 = pyr.l1 + (size_t)pyr.h1 * pyr.p1;
+        }
         if ((rc = dev_alloc(v, (void**)&f.unit_list, unit_list_capacity(g) * sizeof(unsigned)))) return bail(rc);
         if ((rc = dev_alloc(v, (void**)&f.list_count, kLists * kListSegs * kListCountStride * sizeof(unsigned))))
             return bail(rc);
@@ -1245,7 +1302,7 @@ static int parse_frame_dev_impl(semtsdf_vol* v, const uint16_t* depth_d, const u
     // launch, 2.45 -> 2.20 k frames/s same-box, profiles/r03/s2/ab_pipeline_mask_stats.txt)
     const bool overlap_prep = SEMTSDF_OVERLAP_PREP && sem && v->n_obs > 0 && !integrate_after_event;
     if (overlap_prep) {
-        if (!v->in_ev) HIPC(hipEventCreateWithFlags(&v->in_ev, hipEventDisableTiming));
+        if (!v->in_ev) HIPC(hipEventCreateWithFlags(&v->in_ev, order_event_flags()));
         HIPC(hipEventRecord(v->in_ev, s));
     }
     if (sem) {
@@ -1847,6 +1904,20 @@ int semtsdf_upload(semtsdf_vol* v, const float* sdf, const int32_t* wt, const vo
     return SEMTSDF_OK;
 }
 
+int semtsdf_map_words(semtsdf_vol* v, uint64_t* out, uint64_t capacity, uint64_t* count) {
+    if (!v || !count) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
+    HIPC(hipSetDevice(v->device));
+    hipStream_t s = v->stream;
+    const bool dist = v->b.bdist && v->b.boct && v->b.botmp;
+    *count = dist ? (uint64_t)v->g.nbx * v->g.nby * v->g.nbz : 0u;
+    if (!dist) return SEMTSDF_OK;
+    if (int rc = ensure_bmin(v, s)) return rc;  // the maps of the current state
+    const uint64_t n = std::min<uint64_t>(capacity, *count);
+    if (out && n) HIPC(hipMemcpyAsync(out, v->b.boct, n * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    return SEMTSDF_OK;
+}
+
 int semtsdf_export_surface(semtsdf_vol* v, float sdf_max, int32_t min_weight, semtsdf_surface_point* out,
                            uint64_t capacity, uint64_t* count) {
     static_assert(sizeof(semtsdf_surface_point) == sizeof(SurfacePoint), "surface point layout");
@@ -1935,6 +2006,7 @@ int semtsdf_get_timing(semtsdf_vol* v, semtsdf_timing* out) {
     out->free_units = c[4];
     out->full_units = c[5];
     out->lazy_voxels = c[6];
+    out->touched_lines = c[7];
     unsigned xr[2] = {0, 0};  // AssocExact::frames, rows
     HIPC(hipMemcpy(xr, &v->exact_d->frames, sizeof(xr), hipMemcpyDeviceToHost));
     out->assoc_exact_frames = xr[0];

@@ -120,6 +120,7 @@ class Timing(C.Structure):
         ("lazy_voxels", C.c_uint64),
         ("assoc_exact_frames", C.c_uint64),
         ("assoc_exact_rows", C.c_uint64),
+        ("touched_lines", C.c_uint64),
     ]
 
 
@@ -182,6 +183,7 @@ SIGNATURES = {
     "semtsdf_download_slab": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P]),
     "semtsdf_upload": (_I, [_P, _P, _P, _P, _P, _P, _P]),
     "semtsdf_export_surface": (_I, [_P, _F, C.c_int32, _P, C.c_uint64, C.POINTER(C.c_uint64)]),
+    "semtsdf_map_words": (_I, [_P, _P, C.c_uint64, C.POINTER(C.c_uint64)]),
     "semtsdf_set_instrumentation": (_I, [_P, _I]),
     "semtsdf_get_timing": (_I, [_P, C.POINTER(Timing)]),
     "semtsdf_reset_timing": (_I, [_P]),

@@ -280,11 +280,25 @@ class Volume:
         L.check(L.load().semtsdf_upload(self._h, *[L.ptr(a) for a in arrs]))
 
     # ---- instrumentation
-    def set_instrumentation(self, events: bool = True, count: bool = False, force_exact: bool = False):
+    def set_instrumentation(self, events: bool = True, count: bool = False, force_exact: bool = False,
+                            global_map_passes: bool = False):
         """events: HIP-event kernel timing; count: touched/gated voxel counters; force_exact: every
-        association row decided from its exact f32 pixel-order sums (tests, cost measurement)."""
-        flags = (1 if events else 0) | (2 if count else 0) | (4 if force_exact else 0)
+        association row decided from its exact f32 pixel-order sums (tests, cost measurement);
+        global_map_passes: the octant maps by the global-memory passes (tests: same maps)."""
+        flags = (1 if events else 0) | (2 if count else 0) | (4 if force_exact else 0) | (8 if global_map_passes else 0)
         L.check(L.load().semtsdf_set_instrumentation(self._h, flags))
+
+    def map_words(self):
+        """The octant distance map of the current state (numpy uint64 per 8^3 brick, x-major, z
+        fastest; byte o = octant o's distance in bricks), or None without octant maps."""
+        import numpy as np
+        n = C.c_uint64(0)
+        L.check(L.load().semtsdf_map_words(self._h, None, 0, C.byref(n)))
+        if n.value == 0:
+            return None
+        out = np.zeros(n.value, dtype=np.uint64)
+        L.check(L.load().semtsdf_map_words(self._h, C.c_void_p(out.ctypes.data), n.value, C.byref(n)))
+        return out
 
     def filter_overlaps_dev(self, probs_ptr: int, box_ptr: int, mask_ptr: int, stream=None) -> L.AssocStats:
         """TSDF::filter_overlaps (tsdf.cu:304-416) on device arrays: probs f32 [H*W][32], box u8

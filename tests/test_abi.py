@@ -27,7 +27,7 @@ def test_library_exports_every_symbol():
     lib = L.load()
     for n in declared():
         assert hasattr(lib, n), n
-    assert lib.semtsdf_abi_version() == 9
+    assert lib.semtsdf_abi_version() == 10
     key = lib.semtsdf_build_key().decode()
     assert len(key) == 64 and int(key, 16) >= 0  # the sha-256 build key (__graft_entry__.build_key)
 
@@ -41,7 +41,7 @@ def test_structs_match_header_sizes():
     assert C.sizeof(L.Params) == 4 * (3 + 9 + 1 + 32 + 2 + 5 + 1 + 3)
     assert C.sizeof(L.AssocStats) == 4 * (2 + 32 + 32) + 256 + 4
     # semtsdf_timing: 16 fields of 8 bytes (doubles or u64)
-    assert C.sizeof(L.Timing) == 8 * 16
+    assert C.sizeof(L.Timing) == 8 * 17
 
 
 def test_argument_errors_without_a_device():
