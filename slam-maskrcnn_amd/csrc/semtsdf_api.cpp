@@ -26,7 +26,7 @@
 using namespace semtsdf;
 
 #ifndef SEMTSDF_EVENT_FLAGS_DEFAULT
-#define SEMTSDF_EVENT_FLAGS_DEFAULT 0  // order_event_flags(): 0 system-scope release, 1 device scope (A/B)
+#define SEMTSDF_EVENT_FLAGS_DEFAULT 2  // order_event_flags(): 0 system-scope release, 1 device-scope release, 2 no system fence
 #endif
 #ifndef SEMTSDF_MARCH_LPT_DEFAULT
 #define SEMTSDF_MARCH_LPT_DEFAULT 1  // env SEMTSDF_MARCH_LPT=0/1 overrides (A/B)
@@ -525,8 +525,12 @@ int ensure_bmin(semtsdf_vol* v, hipStream_t s) {
     if (int rc = order_after_map(v, s)) return rc;
     if (!v->bmin_dirty && !v->bmin_stale) return SEMTSDF_OK;
     // stale (reset/upload): every brick; dirty (integrate): the bricks the cull marked
-    static const char* mg = getenv("SEMTSDF_MAP_GLOBAL");  // A/B: the global-memory map passes
-    HIPC(launch_brick_min(v->g, v->b, v->bmin_stale, s, (v->instr & 8) != 0 || (mg && atoi(mg) != 0)));
+    // the octant maps by the global-memory passes (default) or the LDS line passes (same maps,
+    // measured no faster: profiles/r04/ab_map_passes_pipeline.txt); env SEMTSDF_MAP_GLOBAL=0/1
+    // chooses, instrumentation bit 3 takes the other one (tests)
+    static const char* mg = getenv("SEMTSDF_MAP_GLOBAL");
+    static const bool global_default = mg ? atoi(mg) != 0 : true;
+    HIPC(launch_brick_min(v->g, v->b, v->bmin_stale, s, global_default != ((v->instr & 8) != 0)));
     v->map_stream = s;
     v->map_set = true;
     v->bmin_ev_set = false;
@@ -969,17 +973,8 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
         const size_t nrec = (size_t)pyr.zero + 1;
         if ((rc = dev_alloc(v, (void**)&pyr.px, nrec * 8))) return bail(rc);
         if (hipMemset(pyr.px, 0, nrec * 8) != hipSuccess) return bail(fail(SEMTSDF_ERR_HIP, "memset failed"));
-        pyr.p0 = (pyr.w0 + 4 + 3) & ~3;
-        pyr.p1 = (pyr.w1 + 4 + 3) & ~3;
-        {  // depth words (padded rows, padding zero) then zero flags, per level
-            const size_t n0 = (size_t)pyr.h0 * (pyr.p0 + pyr.w0), n1 = (size_t)pyr.h1 * (pyr.p1 + pyr.w1);
-            if ((rc = dev_alloc(v, (void**)&pyr.l0, n0 * sizeof(unsigned)))) return bail(rc);
-            if ((rc = dev_alloc(v, (void**)&pyr.l1, n1 * sizeof(unsigned)))) return bail(rc);
-            if (hipMemset(pyr.l0, 0, n0 * sizeof(unsigned)) != hipSuccess || hipMemset(pyr.l1, 0, n1 * sizeof(unsigned)) != hipSuccess)
-                return bail(fail(SEMTSDF_ERR_HIP, "memset failed"));
-            pyr.z0 = pyr.l0 + (size_t)pyr.h0 * pyr.p0;
-            pyr.z1 = pyr.l1 + (size_t)pyr.h1 * pyr.p1;
-        }
+        if ((rc = dev_alloc(v, (void**)&pyr.l0, (size_t)pyr.w1 * 4 * pyr.h1 * 4 * sizeof(uint2)))) return bail(rc);
+        if ((rc = dev_alloc(v, (void**)&pyr.l1, (size_t)pyr.w1 * pyr.h1 * sizeof(uint2)))) return bail(rc);
         if ((rc = dev_alloc(v, (void**)&f.unit_list, unit_list_capacity(g) * sizeof(unsigned)))) return bail(rc);
         if ((rc = dev_alloc(v, (void**)&f.list_count, kLists * kListSegs * kListCountStride * sizeof(unsigned))))
             return bail(rc);

@@ -91,17 +91,9 @@ struct DepthPyramid {
                     // in 4 x 4-pixel tiles of one 128-B line each (rec_index): the voxels of a
                     // unit project onto a compact patch of the image, which then spans few lines;
                     // record `zero` (after the tiles) is zero: the target of off-image voxels
-    // Tile levels for the unit cull, 8- and 32-pixel tiles: depth words l (max raw depth |
-    // (0xFFFF - min nonzero raw depth) << 16) in rows of pitch p >= w + 4, so that a row of 4
-    // consecutive tiles is one 16-byte load (the cull's footprints span <= 4 x 4 tiles), and the
-    // zero flags z (1 if a pixel of the tile has depth 0) in rows of w; z points into the
-    // allocation of l, after its h rows.
-    unsigned* l0;
-    unsigned* z0;
-    unsigned* l1;
-    unsigned* z1;
+    uint2* l0;  // [ceil(H/8)][ceil(W/8)]  {max | (0xFFFF - min nonzero) << 16, 1 if a pixel has depth 0}
+    uint2* l1;  // [ceil(H/32)][ceil(W/32)]
     int w0, h0, w1, h1;
-    int p0, p1;
     int tw;         // 4-pixel tiles per image row: ceil(W / 4)
     unsigned zero;  // index of the zero record: ceil(W / 4) * ceil(H / 4) * 16
 };
@@ -308,8 +300,8 @@ hipError_t launch_masks_to_labels(const uint8_t* masks, int npx, int n, int min_
                                   hipStream_t s);
 size_t mask_scratch_bytes();
 size_t mask_scratch_kept_offset();
-// global_passes: the octant maps by k_brick_dilate + k_brick_oct_axis (instrumentation bit 3)
-// instead of the LDS line passes (k_brick_oct_lds); both give the same maps.
+// global_passes: the octant maps by k_brick_dilate + k_brick_oct_axis, else by the LDS line
+// passes (k_brick_oct_lds); both give the same maps.
 hipError_t launch_brick_min(const VolGeom& g, const VolBufs& b, bool all, hipStream_t s, bool global_passes = false);
 hipError_t launch_fill_volume(const VolGeom& g, const VolBufs& b, uint32_t flags, hipStream_t s);
 hipError_t launch_flush_lazy(const VolGeom& g, const VolBufs& b, hipStream_t s);  // lazy weights -> weights

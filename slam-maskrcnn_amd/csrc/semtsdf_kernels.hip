@@ -657,10 +657,7 @@ __global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restric
     const int wv = t >> 6, ln = t & 63;
     if (ln < 8 && (ln & 1) == 0) {
         const int gx0 = tx * 4 + (ln >> 1), gy0 = ty * 4 + wv;
-        if (gx0 < p.w0 && gy0 < p.h0) {
-            p.l0[gy0 * p.p0 + gx0] = m | (n << 16);
-            p.z0[gy0 * p.w0 + gx0] = z;
-        }
+        if (gx0 < p.w0 && gy0 < p.h0) p.l0[gy0 * p.w0 + gx0] = make_uint2(m | (n << 16), z);
     }
 #pragma unroll
     for (int b : {2, 4}) {
@@ -671,11 +668,10 @@ __global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restric
     __shared__ unsigned s_w[4], s_n[4], s_z[4];
     if (ln == 0) { s_w[wv] = m; s_n[wv] = n; s_z[wv] = z; }
     __syncthreads();
-    if (t == 0) {
-        p.l1[ty * p.p1 + tx] = max(max(s_w[0], s_w[1]), max(s_w[2], s_w[3])) |
-                               (max(max(s_n[0], s_n[1]), max(s_n[2], s_n[3])) << 16);
-        p.z1[ty * p.w1 + tx] = max(max(s_z[0], s_z[1]), max(s_z[2], s_z[3]));
-    }
+    if (t == 0)
+        p.l1[ty * p.w1 + tx] = make_uint2(max(max(s_w[0], s_w[1]), max(s_w[2], s_w[3])) |
+                                              (max(max(s_n[0], s_n[1]), max(s_n[2], s_n[3])) << 16),
+                                          max(max(s_z[0], s_z[1]), max(s_z[2], s_z[3])));
 }
 
 hipError_t launch_depth_pyramid(const uint16_t* depth, const uint8_t* rgb, uint8_t* mask, int w, int h,
@@ -764,34 +760,15 @@ __device__ __forceinline__ void screen(const IntegrateArgs& a, float qx, float q
     }
 }
 
-// Conservative unit test: class 1 when no voxel of the unit can pass the projection / depth
-// tests of tsdf.cu:46-50 (dead), 2 when every voxel that passes them has f == 1 (free:
-// tsdf.cu:46-56 with diff >= mu), 3 when besides every voxel is touched (full free), else 0;
-// culling never changes results.  In three steps so that a lane can test two units with both
-// units' pyramid loads in flight together: cull_geo (the projected hull, no memory), cull_fetch
-// (the pyramid loads), cull_finish (the class).
-struct CullGeo {
-    int res;                 // >= 0: decided without the pyramid
-    unsigned uu, vv;         // the footprint (pixels, guard band included): u0 | u1 << 16, v0 | v1 << 16
-    float zmin, zmax;        // camera depth range of the unit's corners
-    bool full_ok;            // hull 1 px inside the image, every voxel stored and inside the volume (full free)
-    __device__ int u0() const { return (int)(uu & 0xFFFFu); }
-    __device__ int u1() const { return (int)(uu >> 16); }
-    __device__ int v0() const { return (int)(vv & 0xFFFFu); }
-    __device__ int v1() const { return (int)(vv >> 16); }
-};
-
-__device__ __forceinline__ CullGeo cull_geo(const IntegrateArgs& a, int x0, int y0, int lz0) {
+// Conservative unit test: returns 1 when no voxel of the unit can pass the projection /
+// depth tests of tsdf.cu:46-50 (dead), 2 when every voxel that passes them has f == 1
+// (free: tsdf.cu:46-56 with diff >= mu), else 0; culling never changes results.
+__device__ int unit_cull(const IntegrateArgs& a, int x0, int y0, int lz0) {
     const VolGeom& g = a.g;
-    CullGeo G;
-    G.res = -1;
-    G.uu = G.vv = 0u;
-    G.zmin = G.zmax = 0.0f;
-    G.full_ok = false;
     const int x1 = min(x0 + UX - 1, g.dimx - 1);
     const int y1 = min(y0 + UY - 1, g.dimy - 1);
     const int gz0 = local_to_global_z(g, lz0);
-    if (gz0 >= g.dimz) { G.res = 1; return G; }  // only halo/padding planes beyond the volume
+    if (gz0 >= g.dimz) return 1;  // only halo/padding planes beyond the volume
     const int gz1 = min(local_to_global_z(g, min(lz0 + UZ - 1, g.lz - 1)), g.dimz - 1);
     float umin = 3.0e38f, umax = -3.0e38f, vmin = 3.0e38f, vmax = -3.0e38f;
     float zmin = 3.0e38f, zmax = -3.0e38f, wmin = 3.0e38f, wmax = -3.0e38f;
@@ -825,130 +802,80 @@ __device__ __forceinline__ CullGeo cull_geo(const IntegrateArgs& a, int x0, int 
     // The image of a box under a perspective map is the hull of its corner images only
     // when the projective depth sz keeps one sign over the box.
     const float zeps = 1.0e-3f;
-    if (!(wmin > zeps) && !(wmax < -zeps)) { G.res = 0; return G; }
-    if (!(umin == umin) || !(vmin == vmin) || !(umax == umax) || !(vmax == vmax)) { G.res = 0; return G; }
+    if (!(wmin > zeps) && !(wmax < -zeps)) return 0;
+    if (!(umin == umin) || !(vmin == vmin) || !(umax == umax) || !(vmax == vmax)) return 0;
     const float W = (float)a.width, H = (float)a.height;
     // 1-pixel guard band around the projected hull
-    if (umax + 1.0f < 0.0f || umin - 1.0f > W || vmax + 1.0f < 0.0f || vmin - 1.0f > H) { G.res = 1; return G; }
+    if (umax + 1.0f < 0.0f || umin - 1.0f > W || vmax + 1.0f < 0.0f || vmin - 1.0f > H) return 1;
     const int u0 = (int)fmaxf(floorf(umin) - 1.0f, 0.0f);
     const int u1 = (int)fminf(floorf(umax) + 1.0f, W - 1.0f);
     const int v0 = (int)fmaxf(floorf(vmin) - 1.0f, 0.0f);
     const int v1 = (int)fminf(floorf(vmax) + 1.0f, H - 1.0f);
-    if (u0 > u1 || v0 > v1) { G.res = 1; return G; }
-    G.uu = (unsigned)u0 | ((unsigned)u1 << 16);  // image sides < 65536 (semtsdf_create)
-    G.vv = (unsigned)v0 | ((unsigned)v1 << 16);
-    G.zmin = zmin;
-    G.zmax = zmax;
-    G.full_ok = umin >= 1.0f && vmin >= 1.0f && umax <= W - 2.0f && vmax <= H - 2.0f && x0 + UX <= g.dimx &&
-                y0 + UY <= g.dimy && lz0 + UZ <= g.lz && local_to_global_z(g, lz0 + UZ - 1) < g.dimz;
-    return G;
-}
-
-// The footprint's pyramid words on the finest level covering it with <= 4x4 tiles: one 16-byte
-// load per tile row (the level's padded rows; lanes past the footprint masked after the load),
-// the 4 loads issued together; only the depth words: the zero flags are read in cull_finish for
-// the rare full-free candidates.  Other footprints take loops in cull_finish.
-typedef unsigned u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
-struct CullFetch {
-    unsigned t[16];
-    int mode;  // 0: t holds the words of the level fit0 names; 1: thin, level-0 loop; 2: level-1 loop; 3: too wide
-};
-
-// The footprint's tile range on level 0 (8-px tiles) or 1 (32-px).
-__device__ __forceinline__ void cull_range(const CullGeo& G, bool fit0, int& tx0, int& ty0, int& nx, int& ny) {
-    const int sh = fit0 ? 3 : 5;
-    tx0 = G.u0() >> sh;
-    ty0 = G.v0() >> sh;
-    nx = (G.u1() >> sh) - tx0;
-    ny = (G.v1() >> sh) - ty0;
-}
-__device__ __forceinline__ bool cull_fit0(const CullGeo& G) {
-    return ((G.u1() >> 3) - (G.u0() >> 3)) < 4 && ((G.v1() >> 3) - (G.v0() >> 3)) < 4;
-}
-
-__device__ __forceinline__ void cull_fetch(const IntegrateArgs& a, const CullGeo& G, CullFetch& F) {
-    F.mode = 3;
-    if (G.res >= 0) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) F.t[j] = 0u;
-        return;
-    }
-    const int u0 = G.u0(), u1 = G.u1(), v0 = G.v0(), v1 = G.v1();
-    const bool fit0 = cull_fit0(G);
-    const bool fit1 = ((u1 >> 5) - (u0 >> 5)) < 4 && ((v1 >> 5) - (v0 >> 5)) < 4;
-    if (!fit0 && ((u1 >> 3) - (u0 >> 3) + 1) * ((v1 >> 3) - (v0 >> 3) + 1) <= 16) F.mode = 1;  // thin footprints
-    else if (fit0 || fit1) F.mode = 0;
-    else if (((u1 >> 5) - (u0 >> 5) + 1) * ((v1 >> 5) - (v0 >> 5) + 1) <= 64) F.mode = 2;
-    const unsigned* lv = fit0 ? a.pyr.l0 : a.pyr.l1;
-    const int pl = fit0 ? a.pyr.p0 : a.pyr.p1;
-    int tx0, ty0, nx, ny;
-    cull_range(G, fit0, tx0, ty0, nx, ny);
-    const bool m0 = F.mode == 0;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const bool ok = m0 && r <= ny;
-        const u32x4_a4 w = *reinterpret_cast<const u32x4_a4*>(lv + (ok ? (ty0 + r) * pl + tx0 : 0));
-#pragma unroll
-        for (int c = 0; c < 4; ++c) F.t[4 * r + c] = (ok && c <= nx) ? w[c] : 0u;
-    }
-}
-
-__device__ __forceinline__ int cull_finish(const IntegrateArgs& a, const CullGeo& G, const CullFetch& F) {
-    const VolGeom& g = a.g;
-    if (G.res >= 0) return G.res;
+    if (u0 > u1 || v0 > v1) return 1;
+    // max depth (and min nonzero depth) over the footprint, on the finest pyramid level
+    // covering it with <= 4x4 tiles: the 16 loads are issued together (predicated), one round trip
     unsigned m = 0, nz = 0;  // nz: 0xFFFF - min nonzero raw depth (0: none)
-    unsigned zf = 0;         // a pixel of the covering tiles has depth 0 (loops only; mode 0 below)
-    if (F.mode == 0) {
+    unsigned zf = 0;         // a pixel of the covering tiles has depth 0
+    const bool fit0 = ((u1 >> 3) - (u0 >> 3)) < 4 && ((v1 >> 3) - (v0 >> 3)) < 4;
+    const bool fit1 = ((u1 >> 5) - (u0 >> 5)) < 4 && ((v1 >> 5) - (v0 >> 5)) < 4;
+    if (!fit0 && ((u1 >> 3) - (u0 >> 3) + 1) * ((v1 >> 3) - (v0 >> 3) + 1) <= 16) {  // thin footprints
+        for (int ty = v0 >> 3; ty <= (v1 >> 3); ++ty)
+            for (int tx = u0 >> 3; tx <= (u1 >> 3); ++tx) {
+                const uint2 w = a.pyr.l0[ty * a.pyr.w0 + tx];
+                m = max(m, w.x & 0xFFFFu);
+                nz = max(nz, w.x >> 16);
+                zf |= w.y;
+            }
+    } else if (fit0 || fit1) {
+        const int sh = fit0 ? 3 : 5;
+        const uint2* lv = fit0 ? a.pyr.l0 : a.pyr.l1;
+        const int wl = fit0 ? a.pyr.w0 : a.pyr.w1;
+        const int tx0 = u0 >> sh, ty0 = v0 >> sh, nx = (u1 >> sh) - tx0, ny = (v1 >> sh) - ty0;
+        uint2 t[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-            m = max(m, F.t[j] & 0xFFFFu);
-            nz = max(nz, F.t[j] >> 16);
+            const bool ok = (j & 3) <= nx && (j >> 2) <= ny;
+            t[j] = lv[ok ? (ty0 + (j >> 2)) * wl + tx0 + (j & 3) : 0];
+            t[j].x = ok ? t[j].x : 0u;
+            t[j].y = ok ? t[j].y : 0u;
         }
-    } else if (F.mode == 1) {
-        for (int ty = G.v0() >> 3; ty <= (G.v1() >> 3); ++ty)
-            for (int tx = G.u0() >> 3; tx <= (G.u1() >> 3); ++tx) {
-                const unsigned w = a.pyr.l0[ty * a.pyr.p0 + tx];
-                m = max(m, w & 0xFFFFu);
-                nz = max(nz, w >> 16);
-                zf |= a.pyr.z0[ty * a.pyr.w0 + tx];
-            }
-    } else if (F.mode == 2) {
-        for (int ty = G.v0() >> 5; ty <= (G.v1() >> 5); ++ty)
-            for (int tx = G.u0() >> 5; tx <= (G.u1() >> 5); ++tx) {
-                const unsigned w = a.pyr.l1[ty * a.pyr.p1 + tx];
-                m = max(m, w & 0xFFFFu);
-                nz = max(nz, w >> 16);
-                zf |= a.pyr.z1[ty * a.pyr.w1 + tx];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            m = max(m, t[j].x & 0xFFFFu);
+            nz = max(nz, t[j].x >> 16);
+            zf |= t[j].y;
+        }
+    } else if (((u1 >> 5) - (u0 >> 5) + 1) * ((v1 >> 5) - (v0 >> 5) + 1) <= 64) {
+        for (int ty = v0 >> 5; ty <= (v1 >> 5); ++ty)
+            for (int tx = u0 >> 5; tx <= (u1 >> 5); ++tx) {
+                const uint2 w = a.pyr.l1[ty * a.pyr.w1 + tx];
+                m = max(m, w.x & 0xFFFFu);
+                nz = max(nz, w.x >> 16);
+                zf |= w.y;
             }
     } else {
         return 0;  // footprint wider than 256x256 px (units at the near plane): keep
     }
     if (m == 0) return 1;  // every pixel of the footprint has depth 0
     const float dmax = (float)m / a.depth_scale;
-    const float margin = 1.0e-3f + 1.0e-4f * fmaxf(fabsf(G.zmax), fabsf(G.zmin));
+    const float margin = 1.0e-3f + 1.0e-4f * fmaxf(fabsf(zmax), fabsf(zmin));
     // every voxel has qz >= zmin, so diff <= dmax - zmin; rejected when that is <= -mu
-    if (dmax - G.zmin < -g.mu - margin) return 1;
+    if (dmax - zmin < -g.mu - margin) return 1;
     // free unit: every pixel it can touch has depth >= dmin (the zeros leave their voxels
     // untouched), and every voxel has qz <= zmax, so a touched voxel has diff >= mu, i.e.
     // f == 1 exactly; with the gate at or below 1 such a voxel updates only its sdf and weight
     if (a.free_ok && nz != 0) {
         const float dmin = (float)(0xFFFFu - nz) / a.depth_scale;
-        if (dmin - G.zmax > g.mu + margin) {
+        if (dmin - zmax > g.mu + margin) {
             // full free unit: besides, every voxel is stored and inside the volume, projects
             // into the image (hull 1 px inside it: the cull map's ~1e-4 px error cannot move a
             // pixel out) and its pixel has depth != 0 (no zero in the covering tiles), so every
             // voxel is touched with f == 1: the integrate needs no projection
-            if (!G.full_ok) return 2;
-            if (F.mode == 0) {  // the zero flags of the covering tiles (rare: full-free candidates)
-                const bool fit0 = cull_fit0(G);
-                const unsigned* zl = fit0 ? a.pyr.z0 : a.pyr.z1;
-                const int wl = fit0 ? a.pyr.w0 : a.pyr.w1;
-                int tx0, ty0, nx, ny;
-                cull_range(G, fit0, tx0, ty0, nx, ny);
-                for (int ty = ty0; ty <= ty0 + ny; ++ty)
-                    for (int tx = tx0; tx <= tx0 + nx; ++tx) zf |= zl[ty * wl + tx];
-            }
-            return zf == 0u ? 3 : 2;
+            const bool inside = x0 + UX <= g.dimx && y0 + UY <= g.dimy && lz0 + UZ <= g.lz &&
+                                local_to_global_z(g, lz0 + UZ - 1) < g.dimz;
+            if (inside && zf == 0u && umin >= 1.0f && vmin >= 1.0f && umax <= W - 2.0f && vmax <= H - 2.0f)
+                return 3;
+            return 2;
         }
     }
     return 0;
@@ -986,61 +913,32 @@ __host__ __device__ inline UnitGrid unit_grid(const VolGeom& g) {
 // b % kListSegs == c (one counter per segment, 256 B apart, keeps the same-address atomics
 // per counter to 1/64 of the workgroups).  Capacity of a segment: all units of its
 // workgroups.
-#ifndef SEMTSDF_CULL_PER
-#define SEMTSDF_CULL_PER 2
-#endif
 __host__ __device__ inline unsigned list_seg_cap(const UnitGrid& ug) {
-    constexpr unsigned per = 256u * SEMTSDF_CULL_PER;  // units per k_cull_units workgroup
-    const unsigned groups = (ug.nux + per - 1u) / per * ug.nuy * ug.nuz;
-    return (groups + kListSegs - 1u) / kListSegs * per;
+    const unsigned groups = (ug.nux + 255u) / 256u * ug.nuy * ug.nuz;  // k_cull_units workgroups
+    return (groups + kListSegs - 1u) / kListSegs * 256u;
 }
 
-// Cull pass: kCullPer units per lane (x fastest; a lane's units are 256 apart along x), their
-// pyramid loads in flight together.  The units that may hold a touched voxel are appended to
-// the workgroup's segment of one of three live-unit lists: list 0 (general), 1 (free units,
-// class 2), 2 (full free, class 3), each kListSegs segments of seg_cap entries with its own
-// counters (their order is irrelevant: units are independent).
-constexpr unsigned kCullPer = SEMTSDF_CULL_PER;  // units per lane
+// Cull pass: one lane per unit (x fastest).  The units that may hold a touched voxel are
+// appended to the workgroup's segment of one of two live-unit lists: list 0 (general) and
+// list 1 (free units, unit_cull == 2), each kListSegs segments of seg_cap entries with its
+// own counters (their order is irrelevant: units are independent).
 __global__ __launch_bounds__(256) void k_cull_units(IntegrateArgs a, UnitGrid ug, unsigned seg_cap) {
     __shared__ unsigned s_cnt[kLists][4];
     __shared__ unsigned s_base[kLists];
-    // grid (x runs of 256 kCullPer units, uy, uz): no integer division by the runtime unit counts
-    const unsigned ux0 = blockIdx.x * (256u * kCullPer) + threadIdx.x;
-    const unsigned uy = blockIdx.y, uz = blockIdx.z;
+    // grid (x runs of 256 units, uy, uz): no integer division by the runtime unit counts
+    const unsigned ux = blockIdx.x * blockDim.x + threadIdx.x, uy = blockIdx.y, uz = blockIdx.z;
     const unsigned bid = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-    CullGeo G[kCullPer];
-    CullFetch F[kCullPer];
-    int cls[kCullPer];
-#pragma unroll
-    for (unsigned k = 0; k < kCullPer; ++k) {
-        const unsigned ux = ux0 + 256u * k;
-        G[k].res = 1;
-        if (ux < ug.nux) {
-            if (a.cull) G[k] = cull_geo(a, (int)ux * UX, (int)uy * UY, (int)uz * UZ);
-            else G[k].res = 0;
-        }
-    }
-#pragma unroll
-    for (unsigned k = 0; k < kCullPer; ++k) cull_fetch(a, G[k], F[k]);
-#pragma unroll
-    for (unsigned k = 0; k < kCullPer; ++k) cls[k] = cull_finish(a, G[k], F[k]);
+    const bool inside = ux < ug.nux;
+    const unsigned u = pack_unit(ux, uy, uz);
+    int c = 1;  // dead
+    if (inside) c = a.cull ? unit_cull(a, (int)ux * UX, (int)uy * UY, (int)uz * UZ) : 0;
     const int lane = (int)(threadIdx.x & 63u), wv = (int)(threadIdx.x >> 6);
     // list of class c: 0 general (c == 0), 1 free (c == 2), 2 full free (c == 3)
-    unsigned long long bal[kLists][kCullPer];
-#pragma unroll
-    for (unsigned k = 0; k < kCullPer; ++k) {
-        bal[0][k] = __ballot(cls[k] == 0);
-        bal[1][k] = __ballot(cls[k] == 2);
-        bal[2][k] = __ballot(cls[k] == 3);
-    }
+    const unsigned long long bal0 = __ballot(c == 0), bal1 = __ballot(c == 2), bal2 = __ballot(c == 3);
     if (lane == 0) {
-#pragma unroll
-        for (int l = 0; l < kLists; ++l) {
-            unsigned c = 0;
-#pragma unroll
-            for (unsigned k = 0; k < kCullPer; ++k) c += (unsigned)__popcll(bal[l][k]);
-            s_cnt[l][wv] = c;
-        }
+        s_cnt[0][wv] = (unsigned)__popcll(bal0);
+        s_cnt[1][wv] = (unsigned)__popcll(bal1);
+        s_cnt[2][wv] = (unsigned)__popcll(bal2);
     }
     __syncthreads();
     const unsigned seg = bid % (unsigned)kListSegs;
@@ -1050,27 +948,19 @@ __global__ __launch_bounds__(256) void k_cull_units(IntegrateArgs a, UnitGrid ug
         s_base[l] = tot ? atomicAdd(a.list_count + (l * kListSegs + seg) * kListCountStride, tot) : 0u;
     }
     __syncthreads();
-    const unsigned long long below = (1ull << lane) - 1ull;
-    unsigned run[kLists] = {0u, 0u, 0u};  // the wave's entries of the lane's earlier units
-#pragma unroll
-    for (unsigned k = 0; k < kCullPer; ++k) {
-        const int c = cls[k];
-        if (c != 1) {
-            const unsigned l = c == 2 ? 1u : c == 3 ? 2u : 0u;
-            unsigned off = s_base[l] + (unsigned)__popcll(bal[l][k] & below) + run[l];
-            for (int w = 0; w < wv; ++w) off += s_cnt[l][w];
-            a.unit_list[(size_t)l * kListSegs * seg_cap + seg * seg_cap + off] = pack_unit(ux0 + 256u * k, uy, uz);
-        }
-#pragma unroll
-        for (int l = 0; l < kLists; ++l) run[l] += (unsigned)__popcll(bal[l][k]);
+    if (c != 1) {
+        const unsigned l = c == 2 ? 1u : c == 3 ? 2u : 0u;
+        unsigned off = s_base[l] + (unsigned)__popcll((l == 1 ? bal1 : l == 2 ? bal2 : bal0) & ((1ull << lane) - 1ull));
+        for (int w = 0; w < wv; ++w) off += s_cnt[l][w];
+        a.unit_list[(size_t)l * kListSegs * seg_cap + seg * seg_cap + off] = u;
     }
 }
 
 hipError_t launch_cull(const IntegrateArgs& a, hipStream_t s) {
     const UnitGrid ug = unit_grid(a.g);
     if (ug.n == 0) return hipSuccess;  // a shard that owns no chunk
-    hipLaunchKernelGGL(k_cull_units, dim3((ug.nux + 256 * kCullPer - 1) / (256 * kCullPer), ug.nuy, ug.nuz), dim3(256), 0,
-                       s, a, ug, list_seg_cap(ug));
+    hipLaunchKernelGGL(k_cull_units, dim3((ug.nux + 255) / 256, ug.nuy, ug.nuz), dim3(256), 0, s, a, ug,
+                       list_seg_cap(ug));
     return hipGetLastError();
 }
 

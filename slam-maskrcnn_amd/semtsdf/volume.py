@@ -281,11 +281,11 @@ class Volume:
 
     # ---- instrumentation
     def set_instrumentation(self, events: bool = True, count: bool = False, force_exact: bool = False,
-                            global_map_passes: bool = False):
+                            other_map_passes: bool = False):
         """events: HIP-event kernel timing; count: touched/gated voxel counters; force_exact: every
         association row decided from its exact f32 pixel-order sums (tests, cost measurement);
-        global_map_passes: the octant maps by the global-memory passes (tests: same maps)."""
-        flags = (1 if events else 0) | (2 if count else 0) | (4 if force_exact else 0) | (8 if global_map_passes else 0)
+        other_map_passes: the octant maps by the other of their two implementations (tests: same maps)."""
+        flags = (1 if events else 0) | (2 if count else 0) | (4 if force_exact else 0) | (8 if other_map_passes else 0)
         L.check(L.load().semtsdf_set_instrumentation(self._h, flags))
 
     def map_words(self):

@@ -76,14 +76,14 @@ def test_lds_map_passes_equal_global_passes_and_definition(S, stream, dims):
     semtsdf, L = S
     st, frames = stream
     vols = []
-    for global_passes in (False, True):
+    for other in (False, True):
         p = semtsdf.default_params(64, KI, 640, 480)
         p.dim[0], p.dim[1], p.dim[2] = dims
         semtsdf.place_from_frame(p, frames[0].depth, float(np.mean(frames[0].depth[frames[0].depth > 0])) / 5000.0,
                                  L.PLACE_SFM)
         p.flags = L.F_SEMANTIC | L.F_GATE_COLOR
         v = semtsdf.Volume(p, 0)
-        v.set_instrumentation(events=False, global_map_passes=global_passes)
+        v.set_instrumentation(events=False, other_map_passes=other)
         vols.append(v)
     voxel = float(p.voxel[0])
     skippable = []
