@@ -612,7 +612,7 @@ int associate_impl(semtsdf_vol* v, uint8_t* mask_d, const float E[16], hipStream
         static const char* lpt = getenv("SEMTSDF_MARCH_LPT");
         if (lpt ? atoi(lpt) != 0 : SEMTSDF_MARCH_LPT_DEFAULT) {
             const int n = ((a.width + 15) / 16) * ((a.height + 15) / 16) + ((r.width + 15) / 16) * ((r.height + 15) / 16);
-            if (n > v->tile_cap) {
+            if (n <= 8192 && n > v->tile_cap) {  // tile_order sorts up to 8192 tiles (256 x kTileOrderPer)
                 for (unsigned** q : {&v->tile_cost_d, &v->tile_perm_d})
                     if (*q) { (void)hipFree(*q); v->device_bytes -= (size_t)v->tile_cap * sizeof(unsigned); *q = nullptr; }
                 v->tile_cap = 0;
@@ -621,9 +621,11 @@ int associate_impl(semtsdf_vol* v, uint8_t* mask_d, const float E[16], hipStream
                 if (int rc = dev_alloc(v, (void**)&v->tile_perm_d, (size_t)n * sizeof(unsigned))) return rc;
                 v->tile_cap = n;
             }
-            a.tile_cost = v->tile_cost_d;
-            a.tile_perm = v->tile_n == n ? v->tile_perm_d : nullptr;  // sizes changed: identity
-            order_n = n;
+            if (n <= 8192) {
+                a.tile_cost = v->tile_cost_d;
+                a.tile_perm = v->tile_n == n ? v->tile_perm_d : nullptr;  // sizes changed: identity
+                order_n = n;
+            }
         }
         HIPC(launch_march_fused(a, r, s));
         v->n_render++;

@@ -2984,30 +2984,44 @@ struct DecideLds {
 // The fused march's next launch order from this frame's tile durations: 64 linear cost buckets,
 // heaviest first (LPT), a counting sort in one workgroup.  Order within a bucket is arbitrary;
 // the order never changes results (the association's sums are integer, the render per pixel).
+constexpr int kTileOrderPer = 32;  // tiles per thread of tile_order: launch orders of up to 8192 tiles
 __device__ void tile_order(const unsigned* __restrict__ cost, unsigned* __restrict__ perm, int n, DecideLds& L) {
     const int tid = threadIdx.x;
     if (tid < 64) L.thist[tid] = 0u;
     if (tid == 0) L.tmax = 0u;
-    __syncthreads();
+    unsigned c[kTileOrderPer];
+#pragma unroll
+    for (int j = 0; j < kTileOrderPer; ++j) {  // every load in flight together
+        const int i = tid + 256 * j;
+        c[j] = i < n ? cost[i] : 0u;
+    }
     unsigned mx = 0;
-    for (int i = tid; i < n; i += 256) mx = max(mx, cost[i]);
+#pragma unroll
+    for (int j = 0; j < kTileOrderPer; ++j) mx = max(mx, c[j]);
     for (int off = 32; off > 0; off >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, off, 64));
+    __syncthreads();  // the counters' initialisation
     if ((tid & 63) == 0) atomicMax(&L.tmax, mx);
     __syncthreads();
     const unsigned long long den = (unsigned long long)L.tmax + 1ull;
-    auto bucket = [&](unsigned c) { return 63u - (unsigned)(((unsigned long long)c * 64ull) / den); };
-    for (int i = tid; i < n; i += 256) atomicAdd(&L.thist[bucket(cost[i])], 1u);
+    unsigned bk[kTileOrderPer];
+#pragma unroll
+    for (int j = 0; j < kTileOrderPer; ++j) {
+        bk[j] = 63u - (unsigned)(((unsigned long long)c[j] * 64ull) / den);
+        if (tid + 256 * j < n) atomicAdd(&L.thist[bk[j]], 1u);
+    }
     __syncthreads();
     if (tid == 0) {
         unsigned run = 0;
         for (int k = 0; k < 64; ++k) {
-            const unsigned c = L.thist[k];
+            const unsigned v = L.thist[k];
             L.thist[k] = run;
-            run += c;
+            run += v;
         }
     }
     __syncthreads();
-    for (int i = tid; i < n; i += 256) perm[atomicAdd(&L.thist[bucket(cost[i])], 1u)] = (unsigned)i;
+#pragma unroll
+    for (int j = 0; j < kTileOrderPer; ++j)
+        if (tid + 256 * j < n) perm[atomicAdd(&L.thist[bk[j]], 1u)] = (unsigned)(tid + 256 * j);
 }
 
 __global__ __launch_bounds__(256) void k_assoc_decide(DecideArgs a) {
