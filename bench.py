@@ -314,6 +314,45 @@ def timed_integrate(vol, step, K, warmup, pg=None, device=0, finish=None):
 
 
 # ----------------------------------------------------------------------------- C3 pipeline
+class HipEvent:
+    """A HIP event for ordering this process's streams on one device (the upload ring): no
+    timing and no system-scope fence (hipEventDisableSystemFence: the consumers are kernels of
+    the same device), unlike torch.cuda.Event.  The HIP runtime is torch's (semtsdf._lib loads
+    the library after torch, so both resolve libamdhip64.so.7 to the same copy)."""
+    _hip = None
+
+    def __init__(self):
+        if HipEvent._hip is None:
+            h = ctypes.CDLL("libamdhip64.so.7")
+            h.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+            h.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+            h.hipStreamWaitEvent.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
+            h.hipEventDestroy.argtypes = [ctypes.c_void_p]
+            HipEvent._hip = h
+        self.ev = ctypes.c_void_p()
+        rc = HipEvent._hip.hipEventCreateWithFlags(ctypes.byref(self.ev), 0x2 | 0x20000000)
+        if rc != 0:
+            raise RuntimeError(f"hipEventCreateWithFlags: {rc}")
+
+    @property
+    def cuda_event(self):
+        return self.ev.value
+
+    def record(self, stream):
+        rc = HipEvent._hip.hipEventRecord(self.ev, ctypes.c_void_p(stream.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"hipEventRecord: {rc}")
+
+    def __del__(self):
+        if HipEvent._hip is not None and self.ev:
+            HipEvent._hip.hipEventDestroy(self.ev)
+
+    def wait_on(self, stream):
+        rc = HipEvent._hip.hipStreamWaitEvent(ctypes.c_void_p(stream.cuda_stream), self.ev, 0)
+        if rc != 0:
+            raise RuntimeError(f"hipStreamWaitEvent: {rc}")
+
+
 def run_pipeline(semtsdf, L, p, local, n_frames=100, n_warm=5):
     """§8d frames/s of C3: host pose path + async H2D (pinned, copy stream) + association
     raycast + relabel + integrate + one live raycast view per frame, in the volume stream's
@@ -363,15 +402,23 @@ def run_pipeline(semtsdf, L, p, local, n_frames=100, n_warm=5):
         slot = [(d_all[s].data_ptr(), d_all[s].data_ptr() + NPX * 2, d_all[s].data_ptr() + NPX * 5)
                 for s in range(ring)]
         outs = [torch.empty(NPX * 3, dtype=torch.uint8, device=dev) for _ in range(2)]
-        copied = [torch.cuda.Event() for _ in range(ring)]
-        used = [torch.cuda.Event() for _ in range(ring)]
-        integrated = torch.cuda.Event()
-        rendered = torch.cuda.Event()
+        hip_ev = os.environ.get("BENCH_HIP_EVENTS", "1") != "0"
+        mk = HipEvent if hip_ev else torch.cuda.Event
+        copied = [mk() for _ in range(ring)]
+        used = [mk() for _ in range(ring)]
+        integrated = mk()
+        rendered = mk()
+
+        def wait(stream, ev):
+            if hip_ev:
+                ev.wait_on(stream)
+            else:
+                stream.wait_event(ev)
         torch.cuda.synchronize()
 
         def upload(k):
             s = k % ring
-            cstream.wait_event(used[s])
+            wait(cstream, used[s])
             L.check(lib.semtsdf_memcpy(ctypes.c_void_p(slot[s][0]), ctypes.c_void_p(h_all[k].data_ptr()), NPX * 6, 4,
                                        ctypes.c_void_p(cstream.cuda_stream)))
             copied[s].record(cstream)
@@ -379,7 +426,7 @@ def run_pipeline(semtsdf, L, p, local, n_frames=100, n_warm=5):
         def frame(k, first):
             s = k % ring
             E = P.relative_pose(P.parse_pos(traj[k, 1:]), ext0_inv)  # host pose path (tsdf.cu:217)
-            vstream.wait_event(copied[s])
+            wait(vstream, copied[s])
             after = rendered.cuda_event if (overlap and not first) else None
             pd, pr, pm = slot[s]
             if fused:  # the view shown after frame k - 1, in the launch of frame k's association
@@ -394,7 +441,7 @@ def run_pipeline(semtsdf, L, p, local, n_frames=100, n_warm=5):
             s2w, c = semtsdf.orbit_camera(list(p.Kinv), 0.01 * k, mean_m)
             if overlap:
                 integrated.record(vstream)
-                rstream.wait_event(integrated)
+                wait(rstream, integrated)
             vol.raycast_dev(s2w, c, L.RENDER_LABEL, outs[k % 2].data_ptr(), stream=rstream.cuda_stream)
             if overlap:
                 rendered.record(rstream)
@@ -689,7 +736,7 @@ C4_SPEC = ("C4: 1024^3 semantic TSDF (sdf f32, weight i32, colour u8x3, 32-bin u
            "integrated, and after the K steps one label raycast view (the north star's final raycast composite)")
 
 
-def run_c4_single(semtsdf, L, local, frames, f0, K, warmup):
+def run_c4_single(semtsdf, L, local, frames, f0, K, warmup, async_prepass=True):
     """C4's 1024^3 semantic volume whole on one GPU (the base of the strong-scaling lines):
     K integrated frames + the final label raycast, then the per-frame variant (integrate +
     one raycast view every step)."""
@@ -704,7 +751,10 @@ def run_c4_single(semtsdf, L, local, frames, f0, K, warmup):
 
     def integ(k):
         i = k % len(frames)
-        vol.integrate_dev(dbuf.ptr + i * NPX * 2, rbuf.ptr + i * NPX * 3, mbuf.ptr + i * NPX, Es[i])
+        if async_prepass:  # as the C3 step: the prepass beside the previous frame's integrate
+            vol.integrate_dev_async(dbuf.ptr + i * NPX * 2, rbuf.ptr + i * NPX * 3, mbuf.ptr + i * NPX, Es[i])
+        else:
+            vol.integrate_dev(dbuf.ptr + i * NPX * 2, rbuf.ptr + i * NPX * 3, mbuf.ptr + i * NPX, Es[i])
 
     def view(k=0):
         s2w, c = semtsdf.orbit_camera(list(p.Kinv), 0.01 * k, mean_m)
@@ -755,7 +805,7 @@ def run_c4_single(semtsdf, L, local, frames, f0, K, warmup):
     return res
 
 
-def run_c4_dist(semtsdf, L, rank, world, local, pg, frames, f0, K, warmup, chunk):
+def run_c4_dist(semtsdf, L, rank, world, local, pg, frames, f0, K, warmup, chunk, async_prepass=True):
     """C4 strong scaling: rank r integrates shard r of the 1024^3 volume (no collective on
     that path); after the K frames one label raycast view is composited across the shards
     (DistShardGroup: RCCL all-reduce MIN between the protocol steps).  Then the per-frame
@@ -775,7 +825,10 @@ def run_c4_dist(semtsdf, L, rank, world, local, pg, frames, f0, K, warmup, chunk
 
     def integ(k):
         i = k % len(frames)
-        vol.integrate_dev(dbuf.ptr + i * NPX * 2, rbuf.ptr + i * NPX * 3, mbuf.ptr + i * NPX, Es[i])
+        if async_prepass:  # as the C3 step: the prepass beside the previous frame's integrate
+            vol.integrate_dev_async(dbuf.ptr + i * NPX * 2, rbuf.ptr + i * NPX * 3, mbuf.ptr + i * NPX, Es[i])
+        else:
+            vol.integrate_dev(dbuf.ptr + i * NPX * 2, rbuf.ptr + i * NPX * 3, mbuf.ptr + i * NPX, Es[i])
 
     def view(k=0):
         s2w, c = semtsdf.orbit_camera(list(p.Kinv), 0.01 * k, mean_m)
@@ -844,8 +897,12 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true", help="skip pipeline, orbit, C2 and C4-single")
     ap.add_argument("--no-c4", action="store_true", help="skip the 1024^3 single-GPU C4 measurement")
     ap.add_argument("--no-cull", action="store_true", help="debug: disable unit culling")
-    ap.add_argument("--async-prepass", action="store_true",
-                    help="C3 step: frame prepass on the volume's prep stream (overlap probe; measured no faster)")
+    ap.add_argument("--async-prepass", action="store_true", default=True,
+                    help="C3 step: frame k's prepass (depth pyramid + unit cull) on the volume's prep stream beside "
+                         "frame k-1's integrate (semtsdf_integrate_dev_async; the default: 0.094 against 0.097 ms per "
+                         "step, profiles/r04/ab_async_prepass_c3.txt)")
+    ap.add_argument("--sync-prepass", dest="async_prepass", action="store_false",
+                    help="C3 step: the prepass on the volume's stream in front of its integrate")
     ap.add_argument("--only", choices=["pipeline", "masks", "c2", "c4"], default=None,
                     help="debug: run one section alone and print its record")
     ap.add_argument("--cpu-planes", type=int, default=64)
@@ -878,10 +935,11 @@ def main():
         # 0, whole 1024^3 volume; the other ranks wait): the base of speedup_vs_1gpu
         base = None
         if rank == 0 and not args.no_c4:
-            base = run_c4_single(semtsdf, L, local, frames, f0, args.steps, args.warmup)
+            base = run_c4_single(semtsdf, L, local, frames, f0, args.steps, args.warmup, args.async_prepass)
             log(f"[bench rank 0] C4 on one GPU: {base['ms_per_step']:.4f} ms per step")
         barrier(pg, local)
-        r = run_c4_dist(semtsdf, L, rank, world, local, pg, frames, f0, args.steps, args.warmup, args.c4_chunk)
+        r = run_c4_dist(semtsdf, L, rank, world, local, pg, frames, f0, args.steps, args.warmup, args.c4_chunk,
+                        args.async_prepass)
         if rank == 0:
             value = 1024 ** 3 * args.steps / r["elapsed"] / 1e6
             kf = r["per_frame_steps"]
@@ -945,7 +1003,7 @@ def main():
         elif args.only == "c2":
             r = run_c2(semtsdf, L, local, frames, f0, args.steps, args.warmup, args.c2_traffic_json)
         else:
-            r = run_c4_single(semtsdf, L, local, frames, f0, args.steps, args.warmup)
+            r = run_c4_single(semtsdf, L, local, frames, f0, args.steps, args.warmup, args.async_prepass)
         print(json.dumps({"only": args.only, args.only: r}), flush=True)
         return
     if emu_world > 1:
@@ -999,7 +1057,7 @@ def main():
         masks = run_mask_overlap(semtsdf, L, p, local, frames, f0)
         c2 = run_c2(semtsdf, L, local, frames, f0, args.steps, args.warmup, args.c2_traffic_json)
         if not args.no_c4:
-            c4 = run_c4_single(semtsdf, L, local, frames, f0, args.steps, args.warmup)
+            c4 = run_c4_single(semtsdf, L, local, frames, f0, args.steps, args.warmup, args.async_prepass)
     copy_bw = copy_bandwidth(local) if not args.no_pipeline else None
 
     rec = {
@@ -1025,6 +1083,8 @@ def main():
         },
         "frames_per_s": pipeline["frames_per_s"] if pipeline else None,
         "integrate_frames_per_s": round(args.steps / elapsed, 2),
+        "prepass": ("frame k's depth pyramid + unit cull on the volume's prep stream beside frame k-1's integrate "
+                    "(semtsdf_integrate_dev_async)") if args.async_prepass else "in front of the frame's integrate",
         "integrate_kernel_ms": round(kern_ms, 4),
         "prep_ms": round(prep_ms, 4),
         "touched_per_frame": int(touched),

@@ -340,9 +340,11 @@ int ensure_prep_stream(semtsdf_vol* v) {
 // async: the frame prepass runs on the volume's prep stream, ordered after inputs_ready (when
 // given) and after the integrate that last read its frame set -- not after the earlier work
 // of stream s -- so it may overlap the previous frame's integrate.
+// inputs_on_s: inputs_ready was recorded on s at the start of the caller's frame, after every
+// earlier reader of both frame sets: the prepass needs no frame-set event.
 int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d, const uint8_t* mask_d,
                    const int32_t* cls_d, const float E[16], hipStream_t s, bool async = false,
-                   hipEvent_t inputs_ready = nullptr) {
+                   hipEvent_t inputs_ready = nullptr, bool inputs_on_s = false) {
     if (!E) return fail(SEMTSDF_ERR_INVALID, "E is NULL");
     if (!depth_d || !rgb_d) return fail(SEMTSDF_ERR_INVALID, "depth/rgb is NULL");
     if ((v->p.flags & SEMTSDF_F_SEMANTIC) && !mask_d) return fail(SEMTSDF_ERR_INVALID, "semantic volume needs a mask");
@@ -411,11 +413,13 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
         ps = v->prep_stream;
         v->async_used = true;
         if (inputs_ready) HIPC(hipStreamWaitEvent(ps, inputs_ready, 0));
-        if (!F.free_recorded) {  // the set's last reader is unknown (first asynchronous frame): all of s
-            HIPC(hipEventRecord(F.set_free, s));
-            F.free_recorded = true;
+        if (!(inputs_ready && inputs_on_s)) {
+            if (!F.free_recorded) {  // the set's last reader is unknown (first asynchronous frame): all of s
+                HIPC(hipEventRecord(F.set_free, s));
+                F.free_recorded = true;
+            }
+            HIPC(hipStreamWaitEvent(ps, F.set_free, 0));
         }
-        HIPC(hipStreamWaitEvent(ps, F.set_free, 0));
     }
     v->next_set ^= 1;
     EventPair epp;
@@ -474,7 +478,9 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
         }
     }
     if (ep.a) v->ev_integrate.push_back(ep);
-    if (v->async_used) {  // a later asynchronous prepass into this set waits for this integrate
+    if (v->async_used && async && inputs_ready && inputs_on_s) {
+        F.free_recorded = false;  // a later prepass ordered otherwise records its event then
+    } else if (v->async_used) {  // a later asynchronous prepass into this set waits for this integrate
         HIPC(hipEventRecord(F.set_free, s));
         F.free_recorded = true;
     }
@@ -1316,7 +1322,7 @@ static int parse_frame_dev_impl(semtsdf_vol* v, const uint16_t* depth_d, const u
     // other streams (a live render) finish first; the association above, a read, may overlap them
     if (integrate_after_event) HIPC(hipStreamWaitEvent(s, (hipEvent_t)integrate_after_event, 0));
     int rc = integrate_impl(v, depth_d, rgb_d, sem ? mask_d : nullptr, nullptr, E, s, overlap_prep,
-                            overlap_prep ? v->in_ev : nullptr);
+                            overlap_prep ? v->in_ev : nullptr, overlap_prep);
     if (rc) return relabel_unconsumed(v, mask_d, s, rc);
     v->n_obs++;
     // the next frame's association (and a live view) march this state: refresh the

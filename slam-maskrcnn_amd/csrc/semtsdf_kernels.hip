@@ -3028,6 +3028,12 @@ __global__ __launch_bounds__(256) void k_assoc_decide(DecideArgs a) {
     __shared__ DecideLds L;
     AssocTables* T = a.T;
     const int tid = threadIdx.x;
+    // an extra last workgroup orders the next fused march's tiles, beside the decision
+    const unsigned nwork = gridDim.x - (a.tile_n > 0 ? 1u : 0u);
+    if (blockIdx.x >= nwork) {
+        tile_order(a.tile_cost, a.tile_perm, a.tile_n, L);
+        return;
+    }
     const int max_now = min((int)T->max_label + 1, kMaxObjects);
     const float thr_f = 3.0f * a.eps;  // tsdf.cu:349, a float product
     const double thr = (double)thr_f;
@@ -3105,7 +3111,10 @@ __global__ __launch_bounds__(256) void k_assoc_decide(DecideArgs a) {
         return;
     }
     const bool have_px = a.px.bits != nullptr;
-    if (blockIdx.x == 0 && a.tile_n > 0) tile_order(a.tile_cost, a.tile_perm, a.tile_n, L);
+    // F is the same in every workgroup (the same certificate of the same tables): without a
+    // flagged row nothing is handed over but the tickets, so the hand-off needs no fences (an
+    // agent-scope release writes back the XCD's L2, an acquire invalidates it)
+    const bool exact = F != 0u && have_px;
     // ---- exact sums: column j = blockIdx.x of every flagged row, one pass over the pixels ----
     if (F && have_px && blockIdx.x >= 1) {
         const int j = (int)blockIdx.x;
@@ -3121,14 +3130,14 @@ __global__ __launch_bounds__(256) void k_assoc_decide(DecideArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (exact) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned ticket = __hip_atomic_fetch_add(&a.X->counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        L.last = ticket == gridDim.x - 1u;
+        L.last = ticket == nwork - 1u;
     }
     __syncthreads();
     if (!L.last) return;
-    if (tid == 0) {
+    if (tid == 0 && exact) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -3217,7 +3226,7 @@ __global__ __launch_bounds__(256) void k_assoc_decide(DecideArgs a) {
 hipError_t launch_assoc_decide(const DecideArgs& a, hipStream_t s) {
     // workgroup j >= 1 computes column j of the exact sums: one workgroup when there is no
     // per-pixel data to compute them from
-    const unsigned grid = (a.certify_only || !a.px.bits) ? 1u : (unsigned)kMaxObjects;
+    const unsigned grid = ((a.certify_only || !a.px.bits) ? 1u : (unsigned)kMaxObjects) + (a.tile_n > 0 ? 1u : 0u);
     hipLaunchKernelGGL(k_assoc_decide, dim3(grid), dim3(256), 0, s, a);
     return hipGetLastError();
 }
