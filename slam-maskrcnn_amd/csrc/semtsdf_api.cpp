@@ -28,6 +28,9 @@ using namespace semtsdf;
 #ifndef SEMTSDF_EVENT_FLAGS_DEFAULT
 #define SEMTSDF_EVENT_FLAGS_DEFAULT 2  // order_event_flags(): 0 system-scope release, 1 device-scope release, 2 no system fence
 #endif
+#ifndef SEMTSDF_FRAME_FOLD_DEFAULT
+#define SEMTSDF_FRAME_FOLD_DEFAULT 0  // env SEMTSDF_FRAME_FOLD=0/1 overrides (A/B)
+#endif
 #ifndef SEMTSDF_MARCH_LPT_DEFAULT
 #define SEMTSDF_MARCH_LPT_DEFAULT 1  // env SEMTSDF_MARCH_LPT=0/1 overrides (A/B)
 #endif
@@ -342,9 +345,11 @@ int ensure_prep_stream(semtsdf_vol* v) {
 // of stream s -- so it may overlap the previous frame's integrate.
 // inputs_on_s: inputs_ready was recorded on s at the start of the caller's frame, after every
 // earlier reader of both frame sets: the prepass needs no frame-set event.
+// pre_done: the frame's depth pyramid is already in the next frame set (computed in the fused
+// march's launch, raw labels): only the cull runs, on s.
 int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d, const uint8_t* mask_d,
                    const int32_t* cls_d, const float E[16], hipStream_t s, bool async = false,
-                   hipEvent_t inputs_ready = nullptr, bool inputs_on_s = false) {
+                   hipEvent_t inputs_ready = nullptr, bool inputs_on_s = false, bool pre_done = false) {
     if (!E) return fail(SEMTSDF_ERR_INVALID, "E is NULL");
     if (!depth_d || !rgb_d) return fail(SEMTSDF_ERR_INVALID, "depth/rgb is NULL");
     if ((v->p.flags & SEMTSDF_F_SEMANTIC) && !mask_d) return fail(SEMTSDF_ERR_INVALID, "semantic volume needs a mask");
@@ -405,7 +410,7 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
     // the pending table stays set until the launch consuming it is queued: an error before
     // that leaves it for relabel_unconsumed (the decision already advanced num_objs)
     const uint8_t* lut = mask_d ? v->pending_lut : nullptr;
-    const bool relabel_after = async && lut;
+    const bool relabel_after = (async || pre_done) && lut;
     if (async)
         if (int rc = ensure_prep_stream(v)) return rc;
     hipStream_t ps = s;
@@ -424,8 +429,9 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
     v->next_set ^= 1;
     EventPair epp;
     timing_begin(v, v->ev_prep, ps, &epp);
-    HIPC(launch_depth_pyramid(depth_d, rgb_d, const_cast<uint8_t*>(mask_d), v->p.width, v->p.height, v->p.depth_scale,
-                              F.pyr, F.list_count, ps, relabel_after ? nullptr : lut));
+    if (!pre_done)
+        HIPC(launch_depth_pyramid(depth_d, rgb_d, const_cast<uint8_t*>(mask_d), v->p.width, v->p.height,
+                                  v->p.depth_scale, F.pyr, F.list_count, ps, relabel_after ? nullptr : lut));
     if (lut && !relabel_after) v->pending_lut = nullptr;  // consumed by the prepass
     HIPC(launch_cull(a, ps));
     timing_end(v, v->ev_prep, ps, &epp);
@@ -585,8 +591,12 @@ DecideArgs decide_args(semtsdf_vol* v, const uint8_t* mask_d, AssocPixels px, bo
 // integrate's prepass (v->pending_lut), saving a launch.
 // view (optional): a render of the same volume state launched together with the march
 // (k_march_fused); its arguments were validated by the caller.
+// pre_depth/pre_rgb (with a view): the frame's mask statistics and its prepass tiles (depth
+// pyramid into the next frame set, raw labels) run as the first blocks of the fused launch; the
+// caller's integrate then skips the pyramid (integrate_impl pre_done).
 int associate_impl(semtsdf_vol* v, uint8_t* mask_d, const float E[16], hipStream_t s, bool want_decision,
-                   bool defer_relabel = false, const RenderArgs* view = nullptr) {
+                   bool defer_relabel = false, const RenderArgs* view = nullptr, const uint16_t* pre_depth = nullptr,
+                   const uint8_t* pre_rgb = nullptr) {
     if (v->p.z_nshards != 1) return fail(SEMTSDF_ERR_UNSUPPORTED, "association on a Z-sharded handle is not supported yet");
     if (!(v->p.flags & SEMTSDF_F_SEMANTIC)) return fail(SEMTSDF_ERR_STATE, "association needs a SEMANTIC volume");
     if (v->n_obs == 0) return fail(SEMTSDF_ERR_STATE, "association needs n_obs > 0 (tsdf.cu:426)");
@@ -594,7 +604,8 @@ int associate_impl(semtsdf_vol* v, uint8_t* mask_d, const float E[16], hipStream
     timing_begin(v, v->ev_assoc, s, &ep);
     if (int rc = ensure_bmin(v, s)) return rc;
     if (int rc = tables_ready(v, s)) return rc;
-    HIPC(launch_mask_stats(mask_d, (int)npx(v), v->tables_d, s));
+    const bool fold = view && pre_depth && pre_rgb;
+    if (!fold) HIPC(launch_mask_stats(mask_d, (int)npx(v), v->tables_d, s));
     AssocArgs a{};
     a.g = v->g;
     a.b = v->b;
@@ -633,7 +644,25 @@ int associate_impl(semtsdf_vol* v, uint8_t* mask_d, const float E[16], hipStream
                 order_n = n;
             }
         }
-        HIPC(launch_march_fused(a, r, s));
+        FramePre pre{};
+        if (fold) {
+            const DepthPyramid& pyr = v->fs[v->next_set].pyr;  // the set the caller's integrate uses next
+            pre.mask = mask_d;
+            pre.npx = (int)npx(v);
+            pre.T = v->tables_d;
+            pre.nms = std::min(64, (pre.npx + 255) / 256);
+            pre.depth = pre_depth;
+            pre.rgb = pre_rgb;
+            pre.pmask = mask_d;
+            pre.w = v->p.width;
+            pre.h = v->p.height;
+            pre.scale = v->p.depth_scale;
+            pre.vec = depth_pyramid_vec(pre_depth, pre_rgb, mask_d, v->p.width, pyr);
+            pre.pyr = pyr;
+            pre.list_count = v->fs[v->next_set].list_count;
+            pre.npy = pyr.w1 * pyr.h1;
+        }
+        HIPC(launch_march_fused(a, r, pre, s));
         v->n_render++;
     } else {
         HIPC(launch_assoc_march(a, s));
@@ -1303,14 +1332,20 @@ static int parse_frame_dev_impl(semtsdf_vol* v, const uint16_t* depth_d, const u
     // beside the march (it reads only the frame's inputs), from the work queued so far on s
     // (the mask statistics stay on s: on the prep stream they slowed the fused view + march
     // launch, 2.45 -> 2.20 k frames/s same-box, profiles/r03/s2/ab_pipeline_mask_stats.txt)
-    const bool overlap_prep = SEMTSDF_OVERLAP_PREP && sem && v->n_obs > 0 && !integrate_after_event;
+    // fused view with the frame's mask statistics and depth pyramid folded into the march's
+    // launch (SEMTSDF_FRAME_FOLD): everything on s, no prep-stream events
+    static const char* ff_env = getenv("SEMTSDF_FRAME_FOLD");
+    static const bool ff_on = ff_env ? atoi(ff_env) != 0 : SEMTSDF_FRAME_FOLD_DEFAULT;
+    const bool fold = ff_on && fused && !integrate_after_event;
+    const bool overlap_prep = !fold && SEMTSDF_OVERLAP_PREP && sem && v->n_obs > 0 && !integrate_after_event;
     if (overlap_prep) {
         if (!v->in_ev) HIPC(hipEventCreateWithFlags(&v->in_ev, order_event_flags()));
         HIPC(hipEventRecord(v->in_ev, s));
     }
     if (sem) {
         if (v->n_obs > 0) {
-            int rc = associate_impl(v, mask_d, E, s, false, true, fused ? view : nullptr);
+            int rc = associate_impl(v, mask_d, E, s, false, true, fused ? view : nullptr, fold ? depth_d : nullptr,
+                                    fold ? rgb_d : nullptr);
             if (rc) return rc;
         } else {
             if (int rc = tables_ready(v, s)) return rc;
@@ -1322,7 +1357,7 @@ static int parse_frame_dev_impl(semtsdf_vol* v, const uint16_t* depth_d, const u
     // other streams (a live render) finish first; the association above, a read, may overlap them
     if (integrate_after_event) HIPC(hipStreamWaitEvent(s, (hipEvent_t)integrate_after_event, 0));
     int rc = integrate_impl(v, depth_d, rgb_d, sem ? mask_d : nullptr, nullptr, E, s, overlap_prep,
-                            overlap_prep ? v->in_ev : nullptr, overlap_prep);
+                            overlap_prep ? v->in_ev : nullptr, overlap_prep, fold);
     if (rc) return relabel_unconsumed(v, mask_d, s, rc);
     v->n_obs++;
     // the next frame's association (and a live view) march this state: refresh the

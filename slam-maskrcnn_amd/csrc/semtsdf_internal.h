@@ -333,7 +333,26 @@ hipError_t launch_first_frame_objs(const AssocTables* t, int* num_objs_dev, hipS
 hipError_t launch_relabel(uint8_t* mask, int npx, const AssocDecision* d, hipStream_t s);
 hipError_t launch_relabel_records(uint8_t* mask, int w, int h, const DepthPyramid& p, const AssocDecision* d, hipStream_t s);
 hipError_t launch_render(const RenderArgs& a, hipStream_t s);
-hipError_t launch_march_fused(const AssocArgs& aa, const RenderArgs& ra, hipStream_t s);
+// Work of the frame folded into the fused march's launch (blocks before the march tiles): nms
+// blocks of mask statistics (k_mask_stats) and npy = pyr.w1 * pyr.h1 prepass tiles
+// (k_depth_pyramid, raw labels); nms = npy = 0: none.
+struct FramePre {
+    const uint8_t* mask;
+    int npx;
+    AssocTables* T;
+    int nms;
+    const uint16_t* depth;
+    const uint8_t* rgb;
+    uint8_t* pmask;
+    int w, h;
+    float scale;
+    int vec;
+    DepthPyramid pyr;
+    unsigned* list_count;
+    int npy;
+};
+hipError_t launch_march_fused(const AssocArgs& aa, const RenderArgs& ra, const FramePre& pre, hipStream_t s);
+int depth_pyramid_vec(const uint16_t* depth, const uint8_t* rgb, const uint8_t* mask, int w, const DepthPyramid& p);
 hipError_t launch_copy_host(const void* src, void* dst, size_t n16, hipStream_t s);
 // chunk [v0, v0+nv) of the bin-major histogram <-> voxel-major [nv][32] staging buffer
 hipError_t launch_hist_chunk_to_vm(const uint32_t* bm, uint32_t* vm, const VolGeom& g, uint64_t v0, uint64_t nv,

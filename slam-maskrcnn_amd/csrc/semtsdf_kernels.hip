@@ -576,11 +576,11 @@ hipError_t launch_fill_volume(const VolGeom& g, const VolBufs& b, uint32_t flags
 // ------------------------------------------------------------------------------------
 // lut (optional): the association's relabel table (k_relabel folded in): labels are mapped
 // through it and the relabelled mask is written back in place.
-__global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restrict__ depth, const uint8_t* __restrict__ rgb,
-                                                       uint8_t* mask, int w, int h, float scale,
-                                                       int vec, DepthPyramid p, unsigned* list_count,
-                                                       const uint8_t* __restrict__ lut) {
-    const int tx = blockIdx.x, ty = blockIdx.y;
+// One 32x32-pixel tile (tx, ty) of the prepass, a whole workgroup (k_depth_pyramid, and the
+// prepass blocks of k_march_fused).
+__device__ __forceinline__ void pyramid_tile(const uint16_t* __restrict__ depth, const uint8_t* __restrict__ rgb,
+                                             uint8_t* mask, int w, int h, float scale, int vec, const DepthPyramid& p,
+                                             unsigned* list_count, const uint8_t* __restrict__ lut, int tx, int ty) {
     const int t = threadIdx.x;
     __shared__ uint32_t s_lut[64];
     if (lut) {  // uniform
@@ -674,11 +674,23 @@ __global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restric
                                           max(max(s_z[0], s_z[1]), max(s_z[2], s_z[3])));
 }
 
+__global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restrict__ depth, const uint8_t* __restrict__ rgb,
+                                                       uint8_t* mask, int w, int h, float scale,
+                                                       int vec, DepthPyramid p, unsigned* list_count,
+                                                       const uint8_t* __restrict__ lut) {
+    pyramid_tile(depth, rgb, mask, w, h, scale, vec, p, list_count, lut, (int)blockIdx.x, (int)blockIdx.y);
+}
+
+// Whether the prepass may use its vector path (4-pixel rows aligned).
+int depth_pyramid_vec(const uint16_t* depth, const uint8_t* rgb, const uint8_t* mask, int w, const DepthPyramid& p) {
+    return (w % 4 == 0) && ((uintptr_t)depth % 8 == 0) && ((uintptr_t)p.px % 16 == 0) && (!rgb || (uintptr_t)rgb % 4 == 0) &&
+           (!mask || (uintptr_t)mask % 4 == 0);
+}
+
 hipError_t launch_depth_pyramid(const uint16_t* depth, const uint8_t* rgb, uint8_t* mask, int w, int h,
                                 float scale, const DepthPyramid& p, unsigned* list_count, hipStream_t s,
                                 const uint8_t* lut) {
-    const bool vec = (w % 4 == 0) && ((uintptr_t)depth % 8 == 0) && ((uintptr_t)p.px % 16 == 0) && (!rgb || (uintptr_t)rgb % 4 == 0) &&
-                     (!mask || (uintptr_t)mask % 4 == 0);
+    const bool vec = depth_pyramid_vec(depth, rgb, mask, w, p);
     hipLaunchKernelGGL(k_depth_pyramid, dim3(p.w1, p.h1), dim3(256), 0, s, depth, rgb, mask, w, h, scale,
                        vec ? 1 : 0, p, list_count, lut);
     return hipGetLastError();
@@ -2472,14 +2484,17 @@ __device__ __forceinline__ void ray_render(const MarchCamera& c, int x, int y, f
 // mask statistics: max label and first pixel of every label (for the relabel order of
 // tsdf.cu:371-389 and num_objs of tsdf.cu:463-468)
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_mask_stats(const uint8_t* __restrict__ mask, int npx, AssocTables* t) {
+// Block `blk` of `nblk` of the frame's mask statistics (k_mask_stats, and the mask-statistics
+// blocks of k_march_fused).
+__device__ __forceinline__ void mask_stats_block(const uint8_t* __restrict__ mask, int npx, AssocTables* t, int blk,
+                                                 int nblk) {
     __shared__ unsigned s_first[256];
     __shared__ unsigned s_max;
     for (int k = threadIdx.x; k < 256; k += 256) s_first[k] = 0xFFFFFFFFu;
     if (threadIdx.x == 0) s_max = 0;
     __syncthreads();
     unsigned mx = 0;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < npx; i += gridDim.x * blockDim.x) {
+    for (int i = blk * 256 + (int)threadIdx.x; i < npx; i += nblk * 256) {
         const unsigned m = mask[i];
         mx = max(mx, m);
         if (m) atomicMin(&s_first[m], (unsigned)i);
@@ -2504,6 +2519,10 @@ __global__ __launch_bounds__(256) void k_tables_init(AssocTables* t) {
 hipError_t launch_tables_init(AssocTables* t, hipStream_t s) {
     hipLaunchKernelGGL(k_tables_init, dim3(1), dim3(256), 0, s, t);
     return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_mask_stats(const uint8_t* __restrict__ mask, int npx, AssocTables* t) {
+    mask_stats_block(mask, npx, t, (int)blockIdx.x, (int)gridDim.x);
 }
 
 hipError_t launch_mask_stats(const uint8_t* mask, int npx, AssocTables* t, hipStream_t s) {
@@ -3469,10 +3488,25 @@ template <bool OCT>
 #define SEMTSDF_FUSED_WPE 4  // 4 waves per SIMD: at most 128 VGPRs (the association's per-pixel output put it at 131)
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_FUSED_WPE))) void k_march_fused(
-    AssocArgs aa, RenderArgs ra, int na, int nr) {
+    AssocArgs aa, RenderArgs ra, FramePre pre, int na, int nr) {
     __shared__ AssocLds s;
+    // the frame's mask statistics and prepass tiles first (FramePre: they read only the frame's
+    // inputs; the marches read the volume)
+    const int npre = pre.nms + pre.npy;
+    if ((int)blockIdx.x < npre) {
+        const int pb = (int)blockIdx.x;
+        if (pb < pre.nms) {
+            mask_stats_block(pre.mask, pre.npx, pre.T, pb, pre.nms);
+        } else {
+            const int q = pb - pre.nms;
+            pyramid_tile(pre.depth, pre.rgb, pre.pmask, pre.w, pre.h, pre.scale, pre.vec, pre.pyr, pre.list_count,
+                         nullptr, q % pre.pyr.w1, q / pre.pyr.w1);
+        }
+        return;
+    }
+    const unsigned bt = blockIdx.x - (unsigned)npre;
     // launch order: block b takes tile perm[b] (the previous frame's heaviest first)
-    const int b = aa.tile_perm ? (int)__builtin_amdgcn_readfirstlane(aa.tile_perm[blockIdx.x]) : (int)blockIdx.x;
+    const int b = aa.tile_perm ? (int)__builtin_amdgcn_readfirstlane(aa.tile_perm[bt]) : (int)bt;
     const int m = min(na, nr);
     const uint64_t t0 = aa.tile_cost ? __builtin_amdgcn_s_memrealtime() : 0;
     bool assoc;
@@ -3497,13 +3531,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_FUS
     }
 }
 
-hipError_t launch_march_fused(const AssocArgs& aa, const RenderArgs& ra, hipStream_t s) {
+hipError_t launch_march_fused(const AssocArgs& aa, const RenderArgs& ra, const FramePre& pre, hipStream_t s) {
     const int na = ((aa.width + 15) / 16) * ((aa.height + 15) / 16);
     const int nr = ((ra.width + 15) / 16) * ((ra.height + 15) / 16);
+    const int grid = pre.nms + pre.npy + na + nr;
     if (oct_maps(aa.b))
-        hipLaunchKernelGGL(k_march_fused<true>, dim3(na + nr), dim3(256), 0, s, aa, ra, na, nr);
+        hipLaunchKernelGGL(k_march_fused<true>, dim3(grid), dim3(256), 0, s, aa, ra, pre, na, nr);
     else
-        hipLaunchKernelGGL(k_march_fused<false>, dim3(na + nr), dim3(256), 0, s, aa, ra, na, nr);
+        hipLaunchKernelGGL(k_march_fused<false>, dim3(grid), dim3(256), 0, s, aa, ra, pre, na, nr);
     return hipGetLastError();
 }
 
