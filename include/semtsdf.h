@@ -335,7 +335,8 @@ int semtsdf_map_words(semtsdf_vol* v, uint64_t* out, uint64_t capacity, uint64_t
 /* enable bit0: record HIP events around kernels; bit1: count touched/gated voxels; bit2: every
  * association row takes the exact f32 path (tests and its cost measurement); bit3: the octant
  * maps by the other of their two implementations (global-memory passes, the default, or LDS
- * line passes; tests: same maps). */
+ * line passes; tests: same maps); bit4: parse_frame_view_dev folds the frame's mask statistics
+ * and depth pyramid into its march launch (SEMTSDF_FRAME_FOLD; tests: same results). */
 int semtsdf_set_instrumentation(semtsdf_vol* v, int enable);
 int semtsdf_get_timing(semtsdf_vol* v, semtsdf_timing* out); /* synchronises the stream */
 int semtsdf_reset_timing(semtsdf_vol* v);

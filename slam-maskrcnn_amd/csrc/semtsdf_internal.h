@@ -252,6 +252,11 @@ struct RenderArgs {
     unsigned* ray_stats;     // instrumentation (SEMTSDF_RAY_STATS): per pixel iterations, lookups,
                              // evaluations, skipped samples; per wave start/end ticks after them
     int row0, row1;          // instrumentation (SEMTSDF_RENDER_ROWS): only 16-px tile rows [row0, row1)
+    // k_render launch order (heaviest tiles of the previous render first): each tile's duration
+    // goes to tile_cost[tile], block b takes tile tile_perm[b] (nullptr: identity); the next
+    // order comes from k_tile_order after the render
+    unsigned* tile_cost;
+    const unsigned* tile_perm;
 };
 
 // Z-sharded raycast protocol (k_shard_* in semtsdf_kernels.hip): per-pixel march state.
@@ -352,6 +357,7 @@ struct FramePre {
     int npy;
 };
 hipError_t launch_march_fused(const AssocArgs& aa, const RenderArgs& ra, const FramePre& pre, hipStream_t s);
+hipError_t launch_tile_order(const unsigned* cost, unsigned* perm, int n, hipStream_t s);  // one workgroup
 int depth_pyramid_vec(const uint16_t* depth, const uint8_t* rgb, const uint8_t* mask, int w, const DepthPyramid& p);
 hipError_t launch_copy_host(const void* src, void* dst, size_t n16, hipStream_t s);
 // chunk [v0, v0+nv) of the bin-major histogram <-> voxel-major [nv][32] staging buffer

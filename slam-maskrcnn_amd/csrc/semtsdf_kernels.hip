@@ -2998,16 +2998,18 @@ struct DecideLds {
     float srow[kMaxObjects];  // exact path: the running f32 sum of each flagged row
     unsigned thist[64];       // tile order: bucket counts, then bucket cursors
     unsigned tmax;
+    unsigned fresh_first[256];  // first pixels of the present, unmatched labels (newcount of them)
 };
 
 // The fused march's next launch order from this frame's tile durations: 64 linear cost buckets,
 // heaviest first (LPT), a counting sort in one workgroup.  Order within a bucket is arbitrary;
 // the order never changes results (the association's sums are integer, the render per pixel).
 constexpr int kTileOrderPer = 32;  // tiles per thread of tile_order: launch orders of up to 8192 tiles
-__device__ void tile_order(const unsigned* __restrict__ cost, unsigned* __restrict__ perm, int n, DecideLds& L) {
+__device__ void tile_order(const unsigned* __restrict__ cost, unsigned* __restrict__ perm, int n, unsigned* thist,
+                           unsigned* tmax) {
     const int tid = threadIdx.x;
-    if (tid < 64) L.thist[tid] = 0u;
-    if (tid == 0) L.tmax = 0u;
+    if (tid < 64) thist[tid] = 0u;
+    if (tid == 0) *tmax = 0u;
     unsigned c[kTileOrderPer];
 #pragma unroll
     for (int j = 0; j < kTileOrderPer; ++j) {  // every load in flight together
@@ -3019,28 +3021,40 @@ __device__ void tile_order(const unsigned* __restrict__ cost, unsigned* __restri
     for (int j = 0; j < kTileOrderPer; ++j) mx = max(mx, c[j]);
     for (int off = 32; off > 0; off >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, off, 64));
     __syncthreads();  // the counters' initialisation
-    if ((tid & 63) == 0) atomicMax(&L.tmax, mx);
+    if ((tid & 63) == 0) atomicMax(tmax, mx);
     __syncthreads();
-    const unsigned long long den = (unsigned long long)L.tmax + 1ull;
+    const unsigned long long den = (unsigned long long)*tmax + 1ull;
     unsigned bk[kTileOrderPer];
 #pragma unroll
     for (int j = 0; j < kTileOrderPer; ++j) {
         bk[j] = 63u - (unsigned)(((unsigned long long)c[j] * 64ull) / den);
-        if (tid + 256 * j < n) atomicAdd(&L.thist[bk[j]], 1u);
+        if (tid + 256 * j < n) atomicAdd(&thist[bk[j]], 1u);
     }
     __syncthreads();
     if (tid == 0) {
         unsigned run = 0;
         for (int k = 0; k < 64; ++k) {
-            const unsigned v = L.thist[k];
-            L.thist[k] = run;
+            const unsigned v = thist[k];
+            thist[k] = run;
             run += v;
         }
     }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < kTileOrderPer; ++j)
-        if (tid + 256 * j < n) perm[atomicAdd(&L.thist[bk[j]], 1u)] = (unsigned)(tid + 256 * j);
+        if (tid + 256 * j < n) perm[atomicAdd(&thist[bk[j]], 1u)] = (unsigned)(tid + 256 * j);
+}
+
+__global__ __launch_bounds__(256) void k_tile_order(const unsigned* __restrict__ cost, unsigned* __restrict__ perm, int n) {
+    __shared__ unsigned thist[64];
+    __shared__ unsigned tmax;
+    tile_order(cost, perm, n, thist, &tmax);
+}
+
+hipError_t launch_tile_order(const unsigned* cost, unsigned* perm, int n, hipStream_t s) {
+    if (n <= 0 || n > 256 * kTileOrderPer) return hipSuccess;
+    hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(256), 0, s, cost, perm, n);
+    return hipGetLastError();
 }
 
 __global__ __launch_bounds__(256) void k_assoc_decide(DecideArgs a) {
@@ -3050,21 +3064,31 @@ __global__ __launch_bounds__(256) void k_assoc_decide(DecideArgs a) {
     // an extra last workgroup orders the next fused march's tiles, beside the decision
     const unsigned nwork = gridDim.x - (a.tile_n > 0 ? 1u : 0u);
     if (blockIdx.x >= nwork) {
-        tile_order(a.tile_cost, a.tile_perm, a.tile_n, L);
+        tile_order(a.tile_cost, a.tile_perm, a.tile_n, L.thist, &L.tmax);
         return;
     }
-    const int max_now = min((int)T->max_label + 1, kMaxObjects);
+    // every table word this workgroup reads, loads in flight together (the rows past max_now
+    // hold zeros), and what the last arriver reads besides
+    static_assert(kMaxObjects * kMaxObjects == 4 * 256, "four table entries per thread");
+    const unsigned maxl = T->max_label;
+    const unsigned first_pre = T->first_px[tid];
+    const int num_pre = *a.num_objs_dev;
+    long long Av[4], Cv[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int k = tid + 256 * m, i = k / kMaxObjects, j = k % kMaxObjects;
+        Av[m] = T->t1[i][j] + T->t2[j] - T->t3[i][j];
+        Cv[m] = (long long)T->c1[i] + (long long)T->c2[j] - (long long)T->c3[i][j];
+    }
+    const int max_now = min((int)maxl + 1, kMaxObjects);
     const float thr_f = 3.0f * a.eps;  // tsdf.cu:349, a float product
     const double thr = (double)thr_f;
     // ---- certificate (every workgroup) ----
-    for (int k = tid; k < kMaxObjects * kMaxObjects; k += 256) {
-        const int i = k / kMaxObjects, j = k % kMaxObjects;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int k = tid + 256 * m, i = k / kMaxObjects, j = k % kMaxObjects;
         double lo = 0.0, hi = 0.0, mid = 0.0;
-        if (i >= 1 && j >= 1 && i < max_now) {
-            const long long A = T->t1[i][j] + T->t2[j] - T->t3[i][j];
-            const long long C = (long long)T->c1[i] + (long long)T->c2[j] - (long long)T->c3[i][j];
-            prob_interval(A, C, &lo, &hi, &mid);
-        }
+        if (i >= 1 && j >= 1 && i < max_now) prob_interval(Av[m], Cv[m], &lo, &hi, &mid);
         L.lo[i][j] = lo;
         L.hi[i][j] = hi;
         L.mid[i][j] = mid;
@@ -3174,7 +3198,7 @@ __global__ __launch_bounds__(256) void k_assoc_decide(DecideArgs a) {
         L.prob[i][j] = prob;
     }
     L.rev[tid] = -1;
-    L.first[tid] = T->first_px[tid];
+    L.first[tid] = first_pre;
     if (tid == 0) L.newcount = 0;
     __syncthreads();
     if (tid < kMaxObjects) {
@@ -3204,18 +3228,20 @@ __global__ __launch_bounds__(256) void k_assoc_decide(DecideArgs a) {
         D->assigned_prob[L.map_i[tid]] = (float)L.map_p[tid];
     }
     __syncthreads();
-    const int num = *a.num_objs_dev;
-    // lanes 1..255: a present, unmatched label gets num + (rank of its first pixel)
+    const int num = num_pre;
+    // lanes 1..255: a present, unmatched label gets num + (rank of its first pixel among those
+    // labels; first pixels are distinct), from a compact list of the fresh labels' first pixels
     const bool fresh = tid >= 1 && L.rev[tid] < 0 && L.first[tid] != 0xFFFFFFFFu;
+    if (fresh) L.fresh_first[atomicAdd(&L.newcount, 1)] = L.first[tid];
+    __syncthreads();
     int lut = tid;
     if (tid >= 1 && L.rev[tid] >= 0) {
         lut = L.rev[tid];
     } else if (fresh) {
+        const unsigned mine = L.first[tid];
         int rank = 0;
-        for (int u = 1; u < 256; ++u)
-            rank += (L.rev[u] < 0 && L.first[u] != 0xFFFFFFFFu && L.first[u] < L.first[tid]) ? 1 : 0;
+        for (int u = 0; u < L.newcount; ++u) rank += L.fresh_first[u] < mine ? 1 : 0;
         lut = num + rank;
-        atomicAdd(&L.newcount, 1);
     }
     D->lut[tid] = (unsigned char)lut;
     __syncthreads();
@@ -3475,7 +3501,15 @@ __device__ __forceinline__ void render_tile(const RenderArgs& a, int bx, int by)
 
 template <bool STATS, bool OCT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_MARCH_WPE))) void k_render(RenderArgs a) {
-    render_tile<STATS, OCT>(a, (int)blockIdx.x, (int)blockIdx.y);
+    // launch order (RenderArgs::tile_perm: the previous render's heaviest tiles first)
+    int t = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+    if (a.tile_perm) t = (int)__builtin_amdgcn_readfirstlane(a.tile_perm[t]);
+    const uint64_t t0 = a.tile_cost ? __builtin_amdgcn_s_memrealtime() : 0;
+    render_tile<STATS, OCT>(a, t % (int)gridDim.x, t / (int)gridDim.x);
+    if (a.tile_cost) {  // the tile's duration, all its waves done
+        __syncthreads();
+        if (threadIdx.x == 0) a.tile_cost[t] = (unsigned)min(__builtin_amdgcn_s_memrealtime() - t0, (uint64_t)0xFFFFFFFFu);
+    }
 }
 
 // A render of the volume and the association march of the next frame in one launch: both

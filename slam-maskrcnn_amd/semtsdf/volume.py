@@ -281,11 +281,14 @@ class Volume:
 
     # ---- instrumentation
     def set_instrumentation(self, events: bool = True, count: bool = False, force_exact: bool = False,
-                            other_map_passes: bool = False):
+                            other_map_passes: bool = False, frame_fold: bool = False):
         """events: HIP-event kernel timing; count: touched/gated voxel counters; force_exact: every
         association row decided from its exact f32 pixel-order sums (tests, cost measurement);
-        other_map_passes: the octant maps by the other of their two implementations (tests: same maps)."""
-        flags = (1 if events else 0) | (2 if count else 0) | (4 if force_exact else 0) | (8 if other_map_passes else 0)
+        other_map_passes: the octant maps by the other of their two implementations (tests: same maps);
+        frame_fold: parse_frame_view_dev folds the frame's mask statistics and depth pyramid into its
+        march launch (tests: same results)."""
+        flags = ((1 if events else 0) | (2 if count else 0) | (4 if force_exact else 0) | (8 if other_map_passes else 0)
+                 | (16 if frame_fold else 0))
         L.check(L.load().semtsdf_set_instrumentation(self._h, flags))
 
     def map_words(self):

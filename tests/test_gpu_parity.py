@@ -806,6 +806,8 @@ def test_parse_frame_view_fused_equals_serial(S, stream, D):
                                  L.PLACE_SFM)
         p.flags = L.F_SEMANTIC | L.F_GATE_COLOR
         vol = semtsdf.Volume(p, 0)
+        if fused == "fold":  # the frame's mask statistics and depth pyramid in the march launch
+            vol.set_instrumentation(events=False, frame_fold=True)
         masks = [m.clone() for m in m_in]
         torch.cuda.synchronize()
         views = []
@@ -838,7 +840,7 @@ def test_parse_frame_view_fused_equals_serial(S, stream, D):
 
     (va, ma), sa = run(False)
     assert sum(int(v.count_nonzero()) for v in va[::2]) > 0
-    for variant in (True, "host"):
+    for variant in (True, "fold", "host"):
         (vb, mb), sb = run(variant)
         for x, y in zip(va + ma, vb + mb):
             assert torch.equal(x, y), variant
