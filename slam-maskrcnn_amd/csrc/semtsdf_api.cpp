@@ -31,9 +31,6 @@ using namespace semtsdf;
 #ifndef SEMTSDF_FRAME_FOLD_DEFAULT
 #define SEMTSDF_FRAME_FOLD_DEFAULT 0  // env SEMTSDF_FRAME_FOLD=0/1 overrides (A/B)
 #endif
-#ifndef SEMTSDF_RENDER_LPT_DEFAULT
-#define SEMTSDF_RENDER_LPT_DEFAULT 1  // env SEMTSDF_RENDER_LPT=0/1 overrides (A/B)
-#endif
 #ifndef SEMTSDF_MARCH_LPT_DEFAULT
 #define SEMTSDF_MARCH_LPT_DEFAULT 1  // env SEMTSDF_MARCH_LPT=0/1 overrides (A/B)
 #endif
@@ -147,9 +144,6 @@ struct semtsdf_vol {
     unsigned* tile_cost_d = nullptr;
     unsigned* tile_perm_d = nullptr;
     int tile_cap = 0, tile_n = 0;
-    unsigned* rtile_cost_d = nullptr;  // the same for the renders (k_render, ordered by k_tile_order)
-    unsigned* rtile_perm_d = nullptr;
-    int rtile_cap = 0, rtile_n = 0;
     bool tables_clean = false;     // tables_d holds the cleared state (left by k_assoc_decide)
     // instrumentation
     int instr = 0;
@@ -189,7 +183,7 @@ void free_all(semtsdf_vol* v) {
                     v->fs[1].pyr.l0, v->fs[1].pyr.l1, v->tables_d, v->decision_d,
                     v->num_objs_d, v->probs_d, v->box_d, v->palette_d, v->render_d, v->render_t_d,
                     v->counters_d, v->ray_state_d, v->fs[0].unit_list, v->fs[0].list_count, v->fs[1].unit_list,
-                    v->fs[1].list_count, v->rcp_table_d, v->wtrace_d, v->exact_d, v->px.bits, v->px.p, v->tile_cost_d, v->tile_perm_d, v->rtile_cost_d, v->rtile_perm_d};
+                    v->fs[1].list_count, v->rcp_table_d, v->wtrace_d, v->exact_d, v->px.bits, v->px.p, v->tile_cost_d, v->tile_perm_d};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (v->decision_h) (void)hipHostFree(v->decision_h);
@@ -1699,8 +1693,6 @@ static int render_args(semtsdf_vol* v, const float s2w[16], const float c[3], in
     return SEMTSDF_OK;
 }
 
-static int launch_render_ordered(semtsdf_vol* v, RenderArgs& a, hipStream_t s);
-
 static int raycast_impl(semtsdf_vol* v, const float s2w[16], const float c[3], int mode, uint8_t* out_bgr_d,
                         float* out_t_d, hipStream_t s) {
     RenderArgs a;
@@ -1717,7 +1709,7 @@ static int raycast_impl(semtsdf_vol* v, const float s2w[16], const float c[3], i
     static const char* rows = getenv("SEMTSDF_RENDER_ROWS");  // instrumentation: "r0,r1"
     if (rows && sscanf(rows, "%d,%d", &a.row0, &a.row1) != 2) a.row0 = a.row1 = 0;
     timing_begin(v, v->ev_render, s, &ep);
-    if (int rc = launch_render_ordered(v, a, s)) return rc;
+    HIPC(launch_render(a, s));
     timing_end(v, v->ev_render, s, &ep);
     if (rs_path) {
         std::vector<unsigned> h(rs_words);
@@ -1733,41 +1725,11 @@ static int raycast_impl(semtsdf_vol* v, const float s2w[16], const float c[3], i
     return SEMTSDF_OK;
 }
 
-// A render in the launch order of the previous render of the same size (heaviest tiles first;
-// SEMTSDF_RENDER_LPT=0 disables), then the order for the next one (k_tile_order).
-static int launch_render_ordered(semtsdf_vol* v, RenderArgs& a, hipStream_t s) {
-    static const char* lpt = getenv("SEMTSDF_RENDER_LPT");
-    static const bool on = lpt ? atoi(lpt) != 0 : SEMTSDF_RENDER_LPT_DEFAULT;
-    const int n = ((a.width + 15) / 16) * ((a.height + 15) / 16);
-    // only on the volume's own stream: renders there run one after another, so none reads the
-    // permutation while k_tile_order rewrites it
-    const bool order = on && s == v->stream && n <= 8192 && !a.ray_stats && a.row1 <= 0;
-    if (order && n > v->rtile_cap) {
-        for (unsigned** q : {&v->rtile_cost_d, &v->rtile_perm_d})
-            if (*q) { (void)hipFree(*q); v->device_bytes -= (size_t)v->rtile_cap * sizeof(unsigned); *q = nullptr; }
-        v->rtile_cap = 0;
-        v->rtile_n = 0;
-        if (int rc = dev_alloc(v, (void**)&v->rtile_cost_d, (size_t)n * sizeof(unsigned))) return rc;
-        if (int rc = dev_alloc(v, (void**)&v->rtile_perm_d, (size_t)n * sizeof(unsigned))) return rc;
-        v->rtile_cap = n;
-    }
-    if (order) {
-        a.tile_cost = v->rtile_cost_d;
-        a.tile_perm = v->rtile_n == n ? v->rtile_perm_d : nullptr;  // sizes changed: identity
-    }
-    HIPC(launch_render(a, s));
-    if (order) {
-        HIPC(launch_tile_order(v->rtile_cost_d, v->rtile_perm_d, n, s));
-        v->rtile_n = n;
-    }
-    return SEMTSDF_OK;
-}
-
 static int launch_view(semtsdf_vol* v, const RenderArgs& view, hipStream_t s) {
     if (int rc = ensure_bmin(v, s)) return rc;
     RenderArgs a = view;
     a.b = v->b;
-    if (int rc = launch_render_ordered(v, a, s)) return rc;
+    HIPC(launch_render(a, s));
     v->n_render++;
     return SEMTSDF_OK;
 }

@@ -204,7 +204,7 @@ struct DecideArgs {
     int npx;
     int force_exact;        // debug/tests: every present row takes the exact path
     int certify_only;       // write the rows needing the exact path to D->exact_missing, decide nothing
-    const unsigned* tile_cost;  // tile_n > 0: workgroup 0 orders the fused march's tiles by cost
+    const unsigned* tile_cost;  // tile_n > 0: an extra workgroup orders the fused march's tiles by cost
     unsigned* tile_perm;
     int tile_n;
 };
@@ -252,11 +252,6 @@ struct RenderArgs {
     unsigned* ray_stats;     // instrumentation (SEMTSDF_RAY_STATS): per pixel iterations, lookups,
                              // evaluations, skipped samples; per wave start/end ticks after them
     int row0, row1;          // instrumentation (SEMTSDF_RENDER_ROWS): only 16-px tile rows [row0, row1)
-    // k_render launch order (heaviest tiles of the previous render first): each tile's duration
-    // goes to tile_cost[tile], block b takes tile tile_perm[b] (nullptr: identity); the next
-    // order comes from k_tile_order after the render
-    unsigned* tile_cost;
-    const unsigned* tile_perm;
 };
 
 // Z-sharded raycast protocol (k_shard_* in semtsdf_kernels.hip): per-pixel march state.
@@ -357,7 +352,6 @@ struct FramePre {
     int npy;
 };
 hipError_t launch_march_fused(const AssocArgs& aa, const RenderArgs& ra, const FramePre& pre, hipStream_t s);
-hipError_t launch_tile_order(const unsigned* cost, unsigned* perm, int n, hipStream_t s);  // one workgroup
 int depth_pyramid_vec(const uint16_t* depth, const uint8_t* rgb, const uint8_t* mask, int w, const DepthPyramid& p);
 hipError_t launch_copy_host(const void* src, void* dst, size_t n16, hipStream_t s);
 // chunk [v0, v0+nv) of the bin-major histogram <-> voxel-major [nv][32] staging buffer

@@ -3045,18 +3045,6 @@ __device__ void tile_order(const unsigned* __restrict__ cost, unsigned* __restri
         if (tid + 256 * j < n) perm[atomicAdd(&thist[bk[j]], 1u)] = (unsigned)(tid + 256 * j);
 }
 
-__global__ __launch_bounds__(256) void k_tile_order(const unsigned* __restrict__ cost, unsigned* __restrict__ perm, int n) {
-    __shared__ unsigned thist[64];
-    __shared__ unsigned tmax;
-    tile_order(cost, perm, n, thist, &tmax);
-}
-
-hipError_t launch_tile_order(const unsigned* cost, unsigned* perm, int n, hipStream_t s) {
-    if (n <= 0 || n > 256 * kTileOrderPer) return hipSuccess;
-    hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(256), 0, s, cost, perm, n);
-    return hipGetLastError();
-}
-
 __global__ __launch_bounds__(256) void k_assoc_decide(DecideArgs a) {
     __shared__ DecideLds L;
     AssocTables* T = a.T;
@@ -3501,15 +3489,7 @@ __device__ __forceinline__ void render_tile(const RenderArgs& a, int bx, int by)
 
 template <bool STATS, bool OCT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SEMTSDF_MARCH_WPE))) void k_render(RenderArgs a) {
-    // launch order (RenderArgs::tile_perm: the previous render's heaviest tiles first)
-    int t = (int)(blockIdx.y * gridDim.x + blockIdx.x);
-    if (a.tile_perm) t = (int)__builtin_amdgcn_readfirstlane(a.tile_perm[t]);
-    const uint64_t t0 = a.tile_cost ? __builtin_amdgcn_s_memrealtime() : 0;
-    render_tile<STATS, OCT>(a, t % (int)gridDim.x, t / (int)gridDim.x);
-    if (a.tile_cost) {  // the tile's duration, all its waves done
-        __syncthreads();
-        if (threadIdx.x == 0) a.tile_cost[t] = (unsigned)min(__builtin_amdgcn_s_memrealtime() - t0, (uint64_t)0xFFFFFFFFu);
-    }
+    render_tile<STATS, OCT>(a, (int)blockIdx.x, (int)blockIdx.y);
 }
 
 // A render of the volume and the association march of the next frame in one launch: both

@@ -103,3 +103,4 @@ def test_lds_map_passes_equal_global_passes_and_definition(S, stream, dims):
         v.close()
     # the maps are not trivial: some bricks skippable, some not
     assert 0.0 < skippable[-1] < 1.0, skippable
+
