@@ -1142,6 +1142,47 @@ def test_async_prepass_integrate_matches_oracle(S, oracle, stream):
     vol.close()
 
 
+def test_async_prepass_sharded_equals_sync(S, oracle, stream):
+    """The bench's C4 step on a Z-slab shard (semtsdf_integrate_dev_async, the prepass beside
+    the previous integrate) leaves every local array bit-identical to the synchronous
+    integrate of the same shard."""
+    from semtsdf.volume import DeviceBuffer
+
+    st, frames = stream
+    semtsdf, L = S
+    dims = (72, 64, 96)
+    p, vol, g, ost = make(S, oracle, dims, frames[0], 0x3)
+    vol.close()
+    npx = 640 * 480
+    F = len(frames) - 1
+    d, r, m = DeviceBuffer(F * npx * 2), DeviceBuffer(F * npx * 3), DeviceBuffer(F * npx)
+    for i, fr in enumerate(frames[1:]):
+        d.upload(fr.depth, None, i * npx * 2)
+        r.upload(fr.rgb, None, i * npx * 3)
+        m.upload(fr.gt_ids, None, i * npx)
+    for sidx in range(2):
+        q = semtsdf.default_params(64, KI, 640, 480)
+        for fld in ("dim", "vol_start", "vol_end", "voxel", "K", "Kinv"):
+            getattr(q, fld)[:] = getattr(p, fld)[:]
+        q.mu, q.flags = p.mu, p.flags
+        q.z_nshards, q.z_shard, q.z_chunk = 2, sidx, 15
+        va, vb = semtsdf.Volume(q, 0), semtsdf.Volume(q, 0)
+        for i in [0, 1, 2, 3, 4, 0, 1, 2]:
+            E = (frames[1 + i].w2c @ frames[0].c2w).astype(np.float32)
+            va.integrate_dev_async(d.ptr + i * npx * 2, r.ptr + i * npx * 3, m.ptr + i * npx, E)
+            vb.integrate_dev(d.ptr + i * npx * 2, r.ptr + i * npx * 3, m.ptr + i * npx, E)
+        va.sync()
+        vb.sync()
+        xa, xb = va.download(hist=True), vb.download(hist=True)
+        assert np.count_nonzero(xb["wt"]) > 0
+        for key in ("sdf", "wt", "color", "hist"):
+            assert np.array_equal(xa[key].view(np.uint8), xb[key].view(np.uint8)), (sidx, key)
+        va.close()
+        vb.close()
+    for b in (d, r, m):
+        b.free()
+
+
 def test_kernel_copy_from_pinned_and_refusal_of_pageable(S):
     """semtsdf_memcpy kind 4 (the copy kernel the live loop uploads frames with) copies from
     pinned host memory bit for bit, and refuses pageable host memory (a kernel reading it would
