@@ -1087,6 +1087,10 @@ def main():
                     "(semtsdf_integrate_dev_async)") if args.async_prepass else "in front of the frame's integrate",
         "integrate_kernel_ms": round(kern_ms, 4),
         "prep_ms": round(prep_ms, 4),
+        "prep_exposed_ms": round(elapsed * 1e3 / args.steps - kern_ms, 4),
+        "prep_note": ("prep_ms: the prepass kernels' own span, overlapping the previous integrate on the prep stream; "
+                      "prep_exposed_ms: step time not covered by the integrate kernel") if args.async_prepass else
+                     "prep_ms: the prepass kernels in front of the integrate",
         "touched_per_frame": int(touched),
         "gated_per_frame": int(gated),
         "live_units_per_frame": int(live_units),
