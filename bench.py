@@ -667,7 +667,7 @@ def run_mask_overlap(semtsdf, L, p, local, frames, f0, n_frames=48, n_warm=4, ge
 
 
 # ----------------------------------------------------------------------------- C2
-def run_c2(semtsdf, L, local, frames, f0, K=30, warmup=3, traffic_json=None):
+def run_c2(semtsdf, L, local, frames, f0, K=30, warmup=3, traffic_json=None, async_prepass=True):
     """C2: 256^3 TSDF + colour (NumPy rule: int32 colour, no gate), synthetic stream."""
     D = 256
     p = place(semtsdf, L, D, f0)
@@ -678,7 +678,10 @@ def run_c2(semtsdf, L, local, frames, f0, K=30, warmup=3, traffic_json=None):
 
     def step(k):
         i = k % len(frames)
-        vol.integrate_dev(dbuf.ptr + i * NPX * 2, rbuf.ptr + i * NPX * 3, None, Es[i])
+        if async_prepass:  # as the C3 step: the prepass beside the previous frame's integrate
+            vol.integrate_dev_async(dbuf.ptr + i * NPX * 2, rbuf.ptr + i * NPX * 3, None, Es[i])
+        else:
+            vol.integrate_dev(dbuf.ptr + i * NPX * 2, rbuf.ptr + i * NPX * 3, None, Es[i])
 
     elapsed, tm, tc = timed_integrate(vol, step, K, warmup)
     kern_ms = tm.integrate_ms / max(tm.n_integrate, 1)
@@ -708,6 +711,7 @@ def run_c2(semtsdf, L, local, frames, f0, K=30, warmup=3, traffic_json=None):
         "ms_per_step": round(elapsed * 1e3 / K, 4),
         "integrate_kernel_ms": round(kern_ms, 4),
         "frames_per_s_upload_integrate": round(K / t_up, 1),
+        "prepass": "beside the previous integrate (semtsdf_integrate_dev_async)" if async_prepass else "in front",
         "touched_per_frame": int(touched),
         "live_units_per_frame": int(tc.bricks / K),
         "roofline": {"bound": "hbm", "achieved": round(b / (kern_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
@@ -1001,7 +1005,8 @@ def main():
         elif args.only == "masks":
             r = run_mask_overlap(semtsdf, L, p, local, frames, f0)
         elif args.only == "c2":
-            r = run_c2(semtsdf, L, local, frames, f0, args.steps, args.warmup, args.c2_traffic_json)
+            r = run_c2(semtsdf, L, local, frames, f0, args.steps, args.warmup, args.c2_traffic_json,
+                       args.async_prepass)
         else:
             r = run_c4_single(semtsdf, L, local, frames, f0, args.steps, args.warmup, args.async_prepass)
         print(json.dumps({"only": args.only, args.only: r}), flush=True)
@@ -1055,7 +1060,8 @@ def main():
     if not args.no_pipeline and emu_world <= 1:
         pipeline, orbit = run_pipeline(semtsdf, L, p, local)
         masks = run_mask_overlap(semtsdf, L, p, local, frames, f0)
-        c2 = run_c2(semtsdf, L, local, frames, f0, args.steps, args.warmup, args.c2_traffic_json)
+        c2 = run_c2(semtsdf, L, local, frames, f0, args.steps, args.warmup, args.c2_traffic_json,
+                       args.async_prepass)
         if not args.no_c4:
             c4 = run_c4_single(semtsdf, L, local, frames, f0, args.steps, args.warmup, args.async_prepass)
     copy_bw = copy_bandwidth(local) if not args.no_pipeline else None
