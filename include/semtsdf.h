@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SEMTSDF_ABI_VERSION 10
+#define SEMTSDF_ABI_VERSION 11
 #define SEMTSDF_MAX_OBJECTS 32 /* tsdf.cuh:4 */
 
 /* ---- status codes ------------------------------------------------------------ */
@@ -49,6 +49,15 @@ extern "C" {
 #define SEMTSDF_F_COLOR_I32 0x4u  /* colour int32x3 (TSDF_Python tsdf.py:50) instead of u8x3 */
 #define SEMTSDF_F_VOTE 0x8u       /* label vote tsdf_cls/tsdf_cls_cnt (TSDF_Python/tsdf.cu:48-57) */
 #define SEMTSDF_F_NO_CULL 0x10u   /* disable brick frustum/depth culling (debug; same results) */
+/* Instance ids past the histogram (a deviation, opt-in).  The reference hands every unmatched
+ * label the id num_objs++ (tsdf.cu:379-383) without a bound, and its integrate then counts an
+ * id >= 32 in the bins of the next voxel (tsdf.cu:61, out of bounds).  By default the engine
+ * keeps the reference's ids (the u8 mask holds them modulo 256, as mask_ptr[i] = num_objs does),
+ * drops the histogram votes of ids >= 32 (counted in semtsdf_state::label_votes_dropped) and
+ * reports SEMTSDF_ERR_LABEL from the synchronous calls of the frame that minted one; the handle
+ * stays usable.  With SEMTSDF_F_ID_SATURATE an unmatched label that would get an id >= 32 is
+ * relabelled 0 (background) instead, num_objs stops at 32 and no error is reported. */
+#define SEMTSDF_F_ID_SATURATE 0x20u
 
 /* ---- placement modes (a1) ---------------------------------------------- */
 #define SEMTSDF_PLACE_SFM 0    /* SfM tsdf.cu:173-199: f32, depth->u8 saturates, mean in metres */
@@ -70,7 +79,8 @@ typedef struct semtsdf_params {
     float depth_scale;       /* raw depth units per metre: 5000 (tsdf.cu:49) */
     float gate;              /* colour/histogram gate on f: 0.99 (tsdf.cu:57) */
     float box_thresh;        /* association box-mask threshold: 0.3 (tsdf.cu:128) */
-    float prior_mrcnn_err_rate; /* Configuration::prior_mrcnn_err_rate = 0.05 (configuration.h:8) */
+    float prior_mrcnn_err_rate; /* Configuration::prior_mrcnn_err_rate = 0.05 (configuration.h:8);
+                                   must lie in [2^-10, 1) */
     float duplicate_thresh;  /* Configuration::duplicate_thresh = 0.5 (configuration.h:9; unused upstream) */
     uint32_t flags;          /* SEMTSDF_F_* */
     /* Z-slab sharding.  The global z axis is cut into chunks of z_chunk
@@ -89,6 +99,8 @@ typedef struct semtsdf_state {
     int32_t local_dim[3];    /* stored dims on this device (z includes halo planes) */
     uint64_t local_voxels;   /* local_dim product */
     uint64_t device_bytes;   /* bytes of device memory owned by the handle */
+    uint64_t label_votes_dropped; /* histogram votes of ids >= 32 dropped by the integrate since the
+                                     last reset (SEMTSDF_F_ID_SATURATE) */
 } semtsdf_state;
 
 /* Per-frame association result (filter_overlaps tsdf.cu:304-416). */
@@ -101,6 +113,9 @@ typedef struct semtsdf_assoc_stats {
     uint32_t exact_rows;                /* bit i: current label i was decided from its exact f32
                                            pixel-order sums (the rows the fixed-point certificate
                                            could not decide) */
+    uint32_t reject_rows;               /* bit i: the certificate proved every candidate of label i
+                                           at or below 3 * prior for every f32 rounding of its sums:
+                                           rejected (a new id) without the exact path */
 } semtsdf_assoc_stats;
 
 /* Accumulated kernel timings (HIP events on the launch stream). */
@@ -250,7 +265,8 @@ int semtsdf_raycast_dev(semtsdf_vol* v, const float s2w[16], const float c[3], i
  *                   assoc_apply(reduced, mask, stats)         -- decide + relabel
  * The result is bit-identical to the single-volume raycast / association. */
 #define SEMTSDF_RAY_ASSOC 2
-#define SEMTSDF_ASSOC_PARTIAL_LEN 3168 /* int64 words: 32x32 t1, t3; 32 t2, c1, c2; 32x32 c3 */
+#define SEMTSDF_ASSOC_PARTIAL_LEN 3168 /* int64 words: 32x32 t1, t3; 32 t2, c1, c2; 32x32 c3
+                                         (the unused c1[0] word: the largest positive term) */
 /* exchange between protocol steps: every shard's records concatenated in shard order
  * (all-gather; gathered = z_nshards * record_bytes), or their element-wise minimum as
  * little-endian int64 (all-reduce MIN; gathered = record_bytes), 1/z_nshards of the bytes. */

@@ -60,7 +60,8 @@ def lib():
         _lib.oracle_integrate_slab.restype = None
         _lib.oracle_march_probs.argtypes = [P, P, P, P, C.c_int, C.c_int, P, P, C.c_float, P, P, C.c_int, C.c_int]
         _lib.oracle_march_probs.restype = None
-        _lib.oracle_filter_overlaps.argtypes = [P, P, P, C.c_int, C.c_int, C.c_uint32, C.c_float, C.c_int, P, P, P, P]
+        _lib.oracle_filter_overlaps.argtypes = [P, P, P, C.c_int, C.c_int, C.c_uint32, C.c_float, C.c_int, P, P, P, P,
+                                                C.c_int]
         _lib.oracle_filter_overlaps.restype = C.c_int
         _lib.oracle_render.argtypes = [P, P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P, P, C.c_int,
                                        C.c_int]
@@ -198,8 +199,10 @@ def march_probs(g: OGeom, Kinv16, E16, W, H, sdf, hist, box_thresh=0.3):
     return probs, box
 
 
-def filter_overlaps(probs, box, mask, n_obs, num_objs, eps=0.05, precision=0, table=None):
+def filter_overlaps(probs, box, mask, n_obs, num_objs, eps=0.05, precision=0, table=None, id_policy=0):
     """Relabels a copy of mask; returns (mask, num_objs, max_obj_now, assigned_prev, assigned_prob).
+    id_policy 0: the reference's unbounded new ids (held in the u8 mask modulo 256); 1: new ids
+    >= 32 become background (the engine's opt-in SEMTSDF_F_ID_SATURATE).
     precision 0: the reference's f32 rule (logf terms summed in pixel order, expf of the f32
     mean, tsdf.cu:312-349), which the device reproduces; 1: double accumulation (tests only).
     table: optional float64 [32, 32] that receives every candidate probability (row = current
@@ -214,7 +217,8 @@ def filter_overlaps(probs, box, mask, n_obs, num_objs, eps=0.05, precision=0, ta
         table[:] = 0.0
     mx = lib().oracle_filter_overlaps(_p(np.ascontiguousarray(probs, np.float32)),
                                       _p(np.ascontiguousarray(box, np.uint8)), _p(m), W, H, int(n_obs), eps,
-                                      int(precision), C.byref(no), _p(prev), _p(prob), _p(table))
+                                      int(precision), C.byref(no), _p(prev), _p(prob), _p(table),
+                                      int(id_policy))
     return m, no.value, mx, prev, prob
 
 

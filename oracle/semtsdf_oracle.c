@@ -343,10 +343,13 @@ void oracle_march_probs(const int32_t* dims, const float* geo, const float* Kinv
  *   used by the tests to find the cases that f32 rounding decides.
  * mask is relabelled in place; *num_objs is updated.  assigned_prev[i] = previous id
  * matched by current label i (or -1), assigned_prob[i] its probability.
+ * id_policy 0: new ids num_objs++ without a bound, stored in the u8 mask modulo 256 (tsdf.cu:379-383:
+ *   mask_ptr[i] = num_objs, extra_assign is a uint8 map); 1: the engine's opt-in deviation
+ *   SEMTSDF_F_ID_SATURATE -- a new id that would be >= 32 is 0 (background), num_objs stops at 32.
  * Returns max_obj_now. */
 int oracle_filter_overlaps(const float* probs, const uint8_t* box, uint8_t* mask, int width, int height,
                            uint32_t n_obs, float eps, int precision, int* num_objs, int32_t* assigned_prev,
-                           float* assigned_prob, double* prob_table) {
+                           float* assigned_prob, double* prob_table, int id_policy) {
     const size_t n = (size_t)width * height;
     int maxv = 0;
     for (size_t i = 0; i < n; ++i)
@@ -422,9 +425,13 @@ int oracle_filter_overlaps(const float* probs, const uint8_t* box, uint8_t* mask
             mask[i] = (uint8_t)rev[m];
         } else if (m > 0) {
             if (extra[m] < 0) {
-                extra[m] = no;
-                mask[i] = (uint8_t)no;
-                ++no;
+                if (id_policy == 1 && no >= OMAX) {
+                    extra[m] = 0;  /* saturated: background */
+                } else {
+                    extra[m] = (uint8_t)no;
+                    ++no;
+                }
+                mask[i] = (uint8_t)extra[m];
             } else {
                 mask[i] = (uint8_t)extra[m];
             }

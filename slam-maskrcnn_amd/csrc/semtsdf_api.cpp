@@ -96,6 +96,7 @@ struct semtsdf_vol {
         hipEvent_t prep_done = nullptr;  // the set's prepass finished (prep_stream)
         hipEvent_t set_free = nullptr;   // the integrate reading the set finished (recorded once async is in use)
         bool free_recorded = false;
+        hipStream_t reader = nullptr;    // stream of the last integrate that read the set
     } fs[2];
     int next_set = 0;
     hipStream_t prep_stream = nullptr;   // created on the first asynchronous integrate
@@ -145,6 +146,7 @@ struct semtsdf_vol {
     unsigned* tile_perm_d = nullptr;
     int tile_cap = 0, tile_n = 0;
     bool tables_clean = false;     // tables_d holds the cleared state (left by k_assoc_decide)
+    unsigned long long votes_dropped_seen = 0;  // counters[2] at the last check_bad_label
     // instrumentation
     int instr = 0;
     std::vector<EventPair> ev_integrate, ev_assoc, ev_render, ev_prep;
@@ -220,6 +222,11 @@ int check_params(const semtsdf_params* p) {
     if (p->width <= 0 || p->height <= 0 || p->width > 65535 || p->height > 65535 || (int64_t)p->width * p->height > (1 << 28))
         return fail(SEMTSDF_ERR_INVALID, "bad frame size %dx%d", p->width, p->height);
     if (!(p->depth_scale > 0.0f)) return fail(SEMTSDF_ERR_INVALID, "depth_scale must be > 0");
+    // the association's log terms log(max(p / n, prior)) (tsdf.cu:318,329) stay finite and <= 0 for
+    // p <= n, and its f32 rule is evaluated (certificate or exact sums) for a prior
+    // in this range; the reference's value is 0.05 (configuration.h:8)
+    if (!(p->prior_mrcnn_err_rate >= 0x1p-10f && p->prior_mrcnn_err_rate < 1.0f))
+        return fail(SEMTSDF_ERR_INVALID, "prior_mrcnn_err_rate=%g outside [2^-10, 1)", (double)p->prior_mrcnn_err_rate);
     if ((p->flags & SEMTSDF_F_VOTE) && (p->flags & SEMTSDF_F_SEMANTIC))
         return fail(SEMTSDF_ERR_INVALID, "SEMANTIC and VOTE are exclusive");
     for (int i = 0; i < 3; ++i)
@@ -343,8 +350,10 @@ int ensure_prep_stream(semtsdf_vol* v) {
 // async: the frame prepass runs on the volume's prep stream, ordered after inputs_ready (when
 // given) and after the integrate that last read its frame set -- not after the earlier work
 // of stream s -- so it may overlap the previous frame's integrate.
-// inputs_on_s: inputs_ready was recorded on s at the start of the caller's frame, after every
-// earlier reader of both frame sets: the prepass needs no frame-set event.
+// inputs_on_s: inputs_ready was recorded on s at the start of the caller's frame.  When s is the
+// handle's own stream and the set's last reader ran on it too, inputs_ready follows that reader
+// and the prepass needs no frame-set event; on any other stream (a caller's, whose lifetime the
+// handle does not control) the set's event is recorded after every integrate and waited for.
 // pre_done: the frame's depth pyramid is already in the next frame set (computed in the fused
 // march's launch, raw labels): only the cull runs, on s.
 int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d, const uint8_t* mask_d,
@@ -414,13 +423,16 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
     if (async)
         if (int rc = ensure_prep_stream(v)) return rc;
     hipStream_t ps = s;
+    const bool own_order = inputs_ready && inputs_on_s && s == v->stream && (!F.reader || F.reader == v->stream);
     if (async) {
         ps = v->prep_stream;
         v->async_used = true;
         if (inputs_ready) HIPC(hipStreamWaitEvent(ps, inputs_ready, 0));
-        if (!(inputs_ready && inputs_on_s)) {
-            if (!F.free_recorded) {  // the set's last reader is unknown (first asynchronous frame): all of s
-                HIPC(hipEventRecord(F.set_free, s));
+        if (!own_order) {
+            if (!F.free_recorded) {
+                // the set's event was skipped after its last integrate (which then ran on the handle's
+                // own stream): everything queued there; or the first asynchronous frame: all of s
+                HIPC(hipEventRecord(F.set_free, F.reader == v->stream ? v->stream : s));
                 F.free_recorded = true;
             }
             HIPC(hipStreamWaitEvent(ps, F.set_free, 0));
@@ -484,7 +496,8 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
         }
     }
     if (ep.a) v->ev_integrate.push_back(ep);
-    if (v->async_used && async && inputs_ready && inputs_on_s) {
+    F.reader = s;
+    if (v->async_used && async && own_order) {
         F.free_recorded = false;  // a later prepass ordered otherwise records its event then
     } else if (v->async_used) {  // a later asynchronous prepass into this set waits for this integrate
         HIPC(hipEventRecord(F.set_free, s));
@@ -583,6 +596,7 @@ DecideArgs decide_args(semtsdf_vol* v, const uint8_t* mask_d, AssocPixels px, bo
     d.px = px;
     d.npx = (int)npx(v);
     d.force_exact = (v->instr & 4) ? 1 : 0;
+    d.id_policy = (v->p.flags & SEMTSDF_F_ID_SATURATE) ? 1 : 0;
     d.certify_only = certify_only ? 1 : 0;
     return d;
 }
@@ -692,6 +706,7 @@ void decision_to_stats(const AssocDecision& d, semtsdf_assoc_stats* st) {
     st->max_obj_now = d.max_obj_now;
     st->num_objs = d.num_objs_after;
     st->exact_rows = d.exact_rows;
+    st->reject_rows = d.reject_rows;
     for (int i = 0; i < kMaxObjects; ++i) {
         st->assigned_prev[i] = d.assigned_prev[i];
         st->assigned_prob[i] = d.assigned_prob[i];
@@ -708,16 +723,18 @@ int validate_mask_host(const semtsdf_vol* v, const uint8_t* mask) {
     return SEMTSDF_OK;
 }
 
+// The integrate counts the histogram votes it drops for ids >= 32 (counters[2], cumulative until
+// a reset): a synchronous frame that added some reports SEMTSDF_ERR_LABEL, after the frame has
+// been applied in full (the handle stays usable).
 int check_bad_label(semtsdf_vol* v, hipStream_t s) {
     unsigned long long c[3];
     HIPC(hipMemcpyAsync(c, v->counters_d, sizeof(c), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
-    if (c[2]) {
-        unsigned long long z = 0;
-        HIPC(hipMemcpyAsync(v->counters_d + 2, &z, sizeof(z), hipMemcpyHostToDevice, s));
-        HIPC(hipStreamSynchronize(s));
-        return fail(SEMTSDF_ERR_LABEL, "a mask label >= %d reached the integrate kernel (histogram update skipped)",
-                    kMaxObjects);
+    if (c[2] != v->votes_dropped_seen) {
+        const unsigned long long d = c[2] - v->votes_dropped_seen;
+        v->votes_dropped_seen = c[2];
+        return fail(SEMTSDF_ERR_LABEL, "%llu histogram votes of ids >= %d dropped (tsdf.cu:61 would write past the "
+                    "voxel's bins; SEMTSDF_F_ID_SATURATE avoids such ids)", d, kMaxObjects);
     }
     return SEMTSDF_OK;
 }
@@ -1004,10 +1021,9 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
         DepthPyramid& pyr = f.pyr;
         pyr.w0 = (p->width + 7) / 8; pyr.h0 = (p->height + 7) / 8;
         pyr.w1 = (p->width + 31) / 32; pyr.h1 = (p->height + 31) / 32;
-        pyr.tw = (p->width + 3) / 4;
-        pyr.zero = (unsigned)pyr.tw * (unsigned)((p->height + 3) / 4) * 16u;
-        // the records of the padding pixels of edge tiles and the zero record stay zero
-        const size_t nrec = (size_t)pyr.zero + 1;
+        pyr.rs = 4u * (unsigned)((p->width + 1 + 3) / 4 * 4);
+        // the zero column u = W and row v = H (and the padding of the last band) stay zero
+        const size_t nrec = (size_t)pyr.rs * (size_t)((p->height + 1 + 3) / 4);
         if ((rc = dev_alloc(v, (void**)&pyr.px, nrec * 8))) return bail(rc);
         if (hipMemset(pyr.px, 0, nrec * 8) != hipSuccess) return bail(fail(SEMTSDF_ERR_HIP, "memset failed"));
         if ((rc = dev_alloc(v, (void**)&pyr.l0, (size_t)pyr.w1 * 4 * pyr.h1 * 4 * sizeof(uint2)))) return bail(rc);
@@ -1062,7 +1078,9 @@ int semtsdf_get_params(const semtsdf_vol* v, semtsdf_params* out) {
 int semtsdf_get_state(const semtsdf_vol* v, semtsdf_state* out) {
     if (!v || !out) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
     int n = 0;
+    unsigned long long dropped = 0;
     HIPC(hipMemcpyAsync(&n, v->num_objs_d, sizeof(int), hipMemcpyDeviceToHost, v->stream));
+    HIPC(hipMemcpyAsync(&dropped, v->counters_d + 2, sizeof(dropped), hipMemcpyDeviceToHost, v->stream));
     HIPC(hipStreamSynchronize(v->stream));
     out->n_obs = v->n_obs;
     out->num_objs = n;
@@ -1071,6 +1089,7 @@ int semtsdf_get_state(const semtsdf_vol* v, semtsdf_state* out) {
     out->local_dim[2] = v->g.lz;
     out->local_voxels = (uint64_t)v->g.dimx * v->g.dimy * v->g.lz;
     out->device_bytes = v->device_bytes;
+    out->label_votes_dropped = dropped;
     return SEMTSDF_OK;
 }
 
@@ -1100,6 +1119,7 @@ int semtsdf_reset(semtsdf_vol* v, void* stream) {
     if (v->b.cls_cnt) HIPC(hipMemsetAsync(v->b.cls_cnt, 0, n * 4, s));
     HIPC(hipMemsetAsync(v->num_objs_d, 0, 16, s));
     HIPC(hipMemsetAsync(v->counters_d, 0, kCounters * sizeof(unsigned long long), s));
+    v->votes_dropped_seen = 0;
     v->n_obs = 0;
     v->wmax_bound = 0;
     v->bmin_stale = true;
@@ -1288,11 +1308,13 @@ int semtsdf_parse_frame(semtsdf_vol* v, const uint16_t* depth, const uint8_t* rg
     v->n_obs++;
     if (sem) HIPC(hipMemcpyAsync(mask_inout, v->mask_d, n, hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
+    int rc_label = SEMTSDF_OK;  // reported after the frame is applied in full (the handle stays usable)
     if (sem && v->n_obs > 1) {
         if (stats) decision_to_stats(*v->decision_h, stats);
         if (v->decision_h->bad_label)
-            return fail(SEMTSDF_ERR_LABEL, "association produced %d objects (> %d)", v->decision_h->num_objs_after,
-                        kMaxObjects);
+            rc_label = fail(SEMTSDF_ERR_LABEL, "association produced %d objects (> %d): ids >= %d have no "
+                            "histogram bin (SEMTSDF_F_ID_SATURATE avoids them)", v->decision_h->num_objs_after,
+                            kMaxObjects, kMaxObjects);
     } else if (stats) {
         memset(stats, 0, sizeof(*stats));
         for (int i = 0; i < kMaxObjects; ++i) stats->assigned_prev[i] = -1;
@@ -1302,7 +1324,10 @@ int semtsdf_parse_frame(semtsdf_vol* v, const uint16_t* depth, const uint8_t* rg
         stats->num_objs = no;
         stats->max_obj_now = no;
     }
-    if (sem) return check_bad_label(v, s);
+    if (sem) {
+        const int rc_votes = check_bad_label(v, s);  // also takes note of this frame's dropped votes
+        return rc_label ? rc_label : rc_votes;
+    }
     return SEMTSDF_OK;
 }
 

@@ -88,20 +88,20 @@ struct VolBufs {
 struct DepthPyramid {
     uint2* px;      // pixel records {bits of depth / depth_scale (IEEE, tsdf.cu:49),
                     //                r | g << 8 | b << 16 | label << 24}: one 8-B gather per voxel,
-                    // in 4 x 4-pixel tiles of one 128-B line each (rec_index): the voxels of a
-                    // unit project onto a compact patch of the image, which then spans few lines;
-                    // record `zero` (after the tiles) is zero: the target of off-image voxels
+                    // in 4 x 4-pixel tiles of one 128-B line each, a tile column-major (rec_index):
+                    // the voxels of a unit project onto a compact patch of the image, which then
+                    // spans few lines.  The record image has one more column (u = W) and row (v = H)
+                    // than the frame, always zero (depth 0): off-image coordinates clamp onto them
     uint2* l0;  // [ceil(H/8)][ceil(W/8)]  {max | (0xFFFF - min nonzero) << 16, 1 if a pixel has depth 0}
     uint2* l1;  // [ceil(H/32)][ceil(W/32)]
     int w0, h0, w1, h1;
-    int tw;         // 4-pixel tiles per image row: ceil(W / 4)
-    unsigned zero;  // index of the zero record: ceil(W / 4) * ceil(H / 4) * 16
+    unsigned rs;    // records per band of 4 rows: 4 * (W + 1 rounded up to a multiple of 4)
 };
 
-// Pixel record of pixel (u, v): 4 x 4 tiles, 16 records (one 128-B line) each, the tile's rows
-// of 4 consecutive records.
+// Record of pixel (u, v), 0 <= u <= W, 0 <= v <= H: bands of 4 rows, in a band the 4 records of
+// a column consecutive, so a 128-B line holds the 4 x 4 pixels u = 4a..4a+3, v = 4b..4b+3.
 __device__ inline unsigned rec_index(const DepthPyramid& p, unsigned u, unsigned v) {
-    return ((__umul24(v >> 2, (unsigned)p.tw) + (u >> 2)) << 4) | ((v & 3u) << 2) | (u & 3u);
+    return __umul24(v >> 2, p.rs) + ((u << 2) | (v & 3u));
 }
 
 struct IntegrateArgs {
@@ -156,7 +156,8 @@ struct AssocTables {
     unsigned int c3[kMaxObjects][kMaxObjects];// pixels with box_n & mask == m
     unsigned int first_px[256];               // first pixel index of each label (UINT_MAX none)
     unsigned int max_label;                   // max(mask)
-    unsigned int pad;
+    unsigned int pos_max;                     // largest positive t1 term (p > n_obs), 2^-28 fixed point,
+                                              // saturating; >= 1 whenever any term was positive (0: none)
 };
 static_assert(sizeof(AssocTables) % 8 == 0, "AssocTables is cleared as 8-B words");
 
@@ -172,6 +173,8 @@ struct AssocDecision {
     unsigned exact_rows;    // bit i: row i decided from its exact f32 pixel-order sums
     unsigned exact_missing; // bit i: row i needed them but no pixel data was given (decided from
                             // the fixed-point sums; the sharded protocol then exchanges pixels)
+    unsigned reject_rows;   // bit i: the certificate shows every candidate of row i at or below
+                            // 3 * prior whatever the f32 rounding (rejected without the exact path)
 };
 
 // Per-pixel association data of the last march (the exact path of the decision): for pixel k
@@ -203,6 +206,8 @@ struct DecideArgs {
     AssocPixels px;         // bits == nullptr: no pixel data (exact_missing)
     int npx;
     int force_exact;        // debug/tests: every present row takes the exact path
+    int id_policy;          // 0: new ids num_objs++ as tsdf.cu:379-383 (ids >= 32 get no histogram bin);
+                            // 1 (SEMTSDF_F_ID_SATURATE): new ids >= 32 become 0 (background)
     int certify_only;       // write the rows needing the exact path to D->exact_missing, decide nothing
     const unsigned* tile_cost;  // tile_n > 0: an extra workgroup orders the fused march's tiles by cost
     unsigned* tile_perm;

@@ -621,10 +621,13 @@ __device__ __forceinline__ void pyramid_tile(const uint16_t* __restrict__ depth,
                 o.z = (c1 >> 16) | ((c2 & 0xFFu) << 16) | (((lab >> 16) & 0xFFu) << 24);
                 o.w = (c2 >> 8) | ((lab >> 24) << 24);
             }
-            // depth[img] / 5000.f (tsdf.cu:49), once per pixel; x0 % 4 == 0: one tile row
-            uint4* dst = reinterpret_cast<uint4*>(p.px + rec_index(p, (unsigned)x0, (unsigned)yy));
-            dst[0] = make_uint4(__float_as_uint((float)d[0] / scale), o.x, __float_as_uint((float)d[1] / scale), o.y);
-            dst[1] = make_uint4(__float_as_uint((float)d[2] / scale), o.z, __float_as_uint((float)d[3] / scale), o.w);
+            // depth[img] / 5000.f (tsdf.cu:49), once per pixel; x0 % 4 == 0: one row of a tile,
+            // records 4 apart (a tile is column-major)
+            uint2* dst = p.px + rec_index(p, (unsigned)x0, (unsigned)yy);
+            dst[0] = make_uint2(__float_as_uint((float)d[0] / scale), o.x);
+            dst[4] = make_uint2(__float_as_uint((float)d[1] / scale), o.y);
+            dst[8] = make_uint2(__float_as_uint((float)d[2] / scale), o.z);
+            dst[12] = make_uint2(__float_as_uint((float)d[3] / scale), o.w);
         } else {
             for (int k = 0; k < 4 && x0 + k < w; ++k) {
                 const size_t px = px0 + k;
@@ -683,7 +686,7 @@ __global__ __launch_bounds__(256) void k_depth_pyramid(const uint16_t* __restric
 
 // Whether the prepass may use its vector path (4-pixel rows aligned).
 int depth_pyramid_vec(const uint16_t* depth, const uint8_t* rgb, const uint8_t* mask, int w, const DepthPyramid& p) {
-    return (w % 4 == 0) && ((uintptr_t)depth % 8 == 0) && ((uintptr_t)p.px % 16 == 0) && (!rgb || (uintptr_t)rgb % 4 == 0) &&
+    return (w % 4 == 0) && ((uintptr_t)depth % 8 == 0) && (!rgb || (uintptr_t)rgb % 4 == 0) &&
            (!mask || (uintptr_t)mask % 4 == 0);
 }
 
@@ -1052,9 +1055,10 @@ constexpr unsigned kFlagMax = 255u;  // s - 1 <= 254 pending increments
 struct Proj {
     float qz[4];
     uint2 rec[4];  // gathered pixel record {metres bits, rgbl}
-    int img[4];    // record index (rec_index); pyr.zero (the zero record) off-image or on an invalid plane
-    int lin[4];    // vote mode: the pixel's row-major index, W*H off-image
+    int img[4];    // record index (rec_index); off-image: a record of the zero column / row
+    int lin[4];    // vote mode: the pixel's row-major index, W*H off-image or on an invalid plane
     unsigned sflag;  // steady flag of the lane's sdf line (below)
+    unsigned vmask;  // bit k: plane l0 + k is a voxel of the volume (others are never touched)
 };
 
 struct Cls {
@@ -1115,7 +1119,8 @@ __device__ __forceinline__ void stage_project(const IntegrateArgs& a, const Unit
                                                         (unsigned)lane_y(lane) * 4u) >> 5]
                                  : 0u;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) P.rec[k] = make_uint2(up.ok ? 1u : 0u, 0u);  // "depth != 0" of a real unit
+        for (int k = 0; k < 4; ++k) P.rec[k] = make_uint2(1u, 0u);  // "depth != 0"
+        P.vmask = up.ok ? 0xFu : 0u;  // every voxel of a real unit
         return;
     }
     const int npx = a.width * a.height;
@@ -1132,21 +1137,37 @@ __device__ __forceinline__ void stage_project(const IntegrateArgs& a, const Unit
     // (sx, sy) pairs in packed f32 (v_pk_fma / v_pk_mul / v_pk_add: each lane of a packed op is
     // the scalar IEEE operation, so the values are those of the scalar contract)
     const f32x2 bsxy = {bsx, bsy}, Mxy = {a.M[2], a.M[5]};
-    const float fl0 = (float)l0;  // (float)(l0 + k) == fl0 + k: integers far below 2^24
-    // sharded: the chunk block of l0 once per lane (local_to_global_z without a division per
-    // voxel; l0 + k lies in that block or the next)
+    // (float)(l0 + k) == fl0 + k (integers far below 2^24): one add per plane; the empty asm
+    // keeps the compiler from turning it back into an integer add and a conversion
+    float fl0 = (float)l0;
+    asm volatile("" : "+v"(fl0));
+    // the lane's valid planes (bit k: plane l0 + k exists in this shard's storage and, sharded,
+    // in the volume): voxels outside it project like the others but are never touched
+    // (stage_classify masks them), so the projection carries no per-voxel validity selects
+    unsigned vmask;
     int cblk = 0, w0 = 0;
     const int per = g.chunk + g.halo;
-    if (SHARD) {
+    if (SHARD) {  // the chunk block of l0 once per lane; l0 + k lies in that block or the next
         cblk = l0 / per;
         w0 = l0 - cblk * per;
+        vmask = 0u;
+    } else {
+        vmask = row_ok ? (0xFu >> (4 - min(g.lz - l0, 4))) : 0u;
     }
-    unsigned slow = 0;
+    // floor(sx/sz), floor(sy/sz) through the reciprocal: |qu - RN(sx/sz)| <= 2^-22 |qu|, so for
+    // |qu| < B (host: B = 2^ceil(log2(max(W, H) + 2))) a fraction farther than B 2^-21 from 0
+    // and 1, i.e. |fract - 1/2| < ftol, floors like the IEEE quotient; |qu| >= B is off-image
+    // either way.  Per voxel the NaN-propagating maximum (v_maximum) of |fract - 1/2| of both
+    // coordinates: a near-integer, a huge quotient (fract 0) or NaN/Inf (fract NaN) takes the
+    // exact IEEE division below (per voxel: a wave runs the division of plane k only when one of
+    // its lanes needs it).
+    float mk[4];
+    unsigned uu[4], vv[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        int gz = l0 + k;
-        bool zok = row_ok & (l0 + k < g.lz);
+        float pzk;
         if (SHARD) {
+            int gz;
             if (per >= 4) {  // 4 consecutive planes span at most two blocks
                 const bool nxt = w0 + k >= per;
                 const int cb = cblk + (nxt ? 1 : 0);
@@ -1154,45 +1175,51 @@ __device__ __forceinline__ void stage_project(const IntegrateArgs& a, const Unit
             } else {
                 gz = local_to_global_z(g, l0 + k);
             }
-            zok = zok & (gz < g.dimz);
+            vmask |= ((row_ok & (l0 + k < g.lz) & (gz < g.dimz)) ? 1u : 0u) << k;
+            pzk = (float)gz;
+        } else {
+            pzk = fl0 + (float)k;
         }
-        const float pz = fmaf(SHARD ? (float)gz : fl0 + (float)k, g.voxel[2], g.start[2]);
+        const float pz = fmaf(pzk, g.voxel[2], g.start[2]);
         const f32x2 sxy = __builtin_elementwise_fma(Mxy, (f32x2){pz, pz}, bsxy);
         const float sz = fmaf(a.M[8], pz, bsz);
         P.qz[k] = PIN ? sz : fmaf(a.E[10], pz, bqz);
-        // floor(sx/sz), floor(sy/sz) through the reciprocal: |qu - RN(sx/sz)| <= 2^-22 |qu|,
-        // so for |qu| < B (host: B = 2^ceil(log2(max(W, H) + 2))) a fraction farther than
-        // B 2^-21 from 0 and 1 floors like the IEEE quotient; |qu| >= B is off-image either
-        // way; NaN/Inf and near-integers fail the window and are redone exactly below.
         const float r = __builtin_amdgcn_rcpf(sz);
         const f32x2 q = sxy * r;
         const f32x2 e = (f32x2){__builtin_amdgcn_fractf(q.x), __builtin_amdgcn_fractf(q.y)} - 0.5f;
-        const bool fast = (fabsf(e.x) < a.ftol) & (fabsf(e.y) < a.ftol);
-        const int iu = cvt_flr(q.x), iv = cvt_flr(q.y);  // the window holds only |q| < 2^23
-        slow |= ((zok & !fast) ? 1u : 0u) << k;
-        const bool in = zok & fast & ((unsigned)iu < (unsigned)a.width) & ((unsigned)iv < (unsigned)a.height);
-        P.img[k] = in ? (int)rec_index(a.pyr, (unsigned)iu, (unsigned)iv) : (int)a.pyr.zero;
-        if (LIN) P.lin[k] = in ? (int)__umul24((unsigned)iv, (unsigned)a.width) + iu : npx;
+        mk[k] = __builtin_elementwise_maximum(fabsf(e.x), fabsf(e.y));
+        // off-image pixels (either side) clamp onto the record image's zero column u = W / zero
+        // row v = H (unsigned min: negative coordinates are huge)
+        uu[k] = min((unsigned)cvt_flr(q.x), (unsigned)a.width);
+        vv[k] = min((unsigned)cvt_flr(q.y), (unsigned)a.height);
     }
-    if (slow) {  // rare: exact IEEE quotients (the screen position is recomputed)
+    const float worst = __builtin_elementwise_maximum(__builtin_elementwise_maximum(mk[0], mk[1]),
+                                                      __builtin_elementwise_maximum(mk[2], mk[3]));
+    if (!(worst < a.ftol)) {  // rare: exact IEEE quotients (the screen position is recomputed)
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            if (!(slow & (1u << k))) continue;
+            if (mk[k] < a.ftol) continue;
             const int gz = SHARD ? local_to_global_z(g, l0 + k) : l0 + k;
             const float pz = fmaf((float)gz, g.voxel[2], g.start[2]);
             const float sx = fmaf(a.M[2], pz, bsx), sy = fmaf(a.M[5], pz, bsy), sz = fmaf(a.M[8], pz, bsz);
-            const int ix = f2i_rd(sx / sz), iy = f2i_rd(sy / sz);
-            const bool in = ix >= 0 && ix < a.width && iy >= 0 && iy < a.height;
-            P.img[k] = in ? (int)rec_index(a.pyr, (unsigned)ix, (unsigned)iy) : (int)a.pyr.zero;
-            if (LIN) P.lin[k] = in ? iy * a.width + ix : npx;
+            uu[k] = min((unsigned)f2i_rd(sx / sz), (unsigned)a.width);
+            vv[k] = min((unsigned)f2i_rd(sy / sz), (unsigned)a.height);
         }
+    }
+    P.vmask = vmask;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        P.img[k] = (int)rec_index(a.pyr, uu[k], vv[k]);
+        if (LIN) P.lin[k] = (uu[k] < (unsigned)a.width && vv[k] < (unsigned)a.height && ((vmask >> k) & 1u))
+                                ? (int)__umul24(vv[k], (unsigned)a.width) + (int)uu[k]
+                                : npx;
     }
     // steady flag of the lane's sdf line (one byte per 128-B line, unconditional)
     P.sflag = SEMTSDF_STEADY ? (unsigned)a.b.sflag[(unit_tile(g, up) + (unsigned)lane_zq(lane) * 32u +
                                                     (unsigned)lane_y(lane) * 4u) >> 5]
                              : 0u;
-    // unconditional gathers; an off-image voxel reads the zero record past the image (depth 0);
-    // a free unit needs only the depth word (touched <=> depth != 0, f == 1)
+    // unconditional gathers (an off-image voxel reads a zero record: depth 0); a free unit needs
+    // only the depth word (touched <=> depth != 0, f == 1)
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         if (FREE)
@@ -1234,7 +1261,8 @@ __device__ __forceinline__ unsigned count_lines(unsigned tmask) {
 
 template <bool SEM, bool GATE, bool VOTE, bool COUNT, bool FREE>
 __device__ __forceinline__ void stage_classify(const IntegrateArgs& a, const Proj& P, Cls& C, bool count,
-                                               unsigned& n_touch, unsigned& n_gate, unsigned lutv) {
+                                               unsigned& n_touch, unsigned& n_gate, unsigned& n_lines,
+                                               unsigned lutv) {
     const VolGeom& g = a.g;
     if (FREE) {  // free unit (unit_cull == 2): a voxel with depth is touched with f == 1, never gated
         unsigned tm = 0;
@@ -1244,6 +1272,7 @@ __device__ __forceinline__ void stage_classify(const IntegrateArgs& a, const Pro
             C.fv[k] = 1.0f;
             C.pix[k] = 0u;
         }
+        tm &= P.vmask;
         C.sflag = P.sflag;
         if (kProbes && (a.debug == 3 || a.debug == 21)) tm = 0u;  // probe: no state traffic
         C.tmask = tm;
@@ -1252,12 +1281,13 @@ __device__ __forceinline__ void stage_classify(const IntegrateArgs& a, const Pro
         C.hmode = 0u;
         if (COUNT && count) {
             n_touch += __popc(tm);
-            n_gate += count_lines(tm) << 16;  // high half: touched lines (lane 0)
+            n_lines += count_lines(tm);  // touched lines (lane 0)
         }
         return;
     }
-    unsigned tmask = 0, dslow = 0;
+    unsigned tmask = 0;
     float dm[4];
+    float dmin = 1.0f;  // min |dc| of the lane (NaN-propagating): tiny differences take the IEEE division
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const float d = __uint_as_float(P.rec[k].x);
@@ -1266,21 +1296,22 @@ __device__ __forceinline__ void stage_classify(const IntegrateArgs& a, const Pro
         const bool t = (d != 0.0f) & (diff > -g.mu);
         const float dc = fminf(diff, g.mu);
         C.fv[k] = div_by_rcp(dc, g.mu, a.rmu);
-        dslow |= ((t & !(fabsf(dc) >= 0x1p-60f)) ? 1u : 0u) << k;
+        dmin = __builtin_elementwise_minimum(dmin, fabsf(dc));
         tmask |= (t ? 1u : 0u) << k;
         C.pix[k] = P.rec[k].y;
         if (VOTE) C.img[k] = P.lin[k];
     }
+    tmask &= P.vmask;
     if (SEM && a.lut) {  // uniform: records of a deferred relabel carry raw labels
 #pragma unroll
         for (int k = 0; k < 4; ++k) C.pix[k] = relabel_rec(C.pix[k], lutv);
     }
     C.sflag = P.sflag;
-    if (dslow || !a.fastdiv) {  // rare: tiny differences, or mu outside the reciprocal range
+    if (!(dmin >= 0x1p-60f) || !a.fastdiv) {  // rare: tiny differences, or mu outside the reciprocal range
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const float dc = fminf(dm[k] - P.qz[k], g.mu);
-            if (!a.fastdiv || (dslow & (1u << k))) C.fv[k] = dc == 0.0f ? dc : dc / g.mu;
+            if (!a.fastdiv || !(fabsf(dc) >= 0x1p-60f)) C.fv[k] = dc == 0.0f ? dc : dc / g.mu;
         }
     }
     unsigned gmask = 0;
@@ -1289,7 +1320,8 @@ __device__ __forceinline__ void stage_classify(const IntegrateArgs& a, const Pro
         gmask |= (((((tmask >> k) & 1u) != 0u) & (!GATE || C.fv[k] < a.gate)) ? 1u : 0u) << k;
     if (COUNT && count) {
         n_touch += __popc(tmask);
-        n_gate += __popc(gmask) + (count_lines(tmask) << 16);  // high half: touched lines (lane 0)
+        n_gate += __popc(gmask);
+        n_lines += count_lines(tmask);  // touched lines (lane 0)
     }
     if (kProbes && (a.debug == 3 || a.debug == 21)) tmask = gmask = 0;  // probe: classification only, no state traffic
     if (kProbes && a.debug == 4) gmask = 0;          // timing probe: no colour/histogram traffic
@@ -1439,22 +1471,30 @@ __device__ __forceinline__ void stage_compute(const IntegrateArgs& a, const floa
     const int wo[4] = {L.w4.x + pend, L.w4.y + pend, L.w4.z + pend, L.w4.w + pend};
     float sn[4];
     int wn[4];
-    unsigned uslow = 0;
+    // the reciprocal path's range over the lane's 4 voxels (touched or not: a running maximum of the
+    // weights, a NaN-propagating minimum of |num|) instead of a per-voxel condition; the rare
+    // exact path below decides per voxel
+    unsigned wmax = 0u;
+    float nmin = 1.0f;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const bool t = (tmask >> k) & 1u;
+        const int tk = (int)(tmask << (31 - k)) >> 31;  // touched: all ones (v_bfe_i32), else 0
         const float num = fmaf(so[k], (float)wo[k], C.fv[k]);
         const float rw = s_rcp[min((unsigned)wo[k], (unsigned)kRcpTable - 1u)];
         const float upd = div_by_rcp(num, (float)wo[k] + 1.0f, rw);
-        uslow |= ((t & !(((unsigned)wo[k] < (unsigned)kRcpTable) & (fabsf(num) >= 0x1p-60f))) ? 1u : 0u) << k;
-        sn[k] = t ? upd : so[k];
-        wn[k] = wo[k] + (t ? 1 : 0);
+        wmax = max(wmax, (unsigned)wo[k]);
+        nmin = __builtin_elementwise_minimum(nmin, fabsf(num));
+        // select by the touched mask as bits (v_bfi_b32): no per-voxel lane-mask compare
+        sn[k] = __uint_as_float((__float_as_uint(upd) & (unsigned)tk) | (__float_as_uint(so[k]) & ~(unsigned)tk));
+        wn[k] = wo[k] - tk;
     }
-    if (uslow || !a.fastdiv) {  // rare: weights past the table, tiny numerators
+    if (!((wmax < (unsigned)kRcpTable) & (nmin >= 0x1p-60f)) || !a.fastdiv) {  // rare: weights past the table, tiny numerators
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            if (!((tmask >> k) & 1u) || (a.fastdiv && !(uslow & (1u << k)))) continue;
-            sn[k] = fmaf(so[k], (float)wo[k], C.fv[k]) / (float)(wo[k] + 1);
+            const float num = fmaf(so[k], (float)wo[k], C.fv[k]);
+            const bool slow = !(((unsigned)wo[k] < (unsigned)kRcpTable) & (fabsf(num) >= 0x1p-60f)) || !a.fastdiv;
+            if (!((tmask >> k) & 1u) || !slow) continue;
+            sn[k] = num / (float)(wo[k] + 1);
         }
     }
     O.s4 = make_float4(sn[0], sn[1], sn[2], sn[3]);
@@ -1617,9 +1657,11 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
                         atomicAdd(a.b.hist + (uint64_t)lab * g.nvox + v + k, 1u);
                         atomicOr(a.b.hmask + v + k, 1u << lab);
                     }
-                    bad |= (gk && lab >= (unsigned)kMaxObjects) ? 1u : 0u;
+                    bad += (gk && lab >= (unsigned)kMaxObjects) ? 1u : 0u;
                 }
-                if (bad) atomicOr(reinterpret_cast<unsigned*>(a.counters + 2), 1u);
+                // an id without a histogram bin (tsdf.cu:61 writes past the voxel's 32 bins): the
+                // vote is dropped and counted
+                if (bad) atomicAdd(a.counters + 2, (unsigned long long)bad);
             }
         }
     }
@@ -1662,7 +1704,10 @@ __device__ __forceinline__ ListView list_view(const unsigned* list, const unsign
 // Entry idx < total: its segment is the number of segments ending at or before idx.
 __device__ __forceinline__ unsigned list_entry(const ListView& v, unsigned idx, unsigned seg_cap) {
     const unsigned seg = (unsigned)__popcll(__ballot(v.incl <= idx));
-    const unsigned before = seg ? __builtin_amdgcn_readfirstlane((unsigned)__shfl((int)v.incl, (int)seg - 1, 64)) : 0u;
+    // the entries before the segment: lane seg - 1's prefix, read with v_readlane (a wave-uniform
+    // lane index) -- a __shfl is a ds_bpermute whose lgkmcnt wait would also wait for the
+    // scalar list loads in flight
+    const unsigned before = seg ? (unsigned)__builtin_amdgcn_readlane((int)v.incl, (int)seg - 1) : 0u;
     // constant address space: the list is read-only here, so this is a scalar load (s_load,
     // lgkmcnt) and never waits behind the wave's vector memory operations
     const __attribute__((address_space(4))) unsigned* l4 = (const __attribute__((address_space(4))) unsigned*)v.list;
@@ -1693,6 +1738,11 @@ __device__ __forceinline__ UnitPos lane_pos(const UnitGrid& ug, const unsigned* 
     return p;
 }
 
+// Per-lane counts of the count mode (touched and gated voxels, touched lines on lane 0, lazy voxels).
+struct Counts {
+    unsigned touch, gate, lines, lazy;
+};
+
 // Pipeline state carried from one list into the next: the unit whose project, classify and
 // load stages were issued (primed) but not yet computed and stored.
 struct Pipe {
@@ -1703,6 +1753,7 @@ struct Pipe {
     Out O;
     bool primed = false;
     unsigned lutv = 0;  // deferred relabel table, one dword per lane (IntegrateArgs::lut)
+    unsigned groups = 0;  // priority rotation: SEMTSDF_PRIO_EVERY x the workgroup's dispatch round + groups done
 };
 
 // Unit-kind of a list: 0 general, 1 free (projected), 2 full free (no projection).
@@ -1714,7 +1765,7 @@ struct KindOf {
 // The project / classify / load stages of the wave's first group of list v (v.i < v.ngroups).
 template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT, bool SHARD, bool PIN, int KIND>
 __device__ __forceinline__ void list_prime(const IntegrateArgs& a, const UnitGrid& ug, unsigned seg_cap,
-                                           const ListView& v, Pipe& S, unsigned& n_touch, unsigned& n_gate) {
+                                           const ListView& v, Pipe& S, Counts& n) {
     constexpr bool FREE = KindOf<KIND>::FREE, FULL = KindOf<KIND>::FULL;
     const int lane = threadIdx.x & 63;
     const unsigned coff = (unsigned)lane_zq(lane) * 32u + (unsigned)lane_y(lane) * 4u;
@@ -1722,7 +1773,7 @@ __device__ __forceinline__ void list_prime(const IntegrateArgs& a, const UnitGri
     group_entries(v, v.i, seg_cap, e);
     S.cur = lane_pos(ug, e);
     stage_project<SHARD, PIN, FREE, FULL, VOTE>(a, S.cur, lane, S.P);
-    stage_classify<SEM, GATE, VOTE, COUNT, FREE>(a, S.P, S.C, true, n_touch, n_gate, S.lutv);
+    stage_classify<SEM, GATE, VOTE, COUNT, FREE>(a, S.P, S.C, true, n.touch, n.gate, n.lines, S.lutv);
     stage_load<SEM, CI32, VOTE, FREE>(a, S.cur, coff, S.C, S.L);
     S.primed = true;
 }
@@ -1737,6 +1788,16 @@ __device__ __forceinline__ void list_prime(const IntegrateArgs& a, const UnitGri
 // quarter of the time.
 #ifndef SEMTSDF_PRIO_ROTATE
 #define SEMTSDF_PRIO_ROTATE 1
+#endif
+#ifndef SEMTSDF_PRIO_EVERY
+#define SEMTSDF_PRIO_EVERY 4  // groups per priority step (a power of two); 1 rotated every group (r04)
+#endif
+static_assert((SEMTSDF_PRIO_EVERY & (SEMTSDF_PRIO_EVERY - 1)) == 0, "a power of two");
+#ifndef SEMTSDF_PROBE_SALU
+#define SEMTSDF_PROBE_SALU 0  // instrumentation builds: extra scalar ALU ops per group (issue probe)
+#endif
+#ifndef SEMTSDF_PROBE_VALU
+#define SEMTSDF_PROBE_VALU 0  // instrumentation builds: extra vector ALU ops per group (issue probe)
 #endif
 __device__ __forceinline__ void rotate_prio(unsigned p) {
     if (!SEMTSDF_PRIO_ROTATE) return;
@@ -1758,8 +1819,7 @@ __device__ __forceinline__ unsigned dispatch_round() {
 template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT, bool SHARD, bool PIN, int KIND, int NKIND>
 __device__ __forceinline__ void integrate_list(const IntegrateArgs& a, const UnitGrid& ug, unsigned seg_cap,
                                                const float* __restrict__ s_rcp, ListView& v, const ListView* nx,
-                                               unsigned nwaves, Pipe& S, unsigned& n_touch, unsigned& n_gate,
-                                               unsigned& n_lazy) {
+                                               unsigned nwaves, Pipe& S, Counts& n) {
     constexpr bool FREE = KindOf<KIND>::FREE, FULL = KindOf<KIND>::FULL;
     constexpr bool NFREE = KindOf<(NKIND < 0 ? 0 : NKIND)>::FREE, NFULL = KindOf<(NKIND < 0 ? 0 : NKIND)>::FULL;
     const int lane = threadIdx.x & 63;
@@ -1768,7 +1828,7 @@ __device__ __forceinline__ void integrate_list(const IntegrateArgs& a, const Uni
     // no group of this list for the wave: the next list primes itself (a primed pipeline
     // always holds a unit of the first list, in order, that has a group for the wave)
     if (v.i >= v.ngroups) return;
-    if (!S.primed) list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, KIND>(a, ug, seg_cap, v, S, n_touch, n_gate);
+    if (!S.primed) list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, KIND>(a, ug, seg_cap, v, S, n);
     unsigned en[kSlots];
     if (v.i + nwaves < v.ngroups) group_entries(v, v.i + nwaves, seg_cap, en);
     const bool chain = NKIND >= 0 && SEMTSDF_CHAIN && nx->i < nx->ngroups;
@@ -1780,12 +1840,26 @@ __device__ __forceinline__ void integrate_list(const IntegrateArgs& a, const Uni
         stage_project<SHARD, PIN, FREE, FULL, VOTE>(a, nxt, lane, S.P);
         stage_compute<SEM, GATE, CI32, VOTE, FREE>(a, s_rcp, S.C, S.L, S.O);
         const StoreMeta Mc = store_meta(S.C);
-        stage_classify<SEM, GATE, VOTE, COUNT, FREE>(a, S.P, S.C, true, n_touch, n_gate, S.lutv);
-        stage_store<SEM, CI32, VOTE, FREE, COUNT>(a, S.cur, coff, Mc, S.O, n_lazy);
+        stage_classify<SEM, GATE, VOTE, COUNT, FREE>(a, S.P, S.C, true, n.touch, n.gate, n.lines, S.lutv);
+        stage_store<SEM, CI32, VOTE, FREE, COUNT>(a, S.cur, coff, Mc, S.O, n.lazy);
         stage_load<SEM, CI32, VOTE, FREE>(a, nxt, coff, S.C, S.L);
         S.cur = nxt;
         v.i += nwaves;
-        rotate_prio(dispatch_round() + v.i / nwaves);
+        // the wave's group counter (no division by nwaves in the loop): a priority step every
+        // SEMTSDF_PRIO_EVERY groups
+        ++S.groups;
+        if (SEMTSDF_PRIO_EVERY == 1 || (S.groups & (SEMTSDF_PRIO_EVERY - 1u)) == 0u)
+            rotate_prio(S.groups / SEMTSDF_PRIO_EVERY);
+#if SEMTSDF_PROBE_SALU || SEMTSDF_PROBE_VALU
+        {  // issue probes (instrumentation builds only): N extra scalar / vector ALU ops per group
+            unsigned su = S.groups, vu = threadIdx.x;
+#pragma unroll
+            for (int q = 0; q < SEMTSDF_PROBE_SALU; ++q) asm volatile("s_mov_b32 %0, %0" : "+s"(su));
+#pragma unroll
+            for (int q = 0; q < SEMTSDF_PROBE_VALU; ++q) asm volatile("v_add_u32 %0, %0, 1" : "+v"(vu));
+            if (su == 0xFFFFFFFFu && vu == 0xFFFFFFFFu) S.lutv ^= 1u;  // keeps the probes live
+        }
+#endif
     }
     // the wave's last unit of this list
     if (NKIND >= 0 && SEMTSDF_CHAIN && chain) {
@@ -1793,14 +1867,14 @@ __device__ __forceinline__ void integrate_list(const IntegrateArgs& a, const Uni
         stage_project<SHARD, PIN, NFREE, NFULL, VOTE>(a, nxt, lane, S.P);
         stage_compute<SEM, GATE, CI32, VOTE, FREE>(a, s_rcp, S.C, S.L, S.O);
         const StoreMeta Mc = store_meta(S.C);
-        stage_classify<SEM, GATE, VOTE, COUNT, NFREE>(a, S.P, S.C, true, n_touch, n_gate, S.lutv);
-        stage_store<SEM, CI32, VOTE, FREE, COUNT>(a, S.cur, coff, Mc, S.O, n_lazy);
+        stage_classify<SEM, GATE, VOTE, COUNT, NFREE>(a, S.P, S.C, true, n.touch, n.gate, n.lines, S.lutv);
+        stage_store<SEM, CI32, VOTE, FREE, COUNT>(a, S.cur, coff, Mc, S.O, n.lazy);
         stage_load<SEM, CI32, VOTE, NFREE>(a, nxt, coff, S.C, S.L);
         S.cur = nxt;
         S.primed = true;
     } else {
         stage_compute<SEM, GATE, CI32, VOTE, FREE>(a, s_rcp, S.C, S.L, S.O);
-        stage_store<SEM, CI32, VOTE, FREE, COUNT>(a, S.cur, coff, store_meta(S.C), S.O, n_lazy);
+        stage_store<SEM, CI32, VOTE, FREE, COUNT>(a, S.cur, coff, store_meta(S.C), S.O, n.lazy);
         S.primed = false;
     }
     v.i += nwaves;
@@ -1833,9 +1907,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
     // (gathers and state loads in flight) before the workgroup's barrier
     for (int i = (int)threadIdx.x; i < kRcpTable; i += (int)blockDim.x) s_rcp[i] = a.rcp_table[i];
     const int lane = threadIdx.x & 63;
-    unsigned n_touch = 0, n_gate = 0, n_lazy = 0;
+    Counts n{};
     unsigned nlive = 0;
     Pipe S;
+    S.groups = dispatch_round() * SEMTSDF_PRIO_EVERY;
     if (SEM && a.lut) S.lutv = reinterpret_cast<const uint32_t*>(a.lut)[lane];
     const unsigned* cnt = a.list_count;
     const unsigned* lst = a.unit_list;
@@ -1849,24 +1924,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
         rot0 = (vf.ngroups + v1.ngroups) % nwaves;
         ListView v0 = list_view(lst, cnt, wave, nwaves, rot0);
         if (vf.i < vf.ngroups)
-            list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 2>(a, ug, seg_cap, vf, S, n_touch, n_gate);
+            list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 2>(a, ug, seg_cap, vf, S, n);
         else if (v1.i < v1.ngroups)
-            list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 1>(a, ug, seg_cap, v1, S, n_touch, n_gate);
+            list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 1>(a, ug, seg_cap, v1, S, n);
         else if (v0.i < v0.ngroups)
-            list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0>(a, ug, seg_cap, v0, S, n_touch, n_gate);
+            list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0>(a, ug, seg_cap, v0, S, n);
         __syncthreads();
         if (SEMTSDF_WAVE_TRACE) tr[1] = tr[2] = tr[3] = wall_clock64();
-        integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 2, 1>(a, ug, seg_cap, s_rcp, vf, &v1, nwaves, S,
-                                                                       n_touch, n_gate, n_lazy);
+        integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 2, 1>(a, ug, seg_cap, s_rcp, vf, &v1, nwaves, S, n);
         if (SEMTSDF_WAVE_TRACE) tr[2] = wall_clock64();
-        integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 1, 0>(a, ug, seg_cap, s_rcp, v1, &v0, nwaves, S,
-                                                                       n_touch, n_gate, n_lazy);
+        integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 1, 0>(a, ug, seg_cap, s_rcp, v1, &v0, nwaves, S, n);
         if (SEMTSDF_WAVE_TRACE) {
             tr[3] = wall_clock64();
             trn = groups_of(vf.total, 0u) | (groups_of(v1.total, vf.ngroups % nwaves) << 20);
         }
-        integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0, -1>(a, ug, seg_cap, s_rcp, v0, nullptr, nwaves, S,
-                                                                        n_touch, n_gate, n_lazy);
+        integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0, -1>(a, ug, seg_cap, s_rcp, v0, nullptr, nwaves, S, n);
         n0 = v0.total;
         if (COUNT && blockIdx.x == 0 && threadIdx.x == 0) {
             atomicAdd(a.counters + 4, (unsigned long long)(v1.total + vf.total));
@@ -1876,11 +1948,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
     } else {
         ListView v0 = list_view(lst, cnt, wave, nwaves, 0u);
         if (v0.i < v0.ngroups)
-            list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0>(a, ug, seg_cap, v0, S, n_touch, n_gate);
+            list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0>(a, ug, seg_cap, v0, S, n);
         __syncthreads();
         if (SEMTSDF_WAVE_TRACE) tr[1] = tr[2] = tr[3] = wall_clock64();
-        integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0, -1>(a, ug, seg_cap, s_rcp, v0, nullptr, nwaves, S,
-                                                                        n_touch, n_gate, n_lazy);
+        integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0, -1>(a, ug, seg_cap, s_rcp, v0, nullptr, nwaves, S, n);
         n0 = v0.total;
     }
     if (SEM && a.lut && a.relabel_mask) {  // the frame's mask through the same table, in place
@@ -1917,8 +1988,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
     }
     if (COUNT) {
         nlive += n0;
-        // n_gate: gated voxels in the low half, touched lines (lane 0 only) in the high half
-        unsigned long long t = n_touch, gg = n_gate & 0xFFFFu, lz = n_lazy, tl = n_gate >> 16;
+        unsigned long long t = n.touch, gg = n.gate, lz = n.lazy, tl = n.lines;
         for (int off = 32; off > 0; off >>= 1) {
             t += __shfl_xor(t, off, 64);
             gg += __shfl_xor(gg, off, 64);
@@ -2552,6 +2622,14 @@ __device__ __forceinline__ long long to_fix(float L) {
     return (long long)rint((double)L * kFixScale);
 }
 
+// A positive t1 term (p / n_obs > 1: a trilinear count rounded above n_obs, or uploaded / given
+// probabilities above it) as AssocTables::pos_max records it: its fixed-point value, at least 1,
+// saturating at 2^32 - 1.  The decision's certificate widens its bounds by the positive terms
+// (prob_interval) and sends every row to the exact path when they leave the validated range.
+__device__ __forceinline__ unsigned pos_fix(float L) {
+    return (unsigned)min(max(to_fix(L), 1ll), 0xFFFFFFFFll);
+}
+
 // Workgroup-local (LDS) copy of the accumulated sums of AssocTables.
 struct AssocLds {
     long long t1[kMaxObjects][kMaxObjects];
@@ -2560,9 +2638,11 @@ struct AssocLds {
     unsigned c1[kMaxObjects];
     unsigned c2[kMaxObjects];
     unsigned c3[kMaxObjects][kMaxObjects];
+    unsigned pos;  // max positive t1 term of the workgroup (pos_fix), 0: none
 };
 
 __device__ __forceinline__ void assoc_lds_clear(AssocLds& s) {
+    if (threadIdx.x == 0) s.pos = 0u;
     for (int k = threadIdx.x; k < kMaxObjects * kMaxObjects; k += blockDim.x) {
         (&s.t1[0][0])[k] = 0;
         (&s.t3[0][0])[k] = 0;
@@ -2581,6 +2661,7 @@ __device__ __forceinline__ void assoc_accumulate(AssocLds& s, const float* p, un
         for (int j = 1; j < kMaxObjects; ++j) {
             const float L = logf(fmaxf(p[j] / n_obs, eps));
             atomicAdd(reinterpret_cast<unsigned long long*>(&s.t1[m][j]), (unsigned long long)to_fix(L));
+            if (L > 0.0f) atomicMax(&s.pos, pos_fix(L));  // rare: p > n_obs
         }
     }
 #pragma unroll
@@ -2621,8 +2702,10 @@ __device__ __forceinline__ void assoc_accumulate_sparse(AssocLds& s, const float
         }
         if (px.bits) px.p[(size_t)j * npx + k] = p[j];
         if (lab) {
-            const long long d = to_fix(logf(fmaxf(p[j] / n_obs, eps))) - F0;
+            const float L1 = logf(fmaxf(p[j] / n_obs, eps));
+            const long long d = to_fix(L1) - F0;
             if (d) atomicAdd(reinterpret_cast<unsigned long long*>(&s.t1[m][j]), (unsigned long long)d);
+            if (L1 > 0.0f) atomicMax(&s.pos, pos_fix(L1));  // rare: p > n_obs
         }
         if (p[j] > box_thresh) {
             const float L = logf(fmaxf(1.0f - p[j] / n_obs, eps));
@@ -2719,6 +2802,7 @@ __device__ __forceinline__ void assoc_tile(const AssocArgs& a, AssocLds& s, int 
         if (s.c1[tid]) atomicAdd(&T->c1[tid], s.c1[tid]);
         if (s.c2[tid]) atomicAdd(&T->c2[tid], s.c2[tid]);
     }
+    if (tid == 0 && s.pos) atomicMax(&T->pos_max, s.pos);
 }
 
 template <bool OCT>
@@ -2961,10 +3045,17 @@ __device__ void exact_rows_sum(unsigned rows, int j, const DecideArgs& a, float 
 // Certified interval [lo, hi] of the reference's f32 exp(A/C) from the fixed-point sums, and
 // the point estimate mid (see above).  A fixed = the 2^-28 fixed-point sum, n = count.  Each
 // fixed-point term differs from the reference's glibc logf term by at most kTermSlack: half a
-// unit of 2^-28 plus the device logf's distance to glibc's (<= 2 ulp over [eps, 1],
-// tests/test_gpu_assoc_exact.py; 4 ulp at |t| < 4 = 2^-20 allowed).
+// unit of 2^-28 plus the device logf's distance to glibc's (<= 2 ulp over [0.05, 32],
+// tests/test_gpu_assoc_exact.py; 4 ulp at |t| < 4 = 2^-20 allowed).  That needs every term in
+// (-4, 4): the certificate is used only for eps >= 0.05 and terms below log 32 (kPosCap; the
+// decide kernel sends every row to the exact path otherwise).
+// P (>= 0): an upper bound of every positive term.  Recursive f32 summation of n terms errs by
+// at most gamma * sum |x_i| = gamma (|S| + 2 sum of the positive terms) <= gamma (|S| + 2 n P);
+// with P == 0 (every term <= 0) that is the same-sign bound gamma |S|.
 constexpr double kTermSlack = 0x1p-29 + 0x1p-20;
-__device__ __forceinline__ void prob_interval(long long A, long long n, double* lo, double* hi, double* mid) {
+constexpr unsigned kPosCap = 930326397u;  // to_fix(log 32) = 3.4657 * 2^28: terms must stay below it
+__device__ __forceinline__ void prob_interval(long long A, long long n, double P, double* lo, double* hi,
+                                              double* mid) {
     if (n <= 0) { *lo = *hi = *mid = 0.0; return; }
     const double dn = (double)n;
     const double S = (double)A / kFixScale;
@@ -2972,10 +3063,15 @@ __device__ __forceinline__ void prob_interval(long long A, long long n, double* 
     const double g = (dn - 1.0) * 0x1p-24;
     if (g >= 0.5) { *lo = 0.0; *hi = 2.0; return; }  // no certificate: the exact path decides
     const double gam = g / (1.0 - g) * (1.0 + 0x1p-40);
+    // the exact sum of the reference's f32 terms lies in [slo, shi] (it is <= n P)
     const double slo = S - dn * kTermSlack * (1.0 + 0x1p-40);
-    const double shi = fmin(S + dn * kTermSlack * (1.0 + 0x1p-40), 0.0);
-    const double qlo = slo * (1.0 + gam) / dn * (1.0 + 0x1p-24 + 0x1p-40) - 0x1p-60;
-    const double qhi = shi * (1.0 - gam) / dn * (1.0 - 0x1p-24 - 0x1p-40) + 0x1p-60;
+    const double shi = fmin(S + dn * kTermSlack * (1.0 + 0x1p-40), dn * P);
+    // its f32 pixel-order sum, then q = RN(A / n) within 2^-24 relative, then expf within 0.502 ulp
+    const double alo = slo - gam * (fabs(slo) + 2.0 * dn * P);
+    const double ahi = shi + gam * (fabs(shi) + 2.0 * dn * P);
+    const double q0 = alo / dn, q1 = ahi / dn;
+    const double qlo = q0 - fabs(q0) * (0x1p-24 + 0x1p-40) - 0x1p-60;
+    const double qhi = q1 + fabs(q1) * (0x1p-24 + 0x1p-40) + 0x1p-60;
     *lo = exp(qlo) * (1.0 - 0x1p-23 - 0x1p-40);
     *hi = exp(qhi) * (1.0 + 0x1p-23 + 0x1p-40);
 }
@@ -2985,6 +3081,7 @@ struct DecideLds {
     unsigned cand[kMaxObjects];   // flagged rows: the ids that can be their argmax
     int win[kMaxObjects];         // certain rows: the argmax (-1: none / rejected)
     unsigned flagged;
+    unsigned reject;              // rows whose every candidate is certainly <= 3 * prior
     int last;
     double prob[kMaxObjects][kMaxObjects];  // final: exact f32 (flagged rows) or the point estimate
     int bestj[kMaxObjects];
@@ -3068,26 +3165,35 @@ __global__ __launch_bounds__(256) void k_assoc_decide(DecideArgs a) {
         Av[m] = T->t1[i][j] + T->t2[j] - T->t3[i][j];
         Cv[m] = (long long)T->c1[i] + (long long)T->c2[j] - (long long)T->c3[i][j];
     }
+    const unsigned posm = T->pos_max;
     const int max_now = min((int)maxl + 1, kMaxObjects);
     const float thr_f = 3.0f * a.eps;  // tsdf.cu:349, a float product
     const double thr = (double)thr_f;
+    // the certificate's assumptions (prob_interval): every term within (-4, 4), the range the
+    // device logf was checked over; outside it (eps below 0.05, probabilities 32 x n_obs or
+    // more) every present row takes the exact path
+    const bool cert_ok = a.eps >= 0.05f && a.eps < 1.0f && posm < kPosCap;
+    const double P = posm ? ((double)posm + 0.5) / kFixScale + kTermSlack : 0.0;
     // ---- certificate (every workgroup) ----
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
         const int k = tid + 256 * m, i = k / kMaxObjects, j = k % kMaxObjects;
         double lo = 0.0, hi = 0.0, mid = 0.0;
-        if (i >= 1 && j >= 1 && i < max_now) prob_interval(Av[m], Cv[m], &lo, &hi, &mid);
+        if (i >= 1 && j >= 1 && i < max_now) prob_interval(Av[m], Cv[m], P, &lo, &hi, &mid);
         L.lo[i][j] = lo;
         L.hi[i][j] = hi;
         L.mid[i][j] = mid;
     }
-    if (tid == 0) L.flagged = 0u;
+    if (tid == 0) {
+        L.flagged = 0u;
+        L.reject = 0u;
+    }
     __syncthreads();
     if (tid < kMaxObjects) {
         const int i = tid;
         unsigned cand = 0u;
         int win = -1;
-        bool flag = false;
+        bool flag = false, rej = false;
         if (i >= 1 && i < max_now) {
             // point-estimate argmax (first maximum) and the best lower bound
             double mp = 0.0, maxlo = 0.0, maxhi = 0.0;
@@ -3106,6 +3212,7 @@ __global__ __launch_bounds__(256) void k_assoc_decide(DecideArgs a) {
             }
             if (!(maxhi > thr)) {
                 win = -1;  // every candidate is rejected whatever the argmax
+                rej = true;
             } else if (certain && w >= 0 && L.lo[i][w] > thr) {
                 win = w;
                 cand = 1u << w;
@@ -3118,6 +3225,7 @@ __global__ __launch_bounds__(256) void k_assoc_decide(DecideArgs a) {
         L.cand[i] = cand;
         L.win[i] = win;
         if (flag) atomicOr(&L.flagged, 1u << i);
+        if (rej) atomicOr(&L.reject, 1u << i);
     }
     __syncthreads();
     if (tid >= 1 && tid < kMaxObjects) {  // greedy per previous id j: potential winners
@@ -3132,12 +3240,15 @@ __global__ __launch_bounds__(256) void k_assoc_decide(DecideArgs a) {
         if (__popc(W) >= 2) atomicOr(&L.flagged, W);
     }
     __syncthreads();
+    const unsigned present = (max_now >= 32 ? 0xFFFFFFFFu : ((1u << max_now) - 1u)) & ~1u;
     unsigned F = L.flagged;
-    if (a.force_exact) F = ((1u << max_now) - 1u) & ~1u;
+    if (a.force_exact || !cert_ok) F = present;
+    const unsigned R = F == present ? 0u : L.reject & ~F;  // rows certainly rejected (not recomputed)
     if (a.certify_only) {  // one workgroup: report, leave tables and counts as they are
         if (tid == 0) {
             a.D->exact_missing = F;
             a.D->exact_rows = 0u;
+            a.D->reject_rows = R;
         }
         return;
     }
@@ -3150,7 +3261,7 @@ __global__ __launch_bounds__(256) void k_assoc_decide(DecideArgs a) {
     if (F && have_px && blockIdx.x >= 1) {
         const int j = (int)blockIdx.x;
         const float c0 = glibc::logf(fmaxf(0.0f, a.eps));
-        const unsigned rows = F & (max_now >= 32 ? 0xFFFFFFFFu : ((1u << max_now) - 1u)) & ~1u;
+        const unsigned rows = F & present;
         exact_rows_sum(rows, j, a, c0, L.scan, L.srow);
         // write-through (sc1) stores: the deciding workgroup may sit on another XCD
         if (tid < kMaxObjects && ((rows >> tid) & 1u))
@@ -3163,7 +3274,9 @@ __global__ __launch_bounds__(256) void k_assoc_decide(DecideArgs a) {
     if (tid == 0) {
         if (exact) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned ticket = __hip_atomic_fetch_add(&a.X->counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // self-resetting ticket: the nwork-th increment wraps the counter back to 0 (the decides
+        // of one handle never overlap: they share its tables)
+        const unsigned ticket = atomicInc(&a.X->counter, nwork - 1u);
         L.last = ticket == nwork - 1u;
     }
     __syncthreads();
@@ -3230,24 +3343,30 @@ __global__ __launch_bounds__(256) void k_assoc_decide(DecideArgs a) {
         int rank = 0;
         for (int u = 0; u < L.newcount; ++u) rank += L.fresh_first[u] < mine ? 1 : 0;
         lut = num + rank;
+        // id policy 1 (a deviation, SEMTSDF_F_ID_SATURATE): an id without a histogram bin is not
+        // minted, the label becomes background
+        if (a.id_policy == 1 && lut >= kMaxObjects) lut = 0;
     }
+    // policy 0: the reference's ids (tsdf.cu:379-383), stored in the u8 mask modulo 256 as its
+    // mask_ptr[i] = num_objs does; ids >= 32 have no histogram bin (the integrate drops their
+    // votes, counting them: semtsdf_state::label_votes_dropped)
     D->lut[tid] = (unsigned char)lut;
     __syncthreads();
     if (tid == 0) {
-        const int after = num + L.newcount;
         const int mx = (int)T->max_label + 1;
+        const int after = a.id_policy == 1 ? max(num, min(num + L.newcount, kMaxObjects)) : num + L.newcount;
         D->max_obj_now = mx;
         D->num_objs_before = num;
         D->num_objs_after = after;
         D->bad_label = (after > kMaxObjects || mx > kMaxObjects) ? 1 : 0;
         D->exact_rows = Fx;
         D->exact_missing = have_px ? 0u : F;
+        D->reject_rows = R;
         *a.num_objs_dev = after;
         if (Fx) {
             a.X->frames += 1u;
             a.X->rows += (unsigned)__popc(Fx);
         }
-        __hip_atomic_store(&a.X->counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // every read of T is above (the last barrier orders them): clear it for the next frame
     uint2* w = reinterpret_cast<uint2*>(T);
@@ -3292,9 +3411,11 @@ __global__ __launch_bounds__(256) void k_assoc_from_probs(const float* __restric
         if (m > 0 && m < (unsigned)kMaxObjects) {
             atomicAdd(&s.c1[m], 1u);
 #pragma unroll
-            for (int j = 1; j < kMaxObjects; ++j)
-                atomicAdd(reinterpret_cast<unsigned long long*>(&s.t1[m][j]),
-                          (unsigned long long)to_fix(glibc::logf(fmaxf(p[j] / n_obs, eps))));
+            for (int j = 1; j < kMaxObjects; ++j) {
+                const float L = glibc::logf(fmaxf(p[j] / n_obs, eps));
+                atomicAdd(reinterpret_cast<unsigned long long*>(&s.t1[m][j]), (unsigned long long)to_fix(L));
+                if (L > 0.0f) atomicMax(&s.pos, pos_fix(L));  // probabilities above n_obs
+            }
         }
 #pragma unroll
         for (int n = 1; n < kMaxObjects; ++n) {
@@ -3323,6 +3444,7 @@ __global__ __launch_bounds__(256) void k_assoc_from_probs(const float* __restric
         if (s.c1[q]) atomicAdd(&t->c1[q], s.c1[q]);
         if (s.c2[q]) atomicAdd(&t->c2[q], s.c2[q]);
     }
+    if (threadIdx.x == 0 && s.pos) atomicMax(&t->pos_max, s.pos);
 }
 
 hipError_t launch_assoc_from_probs(const float* probs, const uint8_t* box, const uint8_t* mask, int npx, float n_obs,
@@ -3380,7 +3502,7 @@ __global__ __launch_bounds__(256) void k_relabel_records(uint8_t* __restrict__ m
                 for (int j = 0; j < 4; ++j) {
                     const unsigned m = s_lut[(m4 >> (8 * j)) & 0xFFu];
                     o4 |= m << (8 * j);
-                    r[j].y = (r[j].y & 0x00FFFFFFu) | (m << 24);
+                    r[4 * j].y = (r[4 * j].y & 0x00FFFFFFu) | (m << 24);  // a tile is column-major
                 }
                 reinterpret_cast<unsigned*>(row)[x4] = o4;
             }
@@ -3993,8 +4115,11 @@ __global__ __launch_bounds__(256) void k_shard_assoc_partial(ShardRayArgs a) {
         if (mine) assoc_accumulate(s, p, a.mask[px], a.n_obs, a.eps, a.box_thresh);
     }
     __syncthreads();
-    // partial layout: t1[32][32], t3[32][32], t2[32], c1[32], c2[32], c3[32][32] (int64)
+    // partial layout: t1[32][32], t3[32][32], t2[32], c1[32], c2[32], c3[32][32] (int64); the
+    // unused c1[0] word (label 0 has no row) carries the rank's largest positive t1 term
+    // (pos_fix): the group's SUM of it bounds the largest term of the group from above
     unsigned long long* P = reinterpret_cast<unsigned long long*>(a.partial);
+    if (threadIdx.x == 0 && s.pos) atomicMax(P + 2 * kMaxObjects * kMaxObjects + kMaxObjects, (unsigned long long)s.pos);
     const int NN = kMaxObjects * kMaxObjects;
     for (int k = threadIdx.x; k < NN; k += 256) {
         const long long v1 = (&s.t1[0][0])[k];
@@ -4064,9 +4189,10 @@ __global__ void k_tables_from_partial(const long long* __restrict__ P, AssocTabl
     if (threadIdx.x < kMaxObjects) {
         const int i = threadIdx.x;
         T->t2[i] = P[2 * NN + i];
-        T->c1[i] = (unsigned)P[2 * NN + kMaxObjects + i];
+        T->c1[i] = i ? (unsigned)P[2 * NN + kMaxObjects + i] : 0u;
         T->c2[i] = (unsigned)P[2 * NN + 2 * kMaxObjects + i];
     }
+    if (threadIdx.x == 0) T->pos_max = (unsigned)min(P[2 * NN + kMaxObjects], 0xFFFFFFFFll);
 }
 
 static dim3 tile_grid(int w, int h) { return dim3((w + 15) / 16, (h + 15) / 16); }

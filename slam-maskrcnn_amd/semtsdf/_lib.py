@@ -30,6 +30,7 @@ F_GATE_COLOR = 0x2
 F_COLOR_I32 = 0x4
 F_VOTE = 0x8
 F_NO_CULL = 0x10
+F_ID_SATURATE = 0x20
 
 PLACE_SFM = 0
 PLACE_PYTHON = 1
@@ -83,6 +84,7 @@ class State(C.Structure):
         ("local_dim", C.c_int32 * 3),
         ("local_voxels", C.c_uint64),
         ("device_bytes", C.c_uint64),
+        ("label_votes_dropped", C.c_uint64),
     ]
 
 
@@ -94,6 +96,7 @@ class AssocStats(C.Structure):
         ("assigned_prob", C.c_float * MAX_OBJECTS),
         ("lut", C.c_uint8 * 256),
         ("exact_rows", C.c_uint32),
+        ("reject_rows", C.c_uint32),
     ]
 
 

@@ -451,13 +451,17 @@ class DistShardGroup:
                 L.check(rc)
         return st
 
-    def parse_frame_dev(self, depth_ptr: int, rgb_ptr: int, mask_ptr: int, E):
+    def parse_frame_dev(self, depth_ptr: int, rgb_ptr: int, mask_ptr: int, E, want_stats=False):
+        """One frame of the sharded pipeline (association when n_obs > 0, integrate); returns the
+        association's stats when want_stats (None without an association)."""
         import ctypes as C
 
         from . import _lib as L
 
+        st = None
         with self._on_stream():
             if self.vol.state().n_obs > 0:
-                self.associate_dev(mask_ptr, E)
+                st = self.associate_dev(mask_ptr, E, want_stats=want_stats)
             self.vol.integrate_dev(depth_ptr, rgb_ptr, mask_ptr, E, self._stream())
             L.check(L.load().semtsdf_shard_note_integrated(self.vol.handle, C.c_void_p(mask_ptr), self._stream()))
+        return st

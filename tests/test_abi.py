@@ -27,7 +27,7 @@ def test_library_exports_every_symbol():
     lib = L.load()
     for n in declared():
         assert hasattr(lib, n), n
-    assert lib.semtsdf_abi_version() == 10
+    assert lib.semtsdf_abi_version() == 11
     key = lib.semtsdf_build_key().decode()
     assert len(key) == 64 and int(key, 16) >= 0  # the sha-256 build key (__graft_entry__.build_key)
 
@@ -39,7 +39,9 @@ def test_structs_match_header_sizes():
 
     # semtsdf_params: 3 i32 + 13 f32 + 32 f32 + 2 i32 + 5 f32 + u32 + 3 i32
     assert C.sizeof(L.Params) == 4 * (3 + 9 + 1 + 32 + 2 + 5 + 1 + 3)
-    assert C.sizeof(L.AssocStats) == 4 * (2 + 32 + 32) + 256 + 4
+    assert C.sizeof(L.AssocStats) == 4 * (2 + 32 + 32) + 256 + 4 + 4
+    # semtsdf_state: u32 n_obs, i32 num_objs, 3 i32 local_dim (+ 4 B padding), 3 u64
+    assert C.sizeof(L.State) == 4 * 5 + 4 + 8 * 3
     # semtsdf_timing: 16 fields of 8 bytes (doubles or u64)
     assert C.sizeof(L.Timing) == 8 * 17
 
@@ -74,3 +76,24 @@ def test_argument_errors_without_a_device():
     assert rc != 0 and b"NULL" in lib.semtsdf_last_error()
     rc = lib.semtsdf_shard_assoc_apply_exact(None, buf, buf, buf, None, None)
     assert rc != 0 and b"NULL" in lib.semtsdf_last_error()
+
+
+def test_params_validation_without_a_device():
+    """semtsdf_create validates the parameters before touching a device: the association's prior
+    must lie in [2^-10, 1) (the range its f32 rule is evaluated for)."""
+    import ctypes as C
+
+    from semtsdf import _lib as L
+
+    lib = L.load()
+    p = L.Params()
+    intr = (C.c_float * 4)(520.9, 521.0, 325.1, 249.7)
+    assert lib.semtsdf_params_default(C.byref(p), 32, intr, 64, 48) == 0
+    for a in range(3):
+        p.voxel[a] = 0.01
+    p.mu = 0.05
+    for bad in (0.0, -0.05, 1.0, 2.0, float("nan"), 2.0 ** -11):
+        p.prior_mrcnn_err_rate = bad
+        h = C.c_void_p()
+        rc = lib.semtsdf_create(C.byref(p), 0, C.byref(h))
+        assert rc == L.ERR_INVALID and b"prior_mrcnn_err_rate" in lib.semtsdf_last_error(), bad

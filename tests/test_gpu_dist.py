@@ -59,59 +59,69 @@ def _rank(rank, world, port, exchange, q):
         semtsdf.load()
         st = SyntheticStream(seed=0)
         frames = [st.frame(k) for k in range(6)]
-        vol = semtsdf.Volume(_params(semtsdf, L, frames[0], rank, world), 0)
-        grp = DistShardGroup(vol, exchange=exchange)
-        single = semtsdf.Volume(_params(semtsdf, L, frames[0]), 0) if rank == 0 else None
-        out = {"masks": [], "luts": [], "single_masks": [], "single_luts": []}
-        for k in range(1, 6):
-            fr = frames[k]
-            E = (fr.w2c @ frames[0].c2w).astype(np.float32)
-            d = torch.from_numpy(fr.depth.view(np.int16)).cuda()
-            r = torch.from_numpy(fr.rgb).cuda()
-            m = torch.from_numpy(fr.mask.copy()).cuda()
-            torch.cuda.synchronize()  # inputs copied by torch's stream before the volume's stream reads them
-            if vol.state().n_obs > 0:
-                stt = grp.associate_dev(m.data_ptr(), E, want_stats=True)
-                out["luts"].append(bytes(stt.lut))
-            vol.integrate_dev(d.data_ptr(), r.data_ptr(), m.data_ptr(), E, grp._stream())
-            L.check(L.load().semtsdf_shard_note_integrated(vol.handle, L.ptr(m.data_ptr()), grp._stream()))
-            torch.cuda.synchronize()
-            out["masks"].append(m.cpu().numpy())
-            if single is not None:
-                ms = np.ascontiguousarray(fr.mask.copy())
-                s1 = single.parse_frame(fr.depth, fr.rgb, ms, E)
-                out["single_masks"].append(ms)
-                if k >= 2:
-                    out["single_luts"].append(bytes(s1.lut))
-        dist_c = float(np.mean(frames[0].depth[frames[0].depth > 0]) / 5000.0)
-        out["images"], out["single_images"] = [], []
-        p = vol.params
-        for mode in (L.RENDER_LABEL, L.RENDER_COLOR):
-            for angle in (0.0, 0.3):
-                s2w, c = semtsdf.orbit_camera(list(p.Kinv), angle, dist_c)
-                img, t = grp.raycast(s2w, c, mode, want_t=True)
-                torch.cuda.synchronize()
-                out["images"].append((img.cpu().numpy(), t.cpu().numpy()))
-                if single is not None:
-                    out["single_images"].append(single.raycast(s2w, c, mode, want_t=True))
-        torch.cuda.synchronize()
-        out["local"] = vol.download(hist=True)
-        out["state"] = (int(vol.state().n_obs), int(vol.state().num_objs))
-        if single is not None:
-            out["single"] = single.download(hist=True)
-            out["single_state"] = (int(single.state().n_obs), int(single.state().num_objs))
-            single.close()
-        vol.close()
-        q.put((rank, out))
+        q.put((rank, {force: _rank_pass(semtsdf, L, DistShardGroup, torch, frames, rank, world, exchange, force)
+                      for force in (False, True)}))
     finally:
         dist.destroy_process_group()
 
 
+def _rank_pass(semtsdf, L, DistShardGroup, torch, frames, rank, world, exchange, force):
+    """One pass of a rank: force=True sends every association row of the shard group to the exact
+    path, so every frame's decision runs DistShardGroup.associate_dev's NEED_PIXELS branch (the
+    per-pixel data of every shard, an int32 all-reduce SUM, assoc_apply_exact)."""
+    vol = semtsdf.Volume(_params(semtsdf, L, frames[0], rank, world), 0)
+    vol.set_instrumentation(events=False, force_exact=force)
+    grp = DistShardGroup(vol, exchange=exchange)
+    single = semtsdf.Volume(_params(semtsdf, L, frames[0]), 0) if rank == 0 else None
+    out = {"masks": [], "luts": [], "single_masks": [], "single_luts": [], "exact_rows": []}
+    for k in range(1, 6):
+        fr = frames[k]
+        E = (fr.w2c @ frames[0].c2w).astype(np.float32)
+        d = torch.from_numpy(fr.depth.view(np.int16)).cuda()
+        r = torch.from_numpy(fr.rgb).cuda()
+        m = torch.from_numpy(fr.mask.copy()).cuda()
+        torch.cuda.synchronize()  # inputs copied by torch's stream before the volume's stream reads them
+        if vol.state().n_obs > 0:
+            stt = grp.associate_dev(m.data_ptr(), E, want_stats=True)
+            out["luts"].append(bytes(stt.lut))
+            out["exact_rows"].append(int(stt.exact_rows))
+        vol.integrate_dev(d.data_ptr(), r.data_ptr(), m.data_ptr(), E, grp._stream())
+        L.check(L.load().semtsdf_shard_note_integrated(vol.handle, L.ptr(m.data_ptr()), grp._stream()))
+        torch.cuda.synchronize()
+        out["masks"].append(m.cpu().numpy())
+        if single is not None:
+            ms = np.ascontiguousarray(fr.mask.copy())
+            s1 = single.parse_frame(fr.depth, fr.rgb, ms, E)
+            out["single_masks"].append(ms)
+            if k >= 2:
+                out["single_luts"].append(bytes(s1.lut))
+    dist_c = float(np.mean(frames[0].depth[frames[0].depth > 0]) / 5000.0)
+    out["images"], out["single_images"] = [], []
+    p = vol.params
+    for mode in (L.RENDER_LABEL, L.RENDER_COLOR):
+        for angle in (0.0, 0.3):
+            s2w, c = semtsdf.orbit_camera(list(p.Kinv), angle, dist_c)
+            img, t = grp.raycast(s2w, c, mode, want_t=True)
+            torch.cuda.synchronize()
+            out["images"].append((img.cpu().numpy(), t.cpu().numpy()))
+            if single is not None:
+                out["single_images"].append(single.raycast(s2w, c, mode, want_t=True))
+    torch.cuda.synchronize()
+    out["local"] = vol.download(hist=True)
+    out["state"] = (int(vol.state().n_obs), int(vol.state().num_objs))
+    if single is not None:
+        out["single"] = single.download(hist=True)
+        out["single_state"] = (int(single.state().n_obs), int(single.state().num_objs))
+        single.close()
+    vol.close()
+    return out
+
+
 @pytest.mark.parametrize("exchange", ["min", "allgather"])
 def test_dist_shard_group_two_ranks_equals_single_volume(exchange):
+    """Two gloo ranks, each pass of them: the certified decision, then every row forced onto the
+    exact path (the multi-process NEED_PIXELS exchange, shard.py DistShardGroup.associate_dev)."""
     import torch.multiprocessing as mp
-
-    from semtsdf.shard import ShardLayout
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -126,9 +136,18 @@ def test_dist_shard_group_two_ranks_equals_single_volume(exchange):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0, f"rank exit code {p.exitcode}"
+    for force in (False, True):
+        _check_two_ranks({r: res[r][force] for r in (0, 1)}, force)
+
+
+def _check_two_ranks(res, force):
+    from semtsdf.shard import ShardLayout
+
     r0 = res[0]
     for rank in (0, 1):
         o = res[rank]
+        if force:  # every decision took the exchanged exact path on every rank
+            assert len(o["exact_rows"]) == 4 and all(x != 0 for x in o["exact_rows"]), o["exact_rows"]
         for k, (m, ms) in enumerate(zip(o["masks"], r0["single_masks"])):
             assert np.array_equal(m.reshape(-1), ms.reshape(-1)), (rank, k)
         assert o["luts"] == r0["single_luts"], rank
@@ -172,12 +191,15 @@ def _rccl_rank(port, q):
         dist_c = float(np.mean(frames[0].depth[frames[0].depth > 0]) / 5000.0)
         res = {}
         user = torch.cuda.Stream()
-        for exchange in ("min", "allgather"):
+        for exchange, force in (("min", False), ("allgather", False), ("min", True), ("allgather", True)):
             vol = semtsdf.Volume(_params(semtsdf, L, frames[0], 0, 1), 0)
+            # force: every row on the exact path (the NEED_PIXELS branch: assoc_pixels, an int32
+            # all-reduce SUM over RCCL, assoc_apply_exact)
+            vol.set_instrumentation(events=False, force_exact=force)
             grp = DistShardGroup(vol, exchange=exchange)
             assert grp.nccl
             single = semtsdf.Volume(_params(semtsdf, L, frames[0]), 0)
-            masks, smasks, imgs, simgs = [], [], [], []
+            masks, smasks, imgs, simgs, xrows = [], [], [], [], []
             with torch.cuda.stream(user):
                 for k in range(1, 6):
                     fr = frames[k]
@@ -186,7 +208,9 @@ def _rccl_rank(port, q):
                     d = torch.from_numpy(fr.depth.view(np.int16)).cuda().clone()
                     r = torch.from_numpy(fr.rgb).cuda().clone()
                     m = torch.from_numpy(fr.mask.copy()).cuda().add(0)
-                    grp.parse_frame_dev(d.data_ptr(), r.data_ptr(), m.data_ptr(), E)
+                    sst = grp.parse_frame_dev(d.data_ptr(), r.data_ptr(), m.data_ptr(), E, want_stats=True)
+                    if sst is not None:
+                        xrows.append(int(sst.exact_rows))
                     masks.append(m.cpu().numpy())  # consumed on the caller's stream
                     ms = np.ascontiguousarray(fr.mask.copy())
                     single.parse_frame(fr.depth, fr.rgb, ms, E)
@@ -199,7 +223,7 @@ def _rccl_rank(port, q):
                         imgs.append((img.cpu().numpy(), t.cpu().numpy()))
                         simgs.append(single.raycast(s2w, c, mode, want_t=True))
             torch.cuda.synchronize()
-            res[exchange] = dict(masks=masks, smasks=smasks, imgs=imgs, simgs=simgs,
+            res[(exchange, force)] = dict(masks=masks, smasks=smasks, imgs=imgs, simgs=simgs, xrows=xrows,
                                  state=(int(vol.state().n_obs), int(vol.state().num_objs)),
                                  sstate=(int(single.state().n_obs), int(single.state().num_objs)),
                                  vol=vol.download(hist=True), single=single.download(hist=True))
@@ -217,7 +241,8 @@ def _rccl_rank(port, q):
 def test_dist_shard_group_rccl_world1_equals_single_volume():
     """DistShardGroup on the RCCL backend (world size 1: RCCL refuses two ranks on the one
     GPU of the test box): the sharded association + integrate + composite raycast, with both
-    exchanges (all-reduce MIN, all_gather_into_tensor), equal the single volume bit for bit."""
+    exchanges (all-reduce MIN, all_gather_into_tensor), equal the single volume bit for bit --
+    with the certified decision and with every row forced onto the exchanged exact path."""
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
@@ -228,7 +253,9 @@ def test_dist_shard_group_rccl_world1_equals_single_volume():
     proc.join(timeout=60)
     assert kind == "ok", res
     assert proc.exitcode == 0
-    for exchange, o in res.items():
+    for (exchange, force), o in res.items():
+        if force:
+            assert len(o["xrows"]) == 4 and all(x != 0 for x in o["xrows"]), o["xrows"]
         for k, (m, ms) in enumerate(zip(o["masks"], o["smasks"])):
             assert np.array_equal(m.reshape(-1), ms.reshape(-1)), (exchange, k)
         assert o["state"] == o["sstate"], exchange

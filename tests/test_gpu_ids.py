@@ -1,0 +1,143 @@
+"""Instance ids past the histogram (include/semtsdf.h SEMTSDF_F_ID_SATURATE).
+
+The reference gives every unmatched label the id num_objs++ without a bound
+(src/SfM_CUDA/tsdf.cu:379-383; the u8 mask stores it modulo 256) and its integrate counts an
+id >= 32 in the bins of the next voxel (tsdf.cu:61, out of bounds).  Here a stream whose masks
+keep introducing new instances drives more than 40 distinct ids through parse_frame_dev:
+
+* policy 0 (default): the reference's ids and object count, votes of ids >= 32 dropped and
+  counted (semtsdf_state.label_votes_dropped); the host parse_frame reports ERR_LABEL for such
+  a frame after applying it in full, and the handle keeps integrating;
+* policy 1 (SEMTSDF_F_ID_SATURATE, a documented deviation): a label that would get an id >= 32
+  becomes background, num_objs stops at 32, nothing is dropped.
+
+Both are checked frame by frame against the C oracle (oracle_filter_overlaps with its id_policy
+extension, the oracle's march and integrate on the same volume state): relabelled masks, object
+counts and, at the end, every array of the volume.
+"""
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+KI = (520.9, 521.0, 325.1, 249.7)
+D = 64
+NFR = 9
+
+
+def _frames():
+    from semtsdf.synth import SyntheticStream
+
+    st = SyntheticStream(seed=3)
+    frames = [st.frame(k) for k in range(NFR)]
+    rng = np.random.default_rng(11)
+    masks = []
+    for k, fr in enumerate(frames):
+        # 9 instance rectangles per frame at fresh places: most labels match no previous id
+        m = np.zeros((480, 640), np.uint8)
+        for lab in range(1, 10):
+            y, x = int(rng.integers(0, 400)), int(rng.integers(0, 560))
+            h, w = int(rng.integers(40, 80)), int(rng.integers(40, 80))
+            m[y:y + h, x:x + w] = lab
+        m[fr.depth == 0] = 0
+        masks.append(m)
+    return frames, masks
+
+
+def _oracle_run(oracle, p, frames, masks, policy):
+    """The reference rule on the oracle: per frame the association (march + filter_overlaps with
+    the id policy) on the state before it, then the integrate of the relabelled mask (the
+    oracle's integrate drops labels >= 32 like the engine)."""
+    g = oracle.OGeom.from_params(p)
+    ost = oracle.OState([D, D, D], p.mu, semantic=True)
+    Ki = np.ascontiguousarray(np.array(list(p.Kinv), np.float32))
+    out, nums = [], []
+    num = 0
+    for k, (fr, m0) in enumerate(zip(frames, masks)):
+        E = (fr.w2c @ frames[0].c2w).astype(np.float32)
+        m = m0.copy()
+        if k == 0:
+            num = int(m.max()) + 1
+        else:
+            probs = np.zeros(640 * 480 * 32, np.float32)
+            box = np.zeros(640 * 480 * 32, np.uint8)
+            E16 = np.ascontiguousarray(E.reshape(16))
+
+            def band(r):
+                oracle.lib().oracle_march_probs(oracle._p(g.dims), oracle._p(g.geo), oracle._p(oracle.k9(Ki)),
+                                                oracle._p(E16), 640, 480, oracle._p(ost.sdf), oracle._p(ost.hist),
+                                                float(p.box_thresh), oracle._p(probs), oracle._p(box), r[0], r[1])
+
+            with ThreadPoolExecutor(8) as ex:
+                list(ex.map(band, [(y, y + 60) for y in range(0, 480, 60)]))
+            m, num, _, _, _ = oracle.filter_overlaps(probs, box, m, k, num, 0.05, precision=0, id_policy=policy)
+        oracle.integrate(g, ost, list(p.K), E, fr.depth, fr.rgb, m, flags=0x3)
+        out.append(m)
+        nums.append(num)
+    return out, nums, ost
+
+
+@pytest.mark.parametrize("policy", [0, 1])
+def test_more_than_31_ids_follow_the_id_policy(oracle, policy):
+    import semtsdf
+    from semtsdf import _lib as L
+    from semtsdf.volume import DeviceBuffer
+
+    semtsdf.load()
+    frames, masks = _frames()
+    mean_m = float(np.mean(frames[0].depth[frames[0].depth > 0])) / 5000.0
+
+    def params():
+        p = semtsdf.default_params(D, KI, 640, 480)
+        semtsdf.place_from_frame(p, frames[0].depth, mean_m, L.PLACE_SFM)
+        p.flags = L.F_SEMANTIC | L.F_GATE_COLOR | (L.F_ID_SATURATE if policy == 1 else 0)
+        return p
+
+    p = params()
+    ref_masks, ref_nums, ost = _oracle_run(oracle, p, frames, masks, policy)
+    # the stream does reach past the histogram under the reference's rule
+    assert ref_nums[-1] >= 32 if policy == 1 else ref_nums[-1] >= 40, ref_nums
+
+    vol = semtsdf.Volume(p, 0)  # device pipeline (parse_frame_dev)
+    host = semtsdf.Volume(params(), 0)  # host pipeline (parse_frame): the synchronous error report
+    npx = 640 * 480
+    dbuf, rbuf, mbuf = DeviceBuffer(npx * 2), DeviceBuffer(npx * 3), DeviceBuffer(npx)
+    label_errors = 0
+    for k, (fr, m) in enumerate(zip(frames, masks)):
+        E = (fr.w2c @ frames[0].c2w).astype(np.float32)
+        dbuf.upload(fr.depth, vol.stream)
+        rbuf.upload(fr.rgb, vol.stream)
+        mbuf.upload(m, vol.stream)
+        vol.parse_frame_dev(dbuf.ptr, rbuf.ptr, mbuf.ptr, E)
+        got = np.zeros(npx, np.uint8)
+        mbuf.download(got, vol.stream)
+        vol.sync()
+        assert np.array_equal(got, ref_masks[k].reshape(-1)), f"frame {k}"
+        st = vol.state()
+        assert st.num_objs == ref_nums[k], (k, st.num_objs, ref_nums[k])
+        mh = np.ascontiguousarray(m.copy())
+        try:
+            host.parse_frame(fr.depth, fr.rgb, mh, E)
+        except L.SemTSDFError as e:  # the frame is applied in full before the error is reported
+            assert e.code == L.ERR_LABEL and policy == 0, (k, str(e))
+            label_errors += 1
+        assert np.array_equal(mh.reshape(-1), ref_masks[k].reshape(-1)), f"host frame {k}"
+        assert host.state().num_objs == ref_nums[k]
+    st = vol.state()
+    if policy == 0:
+        assert st.num_objs >= 40 and st.label_votes_dropped > 0 and label_errors >= 2
+    else:
+        assert st.num_objs == 32 and st.label_votes_dropped == 0 and label_errors == 0
+        assert max(int(x.max()) for x in ref_masks) < 32
+    for v in (vol, host):
+        out = v.download(hist=True)
+        assert np.array_equal(out["sdf"].view(np.uint32), ost.sdf.view(np.uint32))
+        assert np.array_equal(out["wt"], ost.wt) and np.array_equal(out["color"], ost.color)
+        assert np.array_equal(out["hist"], ost.hist)
+    assert int(ost.hist.reshape(-1, 32).sum()) > 100_000
+    for b in (dbuf, rbuf, mbuf):
+        b.free()
+    vol.close()
+    host.close()
