@@ -115,6 +115,7 @@ struct semtsdf_vol {
     uint8_t* render_d = nullptr;
     float* render_t_d = nullptr;
     unsigned long long* counters_d = nullptr;
+    IntegrateRare* rare_d = nullptr;  // the integrate's rare-path fields (IntegrateArgs::rare)
     float* rcp_table_d = nullptr;    // RN(1/n), n = 1..kRcpTable
     AssocDecision* decision_h = nullptr;  // pinned
     // Z-sharded raycast protocol (allocated on first use)
@@ -185,7 +186,7 @@ void free_all(semtsdf_vol* v) {
                     v->fs[1].pyr.l0, v->fs[1].pyr.l1, v->tables_d, v->decision_d,
                     v->num_objs_d, v->probs_d, v->box_d, v->palette_d, v->render_d, v->render_t_d,
                     v->counters_d, v->ray_state_d, v->fs[0].unit_list, v->fs[0].list_count, v->fs[1].unit_list,
-                    v->fs[1].list_count, v->rcp_table_d, v->wtrace_d, v->exact_d, v->px.bits, v->px.p, v->tile_cost_d, v->tile_perm_d};
+                    v->fs[1].list_count, v->rcp_table_d, v->wtrace_d, v->exact_d, v->px.bits, v->px.p, v->tile_cost_d, v->tile_perm_d, v->rare_d};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (v->decision_h) (void)hipHostFree(v->decision_h);
@@ -396,6 +397,7 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
     semtsdf_vol::FrameSet& F = v->fs[fset];
     a.pyr = F.pyr;
     a.counters = v->counters_d;
+    a.rare = v->rare_d;
     a.unit_list = F.unit_list;
     a.list_count = F.list_count;
     a.rcp_table = v->rcp_table_d;
@@ -1049,6 +1051,12 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
     }
     if ((rc = dev_alloc(v, (void**)&v->num_objs_d, 16))) return bail(rc);
     if ((rc = dev_alloc(v, (void**)&v->counters_d, kCounters * sizeof(unsigned long long)))) return bail(rc);
+    if ((rc = dev_alloc(v, (void**)&v->rare_d, sizeof(IntegrateRare)))) return bail(rc);
+    {
+        const IntegrateRare r{v->b.bdirty, v->b.dlist, g.nby, g.nbz, v->counters_d};
+        if (hipMemcpy(v->rare_d, &r, sizeof(r), hipMemcpyHostToDevice) != hipSuccess)
+            return bail(fail(SEMTSDF_ERR_HIP, "upload of the integrate's rare-path fields failed"));
+    }
     if ((rc = dev_alloc(v, (void**)&v->palette_d, sizeof(kPalette)))) return bail(rc);
     if (hipHostMalloc((void**)&v->decision_h, sizeof(AssocDecision), 0) != hipSuccess)
         return bail(fail(SEMTSDF_ERR_HIP, "hipHostMalloc failed"));

@@ -104,6 +104,16 @@ __device__ inline unsigned rec_index(const DepthPyramid& p, unsigned u, unsigned
     return __umul24(v >> 2, p.rs) + ((u << 2) | (v & 3u));
 }
 
+// What the integrate reads only on its rare paths (a voxel crossing the marches' skip threshold,
+// an id without a histogram bin), in device memory (one per volume, filled at create): loaded in
+// those paths only, so the kernel does not hold them in scalar registers through its loop.
+struct IntegrateRare {
+    uint32_t* bdirty;                // VolBufs::bdirty, dlist (nullptr: no empty-space maps)
+    uint32_t* dlist;
+    int nby, nbz;                    // VolGeom::nby, nbz
+    unsigned long long* counters;    // IntegrateArgs::counters
+};
+
 struct IntegrateArgs {
     VolGeom g;
     VolBufs b;
@@ -142,6 +152,7 @@ struct IntegrateArgs {
     const uint8_t* lut;            // deferred relabel of an association decision (256 bytes, device): the
                                    // pixel records carry the frame's raw labels; nullptr: none
     uint8_t* relabel_mask;         // the frame's mask, relabelled in place through lut by the kernel (nullable)
+    const IntegrateRare* rare;     // rare-path fields (device memory)
 };
 constexpr int kWaveTraceWords = 8;
 

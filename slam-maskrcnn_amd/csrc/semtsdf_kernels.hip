@@ -1059,6 +1059,7 @@ struct Proj {
     int lin[4];    // vote mode: the pixel's row-major index, W*H off-image or on an invalid plane
     unsigned sflag;  // steady flag of the lane's sdf line (below)
     unsigned vmask;  // bit k: plane l0 + k is a voxel of the volume (others are never touched)
+    uint32_t ub;     // tiled index of the lane's unit's first voxel (unit_tile), carried to load and store
 };
 
 struct Cls {
@@ -1069,6 +1070,7 @@ struct Cls {
     unsigned hlab;
     int img[4];        // vote mode
     unsigned sflag;    // steady flag of the lane's sdf line
+    uint32_t ub;       // Proj::ub
 };
 
 // What stage_store needs of a classification: masks, histogram mode/label and the 4 labels.
@@ -1103,6 +1105,7 @@ struct Out {
     bool lazy;       // the line's weights take one more pending increment (flag byte + 1)
     unsigned oflag;  // the line's steady flag before this update
     bool cross;      // a voxel's sdf crossed the skip threshold (its brick's map entry may flip)
+    uint32_t ub;     // Proj::ub of the unit
     uint4 c8;
     int4 c32[4];
     uint4 h4;
@@ -1114,8 +1117,9 @@ struct Out {
 template <bool SHARD, bool PIN, bool FREE, bool FULL, bool LIN>
 __device__ __forceinline__ void stage_project(const IntegrateArgs& a, const UnitPos& up, int lane, Proj& P) {
     const VolGeom& g = a.g;
+    P.ub = (uint32_t)unit_tile(g, up);
     if (FULL) {  // full free unit (unit_cull == 3): every voxel touched with f == 1, nothing to project
-        P.sflag = SEMTSDF_STEADY ? (unsigned)a.b.sflag[(unit_tile(g, up) + (unsigned)lane_zq(lane) * 32u +
+        P.sflag = SEMTSDF_STEADY ? (unsigned)a.b.sflag[(P.ub + (unsigned)lane_zq(lane) * 32u +
                                                         (unsigned)lane_y(lane) * 4u) >> 5]
                                  : 0u;
 #pragma unroll
@@ -1152,7 +1156,9 @@ __device__ __forceinline__ void stage_project(const IntegrateArgs& a, const Unit
         w0 = l0 - cblk * per;
         vmask = 0u;
     } else {
-        vmask = row_ok ? (0xFu >> (4 - min(g.lz - l0, 4))) : 0u;
+        // planes l0 .. lz - 1 of the lane (l0 < lz + 16: the shift stays below 20); a listed unit has
+        // x < dimx, so only its y rows and its slot can be invalid
+        vmask = (up.ok & (y < g.dimy)) ? (0xFu >> (4 - min(g.lz - l0, 4))) : 0u;
     }
     // floor(sx/sz), floor(sy/sz) through the reciprocal: |qu - RN(sx/sz)| <= 2^-22 |qu|, so for
     // |qu| < B (host: B = 2^ceil(log2(max(W, H) + 2))) a fraction farther than B 2^-21 from 0
@@ -1215,7 +1221,7 @@ __device__ __forceinline__ void stage_project(const IntegrateArgs& a, const Unit
                                 : npx;
     }
     // steady flag of the lane's sdf line (one byte per 128-B line, unconditional)
-    P.sflag = SEMTSDF_STEADY ? (unsigned)a.b.sflag[(unit_tile(g, up) + (unsigned)lane_zq(lane) * 32u +
+    P.sflag = SEMTSDF_STEADY ? (unsigned)a.b.sflag[(P.ub + (unsigned)lane_zq(lane) * 32u +
                                                     (unsigned)lane_y(lane) * 4u) >> 5]
                              : 0u;
     // unconditional gathers (an off-image voxel reads a zero record: depth 0); a free unit needs
@@ -1274,6 +1280,7 @@ __device__ __forceinline__ void stage_classify(const IntegrateArgs& a, const Pro
         }
         tm &= P.vmask;
         C.sflag = P.sflag;
+        C.ub = P.ub;
         if (kProbes && (a.debug == 3 || a.debug == 21)) tm = 0u;  // probe: no state traffic
         C.tmask = tm;
         C.gmask = 0u;
@@ -1307,6 +1314,7 @@ __device__ __forceinline__ void stage_classify(const IntegrateArgs& a, const Pro
         for (int k = 0; k < 4; ++k) C.pix[k] = relabel_rec(C.pix[k], lutv);
     }
     C.sflag = P.sflag;
+    C.ub = P.ub;
     if (!(dmin >= 0x1p-60f) || !a.fastdiv) {  // rare: tiny differences, or mu outside the reciprocal range
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -1314,10 +1322,14 @@ __device__ __forceinline__ void stage_classify(const IntegrateArgs& a, const Pro
             if (!a.fastdiv || !(fabsf(dc) >= 0x1p-60f)) C.fv[k] = dc == 0.0f ? dc : dc / g.mu;
         }
     }
-    unsigned gmask = 0;
+    // gated: touched and f < gate (tsdf.cu:57): the gate bits in a VGPR, then one AND
+    unsigned gbits = 0xFu;
+    if (GATE) {
+        gbits = 0u;
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-        gmask |= (((((tmask >> k) & 1u) != 0u) & (!GATE || C.fv[k] < a.gate)) ? 1u : 0u) << k;
+        for (int k = 0; k < 4; ++k) gbits |= (C.fv[k] < a.gate ? 1u : 0u) << k;
+    }
+    unsigned gmask = tmask & gbits;
     if (COUNT && count) {
         n_touch += __popc(tmask);
         n_gate += __popc(gmask);
@@ -1418,9 +1430,12 @@ __device__ __forceinline__ void stage_load(const IntegrateArgs& a, const UnitPos
     const VolGeom& g = a.g;
     // wave-uniform unit bases (scalar) + the lane's 32-bit element offset; a lane with
     // nothing to load reads the unit's first vector instead (same line for all of them)
-    const uint64_t ub = unit_tile(g, up);
-    const uint64_t v = ub + coff;
-    const uint4* dummy = reinterpret_cast<const uint4*>(a.rcp_table);
+    (void)up;
+    const uint32_t ub = C.ub;
+    const uint32_t v = ub + coff;
+    // a lane with nothing to load reads the array's first vector (offset 0): one base pointer
+    // per array, the offset selected in 32 bits
+    const uint4* dummy = reinterpret_cast<const uint4*>(a.b.sdf);
     const bool t = tile_line_any(C.tmask != 0u), gt = tile_line_any(C.gmask != 0u);
     const unsigned lt = t ? coff : 0u, lg = gt ? coff : 0u;
     // Steady line: every sdf of the line is exactly 1.0f with weight < 2^23 (flag) and every
@@ -1436,18 +1451,17 @@ __device__ __forceinline__ void stage_load(const IntegrateArgs& a, const UnitPos
                       tile_line_all((C.sflag != 0u) & (C.sflag < kFlagMax) & fone & (C.tmask == 15u));
     L.skip = skip;
     L.lazy = lazy;
-    L.s4 = ld_state<float4>(skip ? reinterpret_cast<const float*>(dummy) : a.b.sdf + ub + lt);
-    L.w4 = ld_state<int4>(lazy ? reinterpret_cast<const int*>(dummy) : a.b.wt + ub + lt);
+    L.s4 = ld_state<float4>(a.b.sdf + (skip ? 0u : ub + lt));
+    L.w4 = ld_state<int4>(a.b.wt + (lazy ? 0u : ub + lt));
     if (FREE) return;  // sdf and weight only
     if (CI32) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) L.c32[k] = reinterpret_cast<const int4*>(a.b.color)[ub + lg + (gt ? k : 0)];
+        for (int k = 0; k < 4; ++k) L.c32[k] = reinterpret_cast<const int4*>(a.b.color)[(uint64_t)ub + lg + (gt ? k : 0)];
     } else {
         L.c8 = ld_state<uint4>(reinterpret_cast<const uint32_t*>(a.b.color) + ub + lg);
     }
     if (SEM)
-        L.h4 = ld_state<uint4, SEMTSDF_NT_HIST>(
-            C.hmode == 1u ? reinterpret_cast<const uint4*>(a.b.hist + (uint64_t)C.hlab * g.nvox + v) : dummy);
+        L.h4 = ld_state<uint4, SEMTSDF_NT_HIST>(a.b.hist + (C.hmode == 1u ? (uint64_t)C.hlab * g.nvox + v : 0ull));
     if (VOTE) {
         L.vc4 = *(t ? reinterpret_cast<const int4*>(a.b.cls + v) : reinterpret_cast<const int4*>(dummy));
         L.vn4 = *(t ? reinterpret_cast<const int4*>(a.b.cls_cnt + v) : reinterpret_cast<const int4*>(dummy));
@@ -1466,6 +1480,7 @@ __device__ __forceinline__ void stage_compute(const IntegrateArgs& a, const floa
     O.skip = L.skip;
     O.lazy = L.lazy;
     O.oflag = C.sflag;
+    O.ub = C.ub;
     // the stored weights plus the line's pending increments (0 unless the line is steady)
     const int pend = (SEMTSDF_STEADY && SEMTSDF_LAZY_WEIGHT && C.sflag) ? (int)C.sflag - 1 : 0;
     const int wo[4] = {L.w4.x + pend, L.w4.y + pend, L.w4.z + pend, L.w4.w + pend};
@@ -1499,10 +1514,12 @@ __device__ __forceinline__ void stage_compute(const IntegrateArgs& a, const floa
     }
     O.s4 = make_float4(sn[0], sn[1], sn[2], sn[3]);
     O.w4 = make_int4(wn[0], wn[1], wn[2], wn[3]);
-    bool cross = false;
+    // a voxel crossed the threshold when so - thr and sn - thr differ in sign (each difference is
+    // exact or keeps its sign; neither is -0): the sign bit of their XOR, ORed over the lane
+    unsigned xs = 0u;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) cross |= (so[k] < a.skip_thr) != (sn[k] < a.skip_thr);
-    O.cross = cross;
+    for (int k = 0; k < 4; ++k) xs |= __float_as_uint(so[k] - a.skip_thr) ^ __float_as_uint(sn[k] - a.skip_thr);
+    O.cross = (int)xs < 0;
     if (FREE) return;  // no colour, histogram or vote state
     if (CI32) {  // tsdf.cu:57-62 on i32 colour; unchanged voxels of a stored row pass through
         // (element-wise selects: a select of whole int4 values is lowered through scratch)
@@ -1590,23 +1607,24 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
     const bool line = SEMTSDF_FULLROW ? trow : ((__ballot(tmask != 0u) >> ((int)__lane_id() % LZQ +
                                                  lane_slot((int)__lane_id()) * kUnitLanes)) & kLineLanes) != 0ull;
     if (!line) return;
-    const uint64_t v = unit_tile(g, up) + coff;
-    if (a.b.bdirty) {
+    const uint64_t v = O.ub + coff;
+    {
         // a brick of the empty-space map changes only where a voxel crossed the threshold:
         // z-brick j of the unit holds the lanes of z-quads 2j, 2j+1 (lane = zq + 8 y)
         const uint64_t cb = __ballot(O.cross);
-        if (cb) {  // rare: most updates keep their side of the threshold
+        const IntegrateRare* R = a.rare;
+        if (cb && R->bdirty) {  // rare: most updates keep their side of the threshold
             // lane j of a slot marks z-brick j of its unit (z-quads 2j, 2j+1)
             const int lane = (int)__lane_id(), j = lane % kUnitLanes;
             const int bz = (up.uz * UZ >> 3) + j;
             const uint64_t pj = ((kLineLanes << (2 * (j & 3))) | (kLineLanes << (2 * (j & 3) + 1)))
                                 << (lane_slot(lane) * kUnitLanes);
-            if (j < UZ / 8 && (cb & pj) && bz < g.nbz) {
+            if (j < UZ / 8 && (cb & pj) && bz < R->nbz) {
                 // the quad's dirty word; the lane that turns it nonzero lists the quad
-                const unsigned nbq = (unsigned)(g.nbz + 3) >> 2;
-                const unsigned q = __umul24(__umul24((unsigned)(up.x * UX >> 3), (unsigned)g.nby) +
+                const unsigned nbq = (unsigned)(R->nbz + 3) >> 2;
+                const unsigned q = __umul24(__umul24((unsigned)(up.x * UX >> 3), (unsigned)R->nby) +
                                                 (unsigned)(up.uy * UY >> 3), nbq) + ((unsigned)bz >> 2);
-                if (atomicOr(&a.b.bdirty[q], 1u << (bz & 3)) == 0u) a.b.dlist[1 + atomicAdd(&a.b.dlist[0], 1u)] = q;
+                if (atomicOr(&R->bdirty[q], 1u << (bz & 3)) == 0u) R->dlist[1 + atomicAdd(&R->dlist[0], 1u)] = q;
             }
         }
     }
@@ -1616,8 +1634,13 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
         st_state(a.b.wt + v, O.w4);
     }
     if (SEMTSDF_STEADY) {  // the line's flag byte after this update (one lane per line writes)
-        const bool vals = (O.s4.x == 1.0f) & (O.s4.y == 1.0f) & (O.s4.z == 1.0f) & (O.s4.w == 1.0f) &
-                          (O.w4.x < (1 << 23)) & (O.w4.y < (1 << 23)) & (O.w4.z < (1 << 23)) & (O.w4.w < (1 << 23));
+        // every sdf exactly 1.0f (bits: AND and OR of the four both equal 1.0f's) and every weight < 2^23
+        const unsigned s_and = __float_as_uint(O.s4.x) & __float_as_uint(O.s4.y) & __float_as_uint(O.s4.z) &
+                               __float_as_uint(O.s4.w);
+        const unsigned s_or = __float_as_uint(O.s4.x) | __float_as_uint(O.s4.y) | __float_as_uint(O.s4.z) |
+                              __float_as_uint(O.s4.w);
+        const int wmx = max(max(O.w4.x, O.w4.y), max(O.w4.z, O.w4.w));
+        const bool vals = (s_and == 0x3f800000u) & (s_or == 0x3f800000u) & (wmx < (1 << 23));
         // a lane that did not load its values (per-lane traffic) keeps what the old flag says
         const bool one = trow ? vals : (O.oflag != 0u);
         // a lazy line counts one more pending increment; any other update stored the weights
@@ -1661,7 +1684,7 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
                 }
                 // an id without a histogram bin (tsdf.cu:61 writes past the voxel's 32 bins): the
                 // vote is dropped and counted
-                if (bad) atomicAdd(a.counters + 2, (unsigned long long)bad);
+                if (bad) atomicAdd(a.rare->counters + 2, (unsigned long long)bad);
             }
         }
     }
