@@ -143,7 +143,8 @@ struct IntegrateArgs {
     float rmu;                     // RN(1/mu), for the exact division by mu (k_integrate)
     int fastdiv;                   // mu in [2^-20, 2^20]: divisions by mu/(w+1) via RN reciprocals
     unsigned* unit_list;           // live units: three lists (general, free, full free) of kListSegs segments (k_cull_units)
-    unsigned* list_count;          // [3][kListSegs * kListCountStride] entries per segment (zeroed by the frame prepass)
+    unsigned* list_count;          // [3][kListSegs * kListCountStride] entries per segment, then the dynamic tail
+                                   // counters of the 8 XCDs (all zeroed by the frame prepass)
     int free_ok;                   // free units allowed: gated colour with gate <= 1 (f == 1 updates sdf/weight only)
     int color_wide;                // colour stored as int32 x 4 (else u8 x 4; see semtsdf_vol::color_wide)
     unsigned long long* wtrace;    // instrumentation (build with SEMTSDF_WAVE_TRACE=1, run with

@@ -590,6 +590,8 @@ __device__ __forceinline__ void pyramid_tile(const uint16_t* __restrict__ depth,
     auto relab = [&](unsigned m) { return (s_lut[m >> 2] >> (8 * (m & 3))) & 0xFFu; };
     if (list_count && tx == 0 && ty == 0 && t < kLists * kListSegs)  // this frame's lists (general, free, full)
         list_count[(t & (kListSegs - 1)) * kListCountStride + (t >> 6) * kListSegs * kListCountStride] = 0u;
+    if (list_count && tx == 0 && ty == 0 && t < 8)  // the integrate's dynamic tail counters, one per XCD
+        list_count[(kLists * kListSegs + t) * kListCountStride] = 0u;
     const int r = t >> 3;          // row in tile
     const int c4 = (t & 7) * 4;    // first column in tile
     const int yy = ty * 32 + r;
@@ -1903,6 +1905,44 @@ __device__ __forceinline__ void integrate_list(const IntegrateArgs& a, const Uni
     v.i += nwaves;
 }
 
+// The dynamic tail of the last list: groups first .. first + ntail - 1, cut into one slice per
+// XCD, handed out one at a time through the XCD's own counter (zeroed by the frame's prepass),
+// each group integrated without the software pipeline (its latency is hidden across the waves
+// instead).  The static round-robin shares end unevenly (per CU by up to ~15 % of the kernel:
+// profiles/r05/wave_trace_*.txt); waves that finish theirs early take the tail, so the waves end
+// together.  The counter of XCD x is only touched by waves running on XCD x (the XCC_ID register),
+// so its atomics are workgroup-scope: performed in that XCD's L2 (agent-scope atomics go to memory
+// and serialise at ~20 ns each, 2x slower kernels).  Ticket in lane 0 (the compiler waits for all
+// of the wave's memory operations before using it: nothing else is in flight here).
+#ifndef SEMTSDF_TAIL_PCT
+#define SEMTSDF_TAIL_PCT 0  // percent of the last list's groups handed out dynamically (measured slower at 10-35 %: 0)
+#endif
+template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT, bool SHARD, bool PIN>
+__device__ __forceinline__ void integrate_tail(const IntegrateArgs& a, const UnitGrid& ug, unsigned seg_cap,
+                                               const float* __restrict__ s_rcp, const ListView& v, unsigned first,
+                                               unsigned ntail, unsigned* counters, Pipe& S, Counts& n) {
+    const int lane = threadIdx.x & 63;
+    const unsigned coff = (unsigned)lane_zq(lane) * 32u + (unsigned)lane_y(lane) * 4u;
+    // HW_REG_XCC_ID (hwreg 20), bits 3:0: the XCD this wave runs on
+    const unsigned xcc = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11))) & 7u;
+    const unsigned lo = first + ntail * xcc / 8u, hi = first + ntail * (xcc + 1u) / 8u;
+    unsigned* counter = counters + xcc * kListCountStride;
+    for (;;) {
+        unsigned t = 0u;
+        if (lane == 0) t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        t = (unsigned)__builtin_amdgcn_readfirstlane((int)t);
+        if (t >= hi - lo) break;
+        unsigned e[kSlots];
+        group_entries(v, lo + t, seg_cap, e);
+        S.cur = lane_pos(ug, e);
+        stage_project<SHARD, PIN, false, false, VOTE>(a, S.cur, lane, S.P);
+        stage_classify<SEM, GATE, VOTE, COUNT, false>(a, S.P, S.C, true, n.touch, n.gate, n.lines, S.lutv);
+        stage_load<SEM, CI32, VOTE, false>(a, S.cur, coff, S.C, S.L);
+        stage_compute<SEM, GATE, CI32, VOTE, false>(a, s_rcp, S.C, S.L, S.O);
+        stage_store<SEM, CI32, VOTE, false, COUNT>(a, S.cur, coff, store_meta(S.C), S.O, n.lazy);
+    }
+}
+
 // Persistent wavefronts over the three live-unit lists of the frame: the full free units, the
 // free units (both sdf/weight only, when the mode allows them), then the general units, the
 // pipeline chained from each list into the next.  A static round-robin share: dynamic
@@ -1919,8 +1959,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
     // the wave's group counts per list
     unsigned long long tr[5] = {0, 0, 0, 0, 0};
     unsigned long long trn = 0;
-    const unsigned wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     const unsigned nwaves = gridDim.x * (blockDim.x >> 6);
+#ifndef SEMTSDF_WAVE_PERM
+#define SEMTSDF_WAVE_PERM 0
+#endif
+    // the wave's slot in the round-robin of the lists; SEMTSDF_WAVE_PERM=1: the 4 waves of a
+    // workgroup take slots nwaves/4 apart, so consecutive (adjacent) groups go to different CUs
+    const unsigned wave = __builtin_amdgcn_readfirstlane(
+        SEMTSDF_WAVE_PERM ? (threadIdx.x >> 6) * gridDim.x + blockIdx.x : blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     auto groups_of = [&](unsigned n, unsigned rot_) -> unsigned long long {
         const unsigned ng = (n + kSlots - 1) / kSlots, i0 = (wave + nwaves - rot_ % nwaves) % nwaves;
         return i0 < ng ? (ng - 1u - i0) / nwaves + 1u : 0u;
@@ -1936,6 +1982,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
     S.groups = dispatch_round() * SEMTSDF_PRIO_EVERY;
     if (SEM && a.lut) S.lutv = reinterpret_cast<const uint32_t*>(a.lut)[lane];
     const unsigned* cnt = a.list_count;
+    unsigned* tail_counter = a.list_count + kLists * kListSegs * kListCountStride;  // zeroed by the prepass
     const unsigned* lst = a.unit_list;
     const size_t lstride = (size_t)kListSegs * seg_cap;
     constexpr int kCnt = kListSegs * kListCountStride;
@@ -1946,6 +1993,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
         ListView v1 = list_view(lst + lstride, cnt + kCnt, wave, nwaves, vf.ngroups % nwaves);
         rot0 = (vf.ngroups + v1.ngroups) % nwaves;
         ListView v0 = list_view(lst, cnt, wave, nwaves, rot0);
+        const unsigned tail0 = SEMTSDF_TAIL_PCT ? v0.ngroups * SEMTSDF_TAIL_PCT / 100u : 0u;
+        v0.ngroups -= tail0;  // the static share: groups 0 .. ngroups - tail0 - 1
         if (vf.i < vf.ngroups)
             list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 2>(a, ug, seg_cap, vf, S, n);
         else if (v1.i < v1.ngroups)
@@ -1962,6 +2011,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
             trn = groups_of(vf.total, 0u) | (groups_of(v1.total, vf.ngroups % nwaves) << 20);
         }
         integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0, -1>(a, ug, seg_cap, s_rcp, v0, nullptr, nwaves, S, n);
+        if (tail0) integrate_tail<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>(a, ug, seg_cap, s_rcp, v0, v0.ngroups, tail0,
+                                                                           tail_counter, S, n);
         n0 = v0.total;
         if (COUNT && blockIdx.x == 0 && threadIdx.x == 0) {
             atomicAdd(a.counters + 4, (unsigned long long)(v1.total + vf.total));
@@ -1970,11 +2021,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
         if (COUNT) nlive += v1.total + vf.total;
     } else {
         ListView v0 = list_view(lst, cnt, wave, nwaves, 0u);
+        const unsigned tail0 = SEMTSDF_TAIL_PCT ? v0.ngroups * SEMTSDF_TAIL_PCT / 100u : 0u;
+        v0.ngroups -= tail0;
         if (v0.i < v0.ngroups)
             list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0>(a, ug, seg_cap, v0, S, n);
         __syncthreads();
         if (SEMTSDF_WAVE_TRACE) tr[1] = tr[2] = tr[3] = wall_clock64();
         integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0, -1>(a, ug, seg_cap, s_rcp, v0, nullptr, nwaves, S, n);
+        if (tail0) integrate_tail<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>(a, ug, seg_cap, s_rcp, v0, v0.ngroups, tail0,
+                                                                           tail_counter, S, n);
         n0 = v0.total;
     }
     if (SEM && a.lut && a.relabel_mask) {  // the frame's mask through the same table, in place
