@@ -1598,6 +1598,20 @@ __device__ __forceinline__ void stage_compute(const IntegrateArgs& a, const floa
     }
 }
 
+// Read-modify-writes of a voxel's own words (its histogram bins and bin mask) as no-return atomics
+// at workgroup scope: within a launch one lane owns the voxel (units are disjoint), so no other
+// lane -- on this XCD or another -- touches the word, and the kernel boundary's L2 write-back makes
+// the result visible as for a store.  A device-scope atomic would be performed at memory (the
+// XCDs' L2s are not coherent), hundreds of cycles longer in vmcnt, which the software pipeline's
+// ordered waits then sit behind.  (Words shared by lanes, e.g. the bricks' dirty bits, keep device
+// scope.)
+__device__ __forceinline__ void voxel_or(uint32_t* p, uint32_t v) {
+    (void)__hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void voxel_add(uint32_t* p, uint32_t v) {
+    (void)__hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 template <bool SEM, bool CI32, bool VOTE, bool FREE, bool COUNT>
 __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPos& up, unsigned coff,
                                             const StoreMeta& M, const Out& O, unsigned& n_lazy) {
@@ -1669,7 +1683,7 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
                 if (nb) {
 #pragma unroll
                     for (int k = 0; k < 4; ++k)
-                        if ((nb >> k) & 1u) atomicOr(a.b.hmask + v + k, 1u << hlab);
+                        if ((nb >> k) & 1u) voxel_or(a.b.hmask + v + k, 1u << hlab);
                 }
             }
             if (hmode == 2u) {  // rare: labels differ inside the lane, or a label >= 32
@@ -1679,8 +1693,8 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
                     const unsigned lab = (M.labs >> (8 * k)) & 0xFFu;
                     const bool gk = (gmask >> k) & 1u;
                     if (gk && lab < (unsigned)kMaxObjects) {
-                        atomicAdd(a.b.hist + (uint64_t)lab * g.nvox + v + k, 1u);
-                        atomicOr(a.b.hmask + v + k, 1u << lab);
+                        voxel_add(a.b.hist + (uint64_t)lab * g.nvox + v + k, 1u);
+                        voxel_or(a.b.hmask + v + k, 1u << lab);
                     }
                     bad += (gk && lab >= (unsigned)kMaxObjects) ? 1u : 0u;
                 }
