@@ -259,7 +259,11 @@ int local_planes(const semtsdf_params* p, int* chunk, int* halo) {
     // round may lack this shard's position
     const int n = p->z_nshards;
     for (int r = 0; r * n < nchunks; ++r)
+#ifdef SEMTSDF_DEAL_RR
+        if (r * n + p->z_shard < nchunks) ++mine;
+#else
         if (r * n + ((r & 1) ? n - 1 - p->z_shard : p->z_shard) < nchunks) ++mine;
+#endif
     return mine * (p->z_chunk + 1);
 }
 

@@ -97,7 +97,12 @@ __device__ __forceinline__ float vox_coord(float p, float start, float voxel, fl
 // a work density that drifts along z evens out over pairs of rounds.  Local chunk r of a
 // shard is its chunk of round r (only the last round may lack it).
 __host__ __device__ __forceinline__ int chunk_pos(int round, int shard, int n) {
+#ifdef SEMTSDF_DEAL_RR
+    (void)round; (void)n;
+    return shard;
+#else
     return (round & 1) ? n - 1 - shard : shard;
+#endif
 }
 __host__ __device__ __forceinline__ int chunk_owner(int c, int n) {
     const int r = c / n;
