@@ -1035,8 +1035,8 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
         if ((rc = dev_alloc(v, (void**)&pyr.l0, (size_t)pyr.w1 * 4 * pyr.h1 * 4 * sizeof(uint2)))) return bail(rc);
         if ((rc = dev_alloc(v, (void**)&pyr.l1, (size_t)pyr.w1 * pyr.h1 * sizeof(uint2)))) return bail(rc);
         if ((rc = dev_alloc(v, (void**)&f.unit_list, unit_list_capacity(g) * sizeof(unsigned)))) return bail(rc);
-        // + the integrate's dynamic tail counters (one per XCD), kListCountStride words apart
-        if ((rc = dev_alloc(v, (void**)&f.list_count, (kLists * kListSegs + 8) * kListCountStride * sizeof(unsigned))))
+        // + the integrate's dynamic counters (per XCD and workgroup slot), kListCountStride words apart
+        if ((rc = dev_alloc(v, (void**)&f.list_count, (kLists * kListSegs + kDynCounters) * kListCountStride * sizeof(unsigned))))
             return bail(rc);
     }
     if ((rc = dev_alloc(v, (void**)&v->rcp_table_d, kRcpTable * sizeof(float)))) return bail(rc);

@@ -17,6 +17,11 @@ constexpr int kZAlign = 32;      // stored z planes per x,y column: a multiple o
 constexpr int kBrickDistCap = SEMTSDF_BRICK_DIST_CAP;  // brick distance map: radius of the largest skip box (bricks)
 constexpr int kListSegs = 64;    // segments (and counters) of the live-unit list
 constexpr int kListCountStride = 64;  // counters 256 B apart (separate memory channels)
+#ifndef SEMTSDF_DYN_SUB
+#define SEMTSDF_DYN_SUB 8
+#endif
+constexpr unsigned kDynSub = SEMTSDF_DYN_SUB;           // integrate dynamic counters per XCD (power of two)
+constexpr int kDynCounters = 8 * SEMTSDF_DYN_SUB;       // after the list counts (zeroed by the prepass)
 constexpr int kLists = 3;             // live-unit lists: general, free (projected), full free (no projection)
 
 // Geometry of the locally stored part of the volume.

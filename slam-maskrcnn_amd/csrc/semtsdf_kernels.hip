@@ -595,7 +595,7 @@ __device__ __forceinline__ void pyramid_tile(const uint16_t* __restrict__ depth,
     auto relab = [&](unsigned m) { return (s_lut[m >> 2] >> (8 * (m & 3))) & 0xFFu; };
     if (list_count && tx == 0 && ty == 0 && t < kLists * kListSegs)  // this frame's lists (general, free, full)
         list_count[(t & (kListSegs - 1)) * kListCountStride + (t >> 6) * kListSegs * kListCountStride] = 0u;
-    if (list_count && tx == 0 && ty == 0 && t < 8)  // the integrate's dynamic tail counters, one per XCD
+    if (list_count && tx == 0 && ty == 0 && t < kDynCounters)  // the integrate's dynamic counters
         list_count[(kLists * kListSegs + t) * kListCountStride] = 0u;
     const int r = t >> 3;          // row in tile
     const int c4 = (t & 7) * 4;    // first column in tile
@@ -1924,6 +1924,72 @@ __device__ __forceinline__ void integrate_list(const IntegrateArgs& a, const Uni
     v.i += nwaves;
 }
 
+// The last list (general units) with its groups past the first round handed out at run time,
+// software-pipelined like integrate_list.  The wave's first group is its static one (v.i <
+// nwaves, primed by the chain from the list before); groups nwaves .. ngroups - 1 are cut into
+// one slice per XCD and handed out through the XCD's own counter (zeroed by the frame's prepass),
+// so waves that finished their earlier lists early take more of them and the waves end together.
+// The counter of XCD x is only touched by waves running on XCD x (the XCC_ID register), so its
+// atomics are workgroup-scope: performed in that XCD's L2.  Every lane of the wave executes the
+// atomic (lane 0 adds 1, the others 0: no divergent branch, so the compiler counts the atomic
+// among the wave's vector-memory operations in order), and the ticket of the group after next
+// is claimed at the end of an iteration and read after the next compute stage, which waits for
+// the state loads issued before it anyway: the claim's round trip hides under the pipeline.
+#ifndef SEMTSDF_DYN_LAST
+#define SEMTSDF_DYN_LAST 0
+#endif
+template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT, bool SHARD, bool PIN>
+__device__ __forceinline__ void integrate_list_dyn(const IntegrateArgs& a, const UnitGrid& ug, unsigned seg_cap,
+                                                   const float* __restrict__ s_rcp, ListView& v, unsigned nwaves,
+                                                   unsigned* xcd_counters, Pipe& S, Counts& n) {
+    const int lane = threadIdx.x & 63;
+    const unsigned coff = (unsigned)lane_zq(lane) * 32u + (unsigned)lane_y(lane) * 4u;
+    if (v.i >= v.ngroups) return;  // then ngroups <= nwaves: no dynamic group either
+    if (!S.primed) list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0>(a, ug, seg_cap, v, S, n);
+    // HW_REG_XCC_ID (hwreg 20), bits 3:0: the XCD this wave runs on
+    const unsigned xcc = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11))) & 7u;
+    // one slice per (XCD, workgroup slot): a single counter per XCD saturates (same-address L2
+    // atomics serialise), so the waves of an XCD share kDynSub counters
+    const unsigned sub = (blockIdx.x >> 3) & (kDynSub - 1u), sl = xcc * kDynSub + sub, ns = 8u * kDynSub;
+    const unsigned D = v.ngroups - min(v.ngroups, nwaves);
+    const unsigned lo = nwaves + D * sl / ns, cnt = nwaves + D * (sl + 1u) / ns - lo;
+    unsigned* ctr = xcd_counters + sl * kListCountStride;
+    auto claim = [&]() -> unsigned {
+        unsigned r = 0u;
+        if (lane == 0) r = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return r;
+    };
+    unsigned en[kSlots];
+    unsigned t = cnt ? (unsigned)__builtin_amdgcn_readlane((int)claim(), 0) : 0u;
+    bool have = t < cnt;
+    if (have) group_entries(v, lo + t, seg_cap, en);
+    // claimed unconditionally (a claim past the slice only moves its counter further): a
+    // conditional one merges with the loop's previous value, and that copy waits for the atomic
+    unsigned pend = claim();
+    while (have) {
+        const UnitPos nxt = lane_pos(ug, en);
+        stage_project<SHARD, PIN, false, false, VOTE>(a, nxt, lane, S.P);
+        stage_compute<SEM, GATE, CI32, VOTE, false>(a, s_rcp, S.C, S.L, S.O);
+        const unsigned t2 = (unsigned)__builtin_amdgcn_readlane((int)pend, 0);
+        const bool have2 = t2 < cnt;
+        if (have2) group_entries(v, lo + t2, seg_cap, en);
+        const StoreMeta Mc = store_meta(S.C);
+        stage_classify<SEM, GATE, VOTE, COUNT, false>(a, S.P, S.C, true, n.touch, n.gate, n.lines, S.lutv);
+        stage_store<SEM, CI32, VOTE, false, COUNT>(a, S.cur, coff, Mc, S.O, n.lazy);
+        stage_load<SEM, CI32, VOTE, false>(a, nxt, coff, S.C, S.L);
+        pend = claim();
+        S.cur = nxt;
+        have = have2;
+        ++S.groups;
+        if (SEMTSDF_PRIO_EVERY == 1 || (S.groups & (SEMTSDF_PRIO_EVERY - 1u)) == 0u)
+            rotate_prio(S.groups / SEMTSDF_PRIO_EVERY);
+    }
+    stage_compute<SEM, GATE, CI32, VOTE, false>(a, s_rcp, S.C, S.L, S.O);
+    stage_store<SEM, CI32, VOTE, false, COUNT>(a, S.cur, coff, store_meta(S.C), S.O, n.lazy);
+    S.primed = false;
+    v.i = v.ngroups;
+}
+
 // The dynamic tail of the last list: groups first .. first + ntail - 1, cut into one slice per
 // XCD, handed out one at a time through the XCD's own counter (zeroed by the frame's prepass),
 // each group integrated without the software pipeline (its latency is hidden across the waves
@@ -2029,7 +2095,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
             tr[3] = wall_clock64();
             trn = groups_of(vf.total, 0u) | (groups_of(v1.total, vf.ngroups % nwaves) << 20);
         }
-        integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0, -1>(a, ug, seg_cap, s_rcp, v0, nullptr, nwaves, S, n);
+        if (SEMTSDF_DYN_LAST)
+            integrate_list_dyn<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>(a, ug, seg_cap, s_rcp, v0, nwaves, tail_counter, S, n);
+        else
+            integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0, -1>(a, ug, seg_cap, s_rcp, v0, nullptr, nwaves, S, n);
         if (tail0) integrate_tail<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>(a, ug, seg_cap, s_rcp, v0, v0.ngroups, tail0,
                                                                            tail_counter, S, n);
         n0 = v0.total;
@@ -2046,7 +2115,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
             list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0>(a, ug, seg_cap, v0, S, n);
         __syncthreads();
         if (SEMTSDF_WAVE_TRACE) tr[1] = tr[2] = tr[3] = wall_clock64();
-        integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0, -1>(a, ug, seg_cap, s_rcp, v0, nullptr, nwaves, S, n);
+        if (SEMTSDF_DYN_LAST)
+            integrate_list_dyn<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>(a, ug, seg_cap, s_rcp, v0, nwaves, tail_counter, S, n);
+        else
+            integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0, -1>(a, ug, seg_cap, s_rcp, v0, nullptr, nwaves, S, n);
         if (tail0) integrate_tail<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>(a, ug, seg_cap, s_rcp, v0, v0.ngroups, tail0,
                                                                            tail_counter, S, n);
         n0 = v0.total;

@@ -1,9 +1,6 @@
 set -u
-T=${1:-r05_s16}
+T=${1:-r05_dyn4}
 O=gpurun_out/$T
 mkdir -p $O
-for CH in 15 31; do
-for r in 0 1 2 3 4 5 6 7; do
-SEMTSDF_LIB=build/var_rr.so BENCH_EMULATE_WORLD=8 BENCH_EMULATE_RANK=$r timeout -k 10 120 python3 bench.py --no-pipeline --no-cpu-baseline --steps 20 --c4-chunk $CH > $O/c${CH}_r$r.json 2>/dev/null || exit 1
-python3 -c "import json; d=json.load(open('$O/c${CH}_r$r.json')); print('rr chunk $CH rank $r ms', d['ms_per_step'], 'kernel', d['integrate_kernel_ms'], 'live', d['live_units_per_frame'], 'free', d['free_units_per_frame'], 'touched', d['touched_per_frame'], 'gated', d['gated_per_frame'])" >> $O/summary.txt
-done; done
+AB_ARGS=--no-c4 bash tools/ab_integrate.sh build/var_noopt.so build/var_dyn_s8.so build/var_dyn_s32.so build/var_noopt.so build/var_dyn_s8.so build/var_dyn_s32.so > $O/ab.txt 2>&1 || { cat $O/ab.txt; exit 1; }
+cat $O/ab.txt
