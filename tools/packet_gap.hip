@@ -44,12 +44,31 @@ int main() {
                            "+ prep kernel waited for, prep after launch i-2 (bench step)",
                            "+ prep kernel waited for, prep waits nothing", "as the bench step, two prep kernels",
                            "as the bench step, prep after launch i-3", "prep after launch i-2, not waited for",
-                           "host-ordered sets: record every 4th, host waits for launch i-8"};
-    for (int mode = 0; mode < 8; ++mode) {
+                           "host-ordered sets: record every 4th, host waits for launch i-8",
+                           "as the bench step, stream wait/write-value (signal memory) in place of events"};
+    uint32_t *flag_s = nullptr, *flag_p = nullptr;
+    CK(hipExtMallocWithFlags((void**)&flag_s, 8, hipMallocSignalMemory));
+    CK(hipExtMallocWithFlags((void**)&flag_p, 8, hipMallocSignalMemory));
+    for (int mode = 0; mode < 9; ++mode) {
+        if (mode == 8) {
+            CK(hipMemset(flag_s, 0, 4));
+            CK(hipMemset(flag_p, 0, 4));
+            CK(hipDeviceSynchronize());
+        }
         for (int rep = 0; rep < 2; ++rep) {
             CK(hipDeviceSynchronize());
             CK(hipEventRecord(t0, s));
             for (int i = 0; i < N; ++i) {
+                if (mode == 8) {  // values are 1-based launch counts; the prep waits for launch i-2
+                    const unsigned base = rep * N;
+                    if (i >= 2) CK(hipStreamWaitValue32(ps, flag_s, base + (unsigned)(i - 1), hipStreamWaitValueGte, 0xFFFFFFFFu));
+                    hipLaunchKernelGGL(spin, dim3(cus / 4), dim3(256), 0, ps, ts, sink);
+                    CK(hipStreamWriteValue32(ps, flag_p, base + (unsigned)i + 1u, 0));
+                    CK(hipStreamWaitValue32(s, flag_p, base + (unsigned)i + 1u, hipStreamWaitValueGte, 0xFFFFFFFFu));
+                    hipLaunchKernelGGL(spin, dim3(cus * 4), dim3(256), 0, s, tb, sink);
+                    CK(hipStreamWriteValue32(s, flag_s, base + (unsigned)i + 1u, 0));
+                    continue;
+                }
                 if (mode >= 2) {
                     const int lag = mode == 5 ? 3 : 2;
                     if (mode == 7) {
