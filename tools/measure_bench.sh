@@ -1,8 +1,8 @@
 #!/bin/bash
-# r04 final measurement, part B: the bench line reading part A's traffic records, rocprofv3
+# Final measurement, part B: the bench line reading part A's traffic records, rocprofv3
 # kernel stats of the C3 bench, march counters
 set -u
-TAG=${1:-r04_final}
+TAG=${1:-final}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$TAG
 mkdir -p $O

@@ -1,18 +1,18 @@
 #!/bin/bash
-# r04 final measurement in one call: PMC traffic + counters of C3 and C2 (stamped with the build
+# Final measurement of a round in one call: PMC traffic + counters of C3 and C2 (stamped with the build
 # key), the traffic records copied where bench.py reads them, the bench line, rocprofv3 kernel
 # stats of the C3 bench, a kernel trace of the fused pipeline and of one C4 emulated rank.
 set -u
-TAG=${1:-r04_final}
+TAG=${1:-final}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 step() { echo "[measure] $1 rc=$2" | tee -a $O/steps.log; if [ $2 -ne 0 ]; then exit $2; fi; }
-bash $R/tools/measure_r04a.sh $TAG
+bash $R/tools/measure_pmc.sh $TAG
 step partA $?
 cp $O/traffic.json $R/profiles/traffic_latest.json && cp $O/c2/traffic.json $R/profiles/traffic_c2_latest.json
 step copy_traffic $?
-bash $R/tools/measure_r04b.sh $TAG
+bash $R/tools/measure_bench.sh $TAG
 step partB $?
 bash $R/tools/trace_pipeline.sh $TAG/trace_pipe > /dev/null 2>&1
 step trace_pipe $?

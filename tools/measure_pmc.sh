@@ -1,7 +1,7 @@
 #!/bin/bash
-# r04 final measurement, part A: PMC traffic + counters of C3 and C2 (stamped with the build key)
+# Final measurement, part A: PMC traffic + counters of C3 and C2 (stamped with the build key)
 set -u
-TAG=${1:-r04_final}
+TAG=${1:-final}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
