@@ -1633,7 +1633,13 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
         // a brick of the empty-space map changes only where a voxel crossed the threshold:
         // z-brick j of the unit holds the lanes of z-quads 2j, 2j+1 (lane = zq + 8 y)
         const uint64_t cb = __ballot(O.cross);
-        const IntegrateRare* R = a.rare;
+        // the struct through the constant address space (scalar loads, lgkmcnt) and its buffers as
+        // global pointers: a pointer loaded from memory is generic, and the FLAT atomics and store
+        // it would take count in vmcnt as another kind of event, after which the compiler waits
+        // for every vector-memory operation at the top of the next group (vmcnt(0) in place of
+        // vmcnt(5): the project stage's gathers no longer overlap the compute stage)
+        const __attribute__((address_space(4))) IntegrateRare* R =
+            (const __attribute__((address_space(4))) IntegrateRare*)a.rare;
         if (cb && R->bdirty) {  // rare: most updates keep their side of the threshold
             // lane j of a slot marks z-brick j of its unit (z-quads 2j, 2j+1)
             const int lane = (int)__lane_id(), j = lane % kUnitLanes;
@@ -1645,7 +1651,10 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
                 const unsigned nbq = (unsigned)(R->nbz + 3) >> 2;
                 const unsigned q = __umul24(__umul24((unsigned)(up.x * UX >> 3), (unsigned)R->nby) +
                                                 (unsigned)(up.uy * UY >> 3), nbq) + ((unsigned)bz >> 2);
-                if (atomicOr(&R->bdirty[q], 1u << (bz & 3)) == 0u) R->dlist[1 + atomicAdd(&R->dlist[0], 1u)] = q;
+                __attribute__((address_space(1))) uint32_t* bd = (__attribute__((address_space(1))) uint32_t*)R->bdirty;
+                __attribute__((address_space(1))) uint32_t* dl = (__attribute__((address_space(1))) uint32_t*)R->dlist;
+                if (__hip_atomic_fetch_or(bd + q, 1u << (bz & 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+                    dl[1 + __hip_atomic_fetch_add(dl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)] = q;
             }
         }
     }
@@ -1705,7 +1714,12 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
                 }
                 // an id without a histogram bin (tsdf.cu:61 writes past the voxel's 32 bins): the
                 // vote is dropped and counted
-                if (bad) atomicAdd(a.rare->counters + 2, (unsigned long long)bad);
+                if (bad) {
+                    const __attribute__((address_space(4))) IntegrateRare* R4 =
+                        (const __attribute__((address_space(4))) IntegrateRare*)a.rare;
+                    __hip_atomic_fetch_add((__attribute__((address_space(1))) unsigned long long*)R4->counters + 2,
+                                           (unsigned long long)bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
         }
     }
