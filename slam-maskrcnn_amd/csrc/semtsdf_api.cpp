@@ -67,6 +67,10 @@ const uint8_t kPalette[kMaxObjects * 3] = {
     128, 0,   0,   170, 255, 195};
 
 constexpr int kCounters = 8;  // device counters of a volume (IntegrateArgs::counters)
+#ifndef SEMTSDF_FRAME_SETS
+#define SEMTSDF_FRAME_SETS 2
+#endif
+constexpr int kFrameSets = SEMTSDF_FRAME_SETS;  // per-frame prepass output sets used in turn
 
 struct EventPair {
     hipEvent_t a, b;
@@ -93,11 +97,12 @@ struct semtsdf_vol {
         DepthPyramid pyr{};
         unsigned* unit_list = nullptr;   // live units of the frame (cull pass)
         unsigned* list_count = nullptr;  // [kLists][kListSegs * kListCountStride] (general, free, full free)
+        unsigned* units = nullptr;       // the lists compacted back to back (k_compact_lists)
         hipEvent_t prep_done = nullptr;  // the set's prepass finished (prep_stream)
         hipEvent_t set_free = nullptr;   // the integrate reading the set finished (recorded once async is in use)
         bool free_recorded = false;
         hipStream_t reader = nullptr;    // stream of the last integrate that read the set
-    } fs[2];
+    } fs[kFrameSets];
     int next_set = 0;
     hipStream_t prep_stream = nullptr;   // created on the first asynchronous integrate
     hipEvent_t in_ev = nullptr;          // parse_frame: the caller's work before the frame (inputs ready)
@@ -182,13 +187,15 @@ int dev_alloc(semtsdf_vol* v, void** p, size_t bytes) {
 
 void free_all(semtsdf_vol* v) {
     void* ptrs[] = {v->b.sdf, v->b.wt, v->b.bmin, v->b.bplain, v->b.sbmin, v->b.bdist, v->b.boct, v->b.botmp, v->b.bdirty, v->b.dlist, v->b.sflag, v->b.color, v->b.hist, v->b.hmask, v->b.cls, v->b.cls_cnt, v->depth_d, v->rgb_d,
-                    v->mask_d, v->cls_d, v->fs[0].pyr.px, v->fs[0].pyr.l0, v->fs[0].pyr.l1, v->fs[1].pyr.px,
-                    v->fs[1].pyr.l0, v->fs[1].pyr.l1, v->tables_d, v->decision_d,
+                    v->mask_d, v->cls_d, v->tables_d, v->decision_d,
                     v->num_objs_d, v->probs_d, v->box_d, v->palette_d, v->render_d, v->render_t_d,
-                    v->counters_d, v->ray_state_d, v->fs[0].unit_list, v->fs[0].list_count, v->fs[1].unit_list,
-                    v->fs[1].list_count, v->rcp_table_d, v->wtrace_d, v->exact_d, v->px.bits, v->px.p, v->tile_cost_d, v->tile_perm_d, v->rare_d};
+                    v->counters_d, v->ray_state_d, v->rcp_table_d, v->wtrace_d, v->exact_d, v->px.bits, v->px.p, v->tile_cost_d, v->tile_perm_d, v->rare_d};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
+    for (auto& f : v->fs)
+        for (void* q : {(void*)f.pyr.px, (void*)f.pyr.l0, (void*)f.pyr.l1, (void*)f.unit_list, (void*)f.list_count,
+                        (void*)f.units})
+            if (q) (void)hipFree(q);
     if (v->decision_h) (void)hipHostFree(v->decision_h);
     for (auto* vec : {&v->ev_integrate, &v->ev_assoc, &v->ev_render, &v->ev_prep})
         for (auto& e : *vec) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
@@ -404,6 +411,7 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
     a.rare = v->rare_d;
     a.unit_list = F.unit_list;
     a.list_count = F.list_count;
+    a.units = F.units;
     a.rcp_table = v->rcp_table_d;
     screen_map(a);
     a.pinhole = (a.K[1] == 0.0f && a.K[3] == 0.0f && a.K[6] == 0.0f && a.K[7] == 0.0f && a.K[8] == 1.0f) ? 1 : 0;
@@ -444,7 +452,7 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
             HIPC(hipStreamWaitEvent(ps, F.set_free, 0));
         }
     }
-    v->next_set ^= 1;
+    v->next_set = (v->next_set + 1) % kFrameSets;
     EventPair epp;
     timing_begin(v, v->ev_prep, ps, &epp);
     if (!pre_done)
@@ -452,6 +460,7 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
                                   v->p.depth_scale, F.pyr, F.list_count, ps, relabel_after ? nullptr : lut));
     if (lut && !relabel_after) v->pending_lut = nullptr;  // consumed by the prepass
     HIPC(launch_cull(a, ps));
+    HIPC(launch_compact_lists(a, ps));
     timing_end(v, v->ev_prep, ps, &epp);
     v->n_prep++;
     if (async) {
@@ -1036,8 +1045,9 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
         if ((rc = dev_alloc(v, (void**)&pyr.l1, (size_t)pyr.w1 * pyr.h1 * sizeof(uint2)))) return bail(rc);
         if ((rc = dev_alloc(v, (void**)&f.unit_list, unit_list_capacity(g) * sizeof(unsigned)))) return bail(rc);
         // + the integrate's dynamic counters (per XCD and workgroup slot), kListCountStride words apart
-        if ((rc = dev_alloc(v, (void**)&f.list_count, (kLists * kListSegs + kDynCounters) * kListCountStride * sizeof(unsigned))))
-            return bail(rc);
+        if ((rc = dev_alloc(v, (void**)&f.list_count, kListCountWords * sizeof(unsigned)))) return bail(rc);
+        // every unit in at most one list, + one pad per list, bases rounded up to even
+        if ((rc = dev_alloc(v, (void**)&f.units, (unit_count(g) + 2 * kLists + 2) * sizeof(unsigned)))) return bail(rc);
     }
     if ((rc = dev_alloc(v, (void**)&v->rcp_table_d, kRcpTable * sizeof(float)))) return bail(rc);
     {

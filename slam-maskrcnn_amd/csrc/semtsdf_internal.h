@@ -22,6 +22,9 @@ constexpr int kListCountStride = 64;  // counters 256 B apart (separate memory c
 #endif
 constexpr unsigned kDynSub = SEMTSDF_DYN_SUB;           // integrate dynamic counters per XCD (power of two)
 constexpr int kDynCounters = 8 * SEMTSDF_DYN_SUB;       // after the list counts (zeroed by the prepass)
+// words of list_count: the segment counts, the dynamic counters, then the compact lists' (base, total)
+constexpr int kListTotalsWord = (3 * kListSegs + kDynCounters) * kListCountStride;
+constexpr int kListCountWords = kListTotalsWord + 8;
 constexpr int kLists = 3;             // live-unit lists: general, free (projected), full free (no projection)
 
 // Geometry of the locally stored part of the volume.
@@ -148,7 +151,9 @@ struct IntegrateArgs {
     float rmu;                     // RN(1/mu), for the exact division by mu (k_integrate)
     int fastdiv;                   // mu in [2^-20, 2^20]: divisions by mu/(w+1) via RN reciprocals
     unsigned* unit_list;           // live units: three lists (general, free, full free) of kListSegs segments (k_cull_units)
-    unsigned* list_count;          // [3][kListSegs * kListCountStride] entries per segment, then the dynamic tail
+    unsigned* list_count;          // [3][kListSegs * kListCountStride] entries per segment, then the dynamic
+                                   // counters, then the compact lists' (base, total) pairs (k_compact_lists)
+    unsigned* units;               // the three lists back to back (k_compact_lists), each followed by a ~0u pad
                                    // counters of the 8 XCDs (all zeroed by the frame prepass)
     int free_ok;                   // free units allowed: gated colour with gate <= 1 (f == 1 updates sdf/weight only)
     int color_wide;                // colour stored as int32 x 4 (else u8 x 4; see semtsdf_vol::color_wide)
@@ -341,6 +346,7 @@ uint64_t unit_count(const VolGeom& g);
 uint64_t unit_list_capacity(const VolGeom& g);
 int unit_grid_fits(int dimx, int dimy, int local_z);  // list entries (pack_unit) hold the unit grid
 hipError_t launch_cull(const IntegrateArgs& a, hipStream_t s);       // per-unit cull flags
+hipError_t launch_compact_lists(const IntegrateArgs& a, hipStream_t s);  // segments -> a.units
 hipError_t launch_tables_init(AssocTables* t, hipStream_t s);  // zero sums, first_px = UINT_MAX
 hipError_t launch_mask_stats(const uint8_t* mask, int npx, AssocTables* t, hipStream_t s);
 hipError_t launch_assoc_march(const AssocArgs& a, hipStream_t s);

@@ -986,6 +986,79 @@ hipError_t launch_cull(const IntegrateArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// The cull's segments compacted into one array: list l at an even base (so a group's two entries are
+// one 8-byte scalar load), followed by a ~0u pad (the second entry of a list's last group when
+// its count is odd), bases and totals after the dynamic counters of list_count.  One wave per
+// (segment, list): lane j holds the count of segment j of every list; the wave's segment offset
+// is the exclusive prefix of its list's counts.  Runs on the prep stream after the cull, so the
+// integrate reads its first group's entries without the counts' prefix (one dependent load less
+// at its start) and decodes no segment per entry.
+__global__ __launch_bounds__(256) void k_compact_lists(const unsigned* __restrict__ list_count,
+                                                       const unsigned* __restrict__ seg_list, unsigned seg_cap,
+                                                       unsigned* __restrict__ units) {
+    // every wave of the workgroup computes the (tiny) prefix itself; all 256 lanes copy
+    const unsigned lane = threadIdx.x & 63u, seg = blockIdx.x, l = blockIdx.y;
+    unsigned c[kLists], tot[kLists];
+#pragma unroll
+    for (int k = 0; k < kLists; ++k) {
+        c[k] = list_count[((unsigned)k * kListSegs + lane) * kListCountStride];
+        tot[k] = c[k];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) tot[k] += (unsigned)__shfl_xor((int)tot[k], off, 64);
+    }
+    unsigned base[kLists];
+    base[0] = 0u;
+#pragma unroll
+    for (int k = 1; k < kLists; ++k) base[k] = (base[k - 1] + tot[k - 1] + 2u) & ~1u;
+    // this list's counts, exclusive prefix over the segments
+    unsigned cl = c[0];
+#pragma unroll
+    for (int k = 1; k < kLists; ++k) cl = l == (unsigned)k ? c[k] : cl;
+    unsigned incl = cl;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const unsigned o = (unsigned)__shfl_up((int)incl, off, 64);
+        if ((int)lane >= off) incl += o;
+    }
+    const unsigned n = (unsigned)__shfl((int)cl, (int)seg, 64), off0 = (unsigned)__shfl((int)(incl - cl), (int)seg, 64);
+    unsigned bl = base[0];
+#pragma unroll
+    for (int k = 1; k < kLists; ++k) bl = l == (unsigned)k ? base[k] : bl;
+    const unsigned* src = seg_list + ((size_t)l * kListSegs + seg) * seg_cap;
+    unsigned* dst = units + bl + off0;
+    // four loads in flight per lane before their stores (the copy is latency-bound otherwise)
+    for (unsigned i0 = threadIdx.x; i0 < n; i0 += 4u * 256u) {
+        unsigned e[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) e[k] = i0 + 256u * k < n ? src[i0 + 256u * k] : 0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (i0 + 256u * k < n) dst[i0 + 256u * k] = e[k];
+    }
+    if (seg == 0u && l == 0u && threadIdx.x < (unsigned)kLists) {
+        unsigned b = base[0], t = tot[0];
+#pragma unroll
+        for (int k = 1; k < kLists; ++k) {
+            b = lane == (unsigned)k ? base[k] : b;
+            t = lane == (unsigned)k ? tot[k] : t;
+        }
+        units[b + t] = ~0u;  // the pad
+        unsigned* tw = const_cast<unsigned*>(list_count) + kListTotalsWord;
+        tw[2 * lane] = b;
+        tw[2 * lane + 1] = t;
+    }
+}
+
+hipError_t launch_compact_lists(const IntegrateArgs& a, hipStream_t s) {
+    const UnitGrid ug = unit_grid(a.g);
+    if (ug.n == 0) {  // a shard that owns no chunk: empty lists
+        return hipMemsetAsync(a.list_count + kListTotalsWord, 0, 8 * sizeof(unsigned), s);
+    }
+    hipLaunchKernelGGL(k_compact_lists, dim3(kListSegs, kLists), dim3(256), 0, s, a.list_count, a.unit_list,
+                       list_seg_cap(ug), a.units);
+    return hipGetLastError();
+}
+
 uint64_t unit_count(const VolGeom& g) { return unit_grid(g).n; }
 uint64_t unit_list_capacity(const VolGeom& g) { return (uint64_t)list_seg_cap(unit_grid(g)) * kListSegs * kLists; }
 
@@ -1732,52 +1805,35 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
 // One list of the frame as one persistent wave sees it: wave w takes the groups w', w' +
 // nwaves, ... with w' = (w - rot) mod nwaves (rot continues the round-robin of the lists
 // before it, so the waves with an extra group alternate), a group being kSlots consecutive
-// entries, one unit per slot.  The list is kListSegs segments; lane l holds the inclusive
-// prefix of the segment counts up to segment l.
+// entries, one unit per slot, of the list's compact array (k_compact_lists).
 struct ListView {
-    const unsigned* list;
-    unsigned incl;             // per lane: entries in segments 0..lane
+    const unsigned* list;      // the list's first entry
     unsigned total, ngroups;   // wave-uniform
     unsigned i;                // the wave's current group
 };
 
-__device__ __forceinline__ ListView list_view(const unsigned* list, const unsigned* list_count, unsigned wave,
+// List l of the frame (base and total written by k_compact_lists; scalar loads).
+__device__ __forceinline__ ListView list_view(const unsigned* units, const unsigned* list_count, int l, unsigned wave,
                                               unsigned nwaves, unsigned rot) {
-    static_assert(kListSegs == 64, "one list segment per lane");
-    const int lane = threadIdx.x & 63;
+    const __attribute__((address_space(4))) unsigned* tw =
+        (const __attribute__((address_space(4))) unsigned*)(list_count + kListTotalsWord);
     ListView v;
-    v.list = list;
-    v.incl = list_count[lane * kListCountStride];
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const unsigned o = (unsigned)__shfl_up((int)v.incl, off, 64);
-        if (lane >= off) v.incl += o;
-    }
-    v.total = __builtin_amdgcn_readfirstlane((unsigned)__shfl((int)v.incl, 63, 64));
+    v.list = units + tw[2 * l];
+    v.total = tw[2 * l + 1];
     v.ngroups = (v.total + kSlots - 1) / kSlots;
     v.i = (wave + nwaves - rot % nwaves) % nwaves;
     return v;
 }
 
-// Entry idx < total: its segment is the number of segments ending at or before idx.
-__device__ __forceinline__ unsigned list_entry(const ListView& v, unsigned idx, unsigned seg_cap) {
-    const unsigned seg = (unsigned)__popcll(__ballot(v.incl <= idx));
-    // the entries before the segment: lane seg - 1's prefix, read with v_readlane (a wave-uniform
-    // lane index) -- a __shfl is a ds_bpermute whose lgkmcnt wait would also wait for the
-    // scalar list loads in flight
-    const unsigned before = seg ? (unsigned)__builtin_amdgcn_readlane((int)v.incl, (int)seg - 1) : 0u;
-    // constant address space: the list is read-only here, so this is a scalar load (s_load,
-    // lgkmcnt) and never waits behind the wave's vector memory operations
-    const __attribute__((address_space(4))) unsigned* l4 = (const __attribute__((address_space(4))) unsigned*)v.list;
-    return l4[seg * seg_cap + (idx - before)];
-}
-
+// The entries of group grp < ngroups: one 8-byte scalar load (constant address space: it never
+// waits behind the wave's vector memory operations); an odd list's last group reads the list's
+// ~0u pad as its second entry.
+static_assert(kSlots == 2, "two entries per group (one 8-byte load, one pad per list)");
 __device__ __forceinline__ void group_entries(const ListView& v, unsigned grp, unsigned seg_cap, unsigned* e) {
-#pragma unroll
-    for (int k = 0; k < kSlots; ++k) {
-        const unsigned idx = grp * kSlots + k;
-        e[k] = idx < v.total ? list_entry(v, idx, seg_cap) : ~0u;
-    }
+    (void)seg_cap;
+    const __attribute__((address_space(4))) unsigned* l4 = (const __attribute__((address_space(4))) unsigned*)v.list;
+    e[0] = l4[2u * grp];
+    e[1] = l4[2u * grp + 1u];
 }
 
 // The lane's unit of a group (the group's first entry exists).
@@ -2082,16 +2138,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
     if (SEM && a.lut) S.lutv = reinterpret_cast<const uint32_t*>(a.lut)[lane];
     const unsigned* cnt = a.list_count;
     unsigned* tail_counter = a.list_count + kLists * kListSegs * kListCountStride;  // zeroed by the prepass
-    const unsigned* lst = a.unit_list;
-    const size_t lstride = (size_t)kListSegs * seg_cap;
-    constexpr int kCnt = kListSegs * kListCountStride;
+    const unsigned* lst = a.units;
     unsigned n0;
     unsigned rot0 = 0;
     if (GATE && !VOTE) {  // free units exist only in gated modes (free_ok): full free, free, general
-        ListView vf = list_view(lst + 2 * lstride, cnt + 2 * kCnt, wave, nwaves, 0u);
-        ListView v1 = list_view(lst + lstride, cnt + kCnt, wave, nwaves, vf.ngroups % nwaves);
+        ListView vf = list_view(lst, cnt, 2, wave, nwaves, 0u);
+        ListView v1 = list_view(lst, cnt, 1, wave, nwaves, vf.ngroups % nwaves);
         rot0 = (vf.ngroups + v1.ngroups) % nwaves;
-        ListView v0 = list_view(lst, cnt, wave, nwaves, rot0);
+        ListView v0 = list_view(lst, cnt, 0, wave, nwaves, rot0);
         const unsigned tail0 = SEMTSDF_TAIL_PCT ? v0.ngroups * SEMTSDF_TAIL_PCT / 100u : 0u;
         v0.ngroups -= tail0;  // the static share: groups 0 .. ngroups - tail0 - 1
         if (vf.i < vf.ngroups)
@@ -2122,7 +2176,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
         }
         if (COUNT) nlive += v1.total + vf.total;
     } else {
-        ListView v0 = list_view(lst, cnt, wave, nwaves, 0u);
+        ListView v0 = list_view(lst, cnt, 0, wave, nwaves, 0u);
         const unsigned tail0 = SEMTSDF_TAIL_PCT ? v0.ngroups * SEMTSDF_TAIL_PCT / 100u : 0u;
         v0.ngroups -= tail0;
         if (v0.i < v0.ngroups)

