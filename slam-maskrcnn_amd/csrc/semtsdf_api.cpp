@@ -1046,8 +1046,10 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
         if ((rc = dev_alloc(v, (void**)&f.unit_list, unit_list_capacity(g) * sizeof(unsigned)))) return bail(rc);
         // + the integrate's dynamic counters (per XCD and workgroup slot), kListCountStride words apart
         if ((rc = dev_alloc(v, (void**)&f.list_count, kListCountWords * sizeof(unsigned)))) return bail(rc);
-        // every unit in at most one list, + one pad per list, bases rounded up to even
-        if ((rc = dev_alloc(v, (void**)&f.units, (unit_count(g) + 2 * kLists + 2) * sizeof(unsigned)))) return bail(rc);
+        // every unit in at most one list, + one pad per list, bases rounded up to even; at least two
+        // entries per persistent wave (k_integrate reads a wave's first free group unconditionally)
+        const uint64_t nunits = std::max<uint64_t>(unit_count(g) + 2 * kLists + 2, 2u * 65536u);
+        if ((rc = dev_alloc(v, (void**)&f.units, nunits * sizeof(unsigned)))) return bail(rc);
     }
     if ((rc = dev_alloc(v, (void**)&v->rcp_table_d, kRcpTable * sizeof(float)))) return bail(rc);
     {

@@ -1006,10 +1006,12 @@ __global__ __launch_bounds__(256) void k_compact_lists(const unsigned* __restric
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) tot[k] += (unsigned)__shfl_xor((int)tot[k], off, 64);
     }
+    // the free list first (k_integrate reads a wave's first free group before the totals), then
+    // the full free list, then the general one
     unsigned base[kLists];
-    base[0] = 0u;
-#pragma unroll
-    for (int k = 1; k < kLists; ++k) base[k] = (base[k - 1] + tot[k - 1] + 2u) & ~1u;
+    base[1] = 0u;
+    base[2] = (tot[1] + 2u) & ~1u;
+    base[0] = (base[2] + tot[2] + 2u) & ~1u;
     // this list's counts, exclusive prefix over the segments
     unsigned cl = c[0];
 #pragma unroll
@@ -1879,12 +1881,17 @@ struct KindOf {
 // The project / classify / load stages of the wave's first group of list v (v.i < v.ngroups).
 template <bool SEM, bool GATE, bool CI32, bool VOTE, bool COUNT, bool SHARD, bool PIN, int KIND>
 __device__ __forceinline__ void list_prime(const IntegrateArgs& a, const UnitGrid& ug, unsigned seg_cap,
-                                           const ListView& v, Pipe& S, Counts& n) {
+                                           const ListView& v, Pipe& S, Counts& n, const unsigned* pre = nullptr) {
     constexpr bool FREE = KindOf<KIND>::FREE, FULL = KindOf<KIND>::FULL;
     const int lane = threadIdx.x & 63;
     const unsigned coff = (unsigned)lane_zq(lane) * 32u + (unsigned)lane_y(lane) * 4u;
     unsigned e[kSlots];
-    group_entries(v, v.i, seg_cap, e);
+    if (pre) {  // loaded ahead (the free list's first group, k_integrate)
+        e[0] = pre[0];
+        e[1] = pre[1];
+    } else {
+        group_entries(v, v.i, seg_cap, e);
+    }
     S.cur = lane_pos(ug, e);
     stage_project<SHARD, PIN, FREE, FULL, VOTE>(a, S.cur, lane, S.P);
     stage_classify<SEM, GATE, VOTE, COUNT, FREE>(a, S.P, S.C, true, n.touch, n.gate, n.lines, S.lutv);
@@ -2142,8 +2149,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
     unsigned n0;
     unsigned rot0 = 0;
     if (GATE && !VOTE) {  // free units exist only in gated modes (free_ok): full free, free, general
+        // the free list lies at the start of the compact array and its groups start at the wave's
+        // own index: the wave's first free group is read before the lists' totals have arrived
+        // (one dependent load less at the start of the kernel; most waves prime a free group)
+        const __attribute__((address_space(4))) unsigned* u4 = (const __attribute__((address_space(4))) unsigned*)lst;
+        const unsigned pre1[2] = {u4[2u * wave], u4[2u * wave + 1u]};
         ListView vf = list_view(lst, cnt, 2, wave, nwaves, 0u);
-        ListView v1 = list_view(lst, cnt, 1, wave, nwaves, vf.ngroups % nwaves);
+        ListView v1 = list_view(lst, cnt, 1, wave, nwaves, 0u);
         rot0 = (vf.ngroups + v1.ngroups) % nwaves;
         ListView v0 = list_view(lst, cnt, 0, wave, nwaves, rot0);
         const unsigned tail0 = SEMTSDF_TAIL_PCT ? v0.ngroups * SEMTSDF_TAIL_PCT / 100u : 0u;
@@ -2151,7 +2163,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
         if (vf.i < vf.ngroups)
             list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 2>(a, ug, seg_cap, vf, S, n);
         else if (v1.i < v1.ngroups)
-            list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 1>(a, ug, seg_cap, v1, S, n);
+            list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 1>(a, ug, seg_cap, v1, S, n, pre1);
         else if (v0.i < v0.ngroups)
             list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0>(a, ug, seg_cap, v0, S, n);
         __syncthreads();
@@ -2161,7 +2173,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
         integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 1, 0>(a, ug, seg_cap, s_rcp, v1, &v0, nwaves, S, n);
         if (SEMTSDF_WAVE_TRACE) {
             tr[3] = wall_clock64();
-            trn = groups_of(vf.total, 0u) | (groups_of(v1.total, vf.ngroups % nwaves) << 20);
+            trn = groups_of(vf.total, 0u) | (groups_of(v1.total, 0u) << 20);
         }
         if (SEMTSDF_DYN_LAST)
             integrate_list_dyn<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>(a, ug, seg_cap, s_rcp, v0, nwaves, tail_counter, S, n);
