@@ -2188,11 +2188,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
         }
         if (COUNT) nlive += v1.total + vf.total;
     } else {
+        // no free units in these modes: the free and full-free lists are empty and the general list
+        // starts at entry 4 of the compact array (k_compact_lists), so the wave's first group is
+        // read before the totals arrive (used when the base is indeed 4)
+        const __attribute__((address_space(4))) unsigned* u4 = (const __attribute__((address_space(4))) unsigned*)lst;
+        const unsigned pre0[2] = {u4[4u + 2u * wave], u4[5u + 2u * wave]};
         ListView v0 = list_view(lst, cnt, 0, wave, nwaves, 0u);
         const unsigned tail0 = SEMTSDF_TAIL_PCT ? v0.ngroups * SEMTSDF_TAIL_PCT / 100u : 0u;
         v0.ngroups -= tail0;
         if (v0.i < v0.ngroups)
-            list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0>(a, ug, seg_cap, v0, S, n);
+            list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0>(a, ug, seg_cap, v0, S, n,
+                                                                   v0.list == lst + 4 ? pre0 : nullptr);
         __syncthreads();
         if (SEMTSDF_WAVE_TRACE) tr[1] = tr[2] = tr[3] = wall_clock64();
         if (SEMTSDF_DYN_LAST)
