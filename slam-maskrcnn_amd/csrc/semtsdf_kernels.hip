@@ -993,7 +993,7 @@ hipError_t launch_cull(const IntegrateArgs& a, hipStream_t s) {
 // is the exclusive prefix of its list's counts.  Runs on the prep stream after the cull, so the
 // integrate reads its first group's entries without the counts' prefix (one dependent load less
 // at its start) and decodes no segment per entry.
-__global__ __launch_bounds__(256) void k_compact_lists(const unsigned* __restrict__ list_count,
+__global__ __launch_bounds__(256) void k_compact_lists(unsigned* __restrict__ list_count,
                                                        const unsigned* __restrict__ seg_list, unsigned seg_cap,
                                                        unsigned* __restrict__ units) {
     // every wave of the workgroup computes the (tiny) prefix itself; all 256 lanes copy
@@ -1045,7 +1045,7 @@ __global__ __launch_bounds__(256) void k_compact_lists(const unsigned* __restric
             t = lane == (unsigned)k ? tot[k] : t;
         }
         units[b + t] = ~0u;  // the pad
-        unsigned* tw = const_cast<unsigned*>(list_count) + kListTotalsWord;
+        unsigned* tw = list_count + kListTotalsWord;  // read only by later launches
         tw[2 * lane] = b;
         tw[2 * lane + 1] = t;
     }
