@@ -517,6 +517,7 @@ def run_pipeline(semtsdf, L, p, local, n_frames=100, n_warm=5):
         "assoc_decisions": int(tm_f.n_assoc),
         "assoc_exact_frames": int(tm_f.assoc_exact_frames),
         "assoc_exact_rows": int(tm_f.assoc_exact_rows),
+        "assoc_pos_max": round(float(tm_f.assoc_pos_max), 6),
         "assoc_exact_note": "decisions (warm-up included) whose certificate left rows to the exact f32 "
                             "pixel-order path (DESIGN.md §4); all_exact_frames_per_s: every row forced onto it",
         "all_exact_frames_per_s": n_frames / t_exact,
@@ -784,7 +785,8 @@ def run_c4_single(semtsdf, L, local, frames, f0, K, warmup, async_prepass=True):
         wm.copy_from(msem.ptr + i * NPX, NPX, stream=vol.stream)
         vol.parse_frame_dev(dbuf.ptr + i * NPX * 2, rbuf.ptr + i * NPX * 3, wm.ptr, Es[i])
 
-    elapsed_s, _, _ = timed_integrate(vol, sem, Kf, 2)
+    elapsed_s, _, tc_s = timed_integrate(vol, sem, Kf, 2)
+    st_s = vol.state()
     res = {
         "workload": "C4 on one GPU: " + C4_SPEC + " (144 GiB)",
         "value": round(1024 ** 3 * K / elapsed / 1e6, 2), "unit": "Mvoxel-updates/s",
@@ -798,7 +800,15 @@ def run_c4_single(semtsdf, L, local, frames, f0, K, warmup, async_prepass=True):
         "per_frame_semantic": {"value": round(1024 ** 3 * Kf / elapsed_s / 1e6, 2), "unit": "Mvoxel-updates/s",
                                "frames_per_s": round(Kf / elapsed_s, 1),
                                "ms_per_step": round(elapsed_s * 1e3 / Kf, 4), "steps": Kf,
-                               "step": "association raycast + relabel + integrate per frame"},
+                               "step": "association raycast + relabel + integrate per frame",
+                               # the decision's exact f32 path over the last pass of Kf frames
+                               "assoc_decisions": int(tc_s.n_assoc),
+                               "exact_frames": int(tc_s.assoc_exact_frames),
+                               "exact_rows": int(tc_s.assoc_exact_rows),
+                               "pos_max": round(float(tc_s.assoc_pos_max), 6),
+                               "n_obs_at_end": int(st_s.n_obs), "num_objs_at_end": int(st_s.num_objs),
+                               "state_note": "every integrated frame (the integrate-only steps before this leg "
+                                             "included) advances n_obs, as tsdf.cu:218-220 (ABI 12)"},
         "touched_per_frame": int(tc.touched / K),
         "device_gib": round(vol.state().device_bytes / 2 ** 30, 1),
     }

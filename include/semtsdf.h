@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SEMTSDF_ABI_VERSION 11
+#define SEMTSDF_ABI_VERSION 12
 #define SEMTSDF_MAX_OBJECTS 32 /* tsdf.cuh:4 */
 
 /* ---- status codes ------------------------------------------------------------ */
@@ -100,7 +100,8 @@ typedef struct semtsdf_state {
     uint64_t local_voxels;   /* local_dim product */
     uint64_t device_bytes;   /* bytes of device memory owned by the handle */
     uint64_t label_votes_dropped; /* histogram votes of ids >= 32 dropped by the integrate since the
-                                     last reset (SEMTSDF_F_ID_SATURATE) */
+                                     last reset: the id policy without SEMTSDF_F_ID_SATURATE (with
+                                     the flag no such id is minted and this stays 0) */
 } semtsdf_state;
 
 /* Per-frame association result (filter_overlaps tsdf.cu:304-416). */
@@ -137,6 +138,8 @@ typedef struct semtsdf_timing {
     uint64_t assoc_exact_rows;   /* rows decided on it, summed over those decisions */
     uint64_t touched_lines;      /* 128-B lines of the sdf array (8 y x 4 z voxels of a tile) holding a
                                     touched voxel: the line-granular floor of the state traffic (count mode only) */
+    double assoc_pos_max;        /* largest positive association term log(p / n_obs) any decision saw
+                                    (p > n_obs; 0: none); from log 32 on every row takes the exact path */
 } semtsdf_timing;
 
 /* ---- library ------------------------------------------------------------------------ */
@@ -177,8 +180,15 @@ int semtsdf_reset(semtsdf_vol* v, void* stream);
 
 /* ---- integrate (a4) ------------------------------------------------------------------
  * One frame into the volume: E = extrinsic * init_extrinsic_inv (row-major 4x4 f32,
- * tsdf.cu:217).  depth u16 [H*W], rgb u8 [H*W*3], mask u8 [H*W] (labels < 32; may be
- * NULL unless SEMANTIC).  Does NOT change n_obs (the driver semtsdf_parse_frame does). */
+ * tsdf.cu:217).  depth u16 [H*W], rgb u8 [H*W*3], mask u8 [H*W] (may be NULL unless
+ * SEMANTIC).  In a SEMANTIC volume every integrated frame is an observation, as every
+ * integrated frame of the reference advances n_obs_ (tsdf.cu:218-220): the first one (n_obs ==
+ * 0) sets num_objs = max(mask) + 1 (tsdf.cu:463-468), and each one advances n_obs by 1, so
+ * semtsdf_associate + semtsdf_integrate leave the state semtsdf_parse_frame leaves (ABI 12; up
+ * to ABI 11 only parse_frame advanced n_obs).  Mask labels >= 32: without
+ * SEMTSDF_F_ID_SATURATE their histogram votes are dropped and counted and the host-pointer
+ * call reports SEMTSDF_ERR_LABEL after applying the frame in full; with it they are refused
+ * (SEMTSDF_ERR_LABEL, nothing applied). */
 int semtsdf_integrate(semtsdf_vol* v, const uint16_t* depth, const uint8_t* rgb,
                       const uint8_t* mask, const float E[16], void* stream);
 /* Same with device pointers (inputs already resident in HBM). */
@@ -295,7 +305,8 @@ int semtsdf_shard_assoc_apply_exact(semtsdf_vol* v, const int64_t* reduced_d, co
  * SEMTSDF_EXCHANGE_MIN for shards driven from one process. */
 int semtsdf_min_i64(int64_t* dst_d, const int64_t* src_d, size_t n, void* stream);
 /* parse_frame for a sharded handle: the host runs the association protocol above (when
- * n_obs > 0), then integrate_dev, then note_integrated (n_obs++, first-frame object count). */
+ * n_obs > 0), then integrate_dev (which advances n_obs and sets the first frame's object count).
+ * note_integrated did that up to ABI 11; it is kept as a no-op that checks its handle. */
 int semtsdf_shard_note_integrated(semtsdf_vol* v, const uint8_t* mask_d, void* stream);
 
 /* ---- mask producer contract --------------------------------------

@@ -1151,6 +1151,25 @@ int semtsdf_reset(semtsdf_vol* v, void* stream) {
     return SEMTSDF_OK;
 }
 
+// The observation count of a semantic volume follows its integrated frames, as in the
+// reference, where every integrated frame advances n_obs_ (tsdf.cu:218-220) and the first one
+// sets num_objs = max(mask) + 1 (tsdf.cu:463-468): the split calls (associate, then integrate)
+// leave the state TSDF::parse_frame leaves, and an association never sees histogram counts
+// above n_obs that the reference could not produce (r06).  Before the frame's
+// integrate: the first frame's object count.
+static int observe_before(semtsdf_vol* v, const uint8_t* mask_d, hipStream_t s) {
+    if (!(v->p.flags & SEMTSDF_F_SEMANTIC) || v->n_obs > 0) return SEMTSDF_OK;
+    if (!mask_d) return fail(SEMTSDF_ERR_INVALID, "semantic volume needs a mask");
+    if (int rc = tables_ready(v, s)) return rc;
+    HIPC(launch_mask_stats(mask_d, (int)npx(v), v->tables_d, s));
+    HIPC(launch_first_frame_objs(v->tables_d, v->num_objs_d, s));
+    return SEMTSDF_OK;
+}
+// ... and after it (only when it was enqueued: a failed integrate leaves n_obs alone)
+static void observe_after(semtsdf_vol* v) {
+    if (v->p.flags & SEMTSDF_F_SEMANTIC) v->n_obs++;
+}
+
 int semtsdf_integrate(semtsdf_vol* v, const uint16_t* depth, const uint8_t* rgb, const uint8_t* mask,
                       const float E[16], void* stream) {
     if (!v || !depth || !rgb) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
@@ -1158,31 +1177,55 @@ int semtsdf_integrate(semtsdf_vol* v, const uint16_t* depth, const uint8_t* rgb,
     hipStream_t s = pick(v, stream);
     const size_t n = npx(v);
     const bool sem = v->p.flags & SEMTSDF_F_SEMANTIC;
+    bool past_bins = false;  // a label >= 32 in the mask
     if (sem) {
         if (!mask) return fail(SEMTSDF_ERR_INVALID, "semantic volume needs a mask");
-        int rc = validate_mask_host(v, mask);
-        if (rc) return rc;
+        // id policy 0: ids >= 32 (an association's fresh ids past the histogram, semtsdf_associate)
+        // are integrated with their votes dropped and counted, and the frame reports ERR_LABEL
+        // once applied in full, as semtsdf_parse_frame does; with SEMTSDF_F_ID_SATURATE no
+        // association mints them, so such a label is a bad input
+        if (v->p.flags & SEMTSDF_F_ID_SATURATE) {
+            if (int rc = validate_mask_host(v, mask)) return rc;
+        } else {
+            past_bins = validate_mask_host(v, mask) != SEMTSDF_OK;
+        }
     }
     HIPC(hipMemcpyAsync(v->depth_d, depth, n * 2, hipMemcpyHostToDevice, s));
     HIPC(hipMemcpyAsync(v->rgb_d, rgb, n * 3, hipMemcpyHostToDevice, s));
     if (sem) HIPC(hipMemcpyAsync(v->mask_d, mask, n, hipMemcpyHostToDevice, s));
+    if (int rc = observe_before(v, sem ? v->mask_d : nullptr, s)) return rc;
     int rc = integrate_impl(v, v->depth_d, v->rgb_d, sem ? v->mask_d : nullptr, nullptr, E, s);
     if (rc) return rc;
+    observe_after(v);
     HIPC(hipStreamSynchronize(s));  // host buffers are borrowed for the call only
-    return SEMTSDF_OK;
+    if (!sem) return SEMTSDF_OK;
+    const int rc_votes = check_bad_label(v, s);  // takes note of the votes this frame dropped
+    if (past_bins)
+        return fail(SEMTSDF_ERR_LABEL, "mask labels >= %d have no histogram bin: their votes were dropped, the "
+                    "frame was applied (SEMTSDF_F_ID_SATURATE keeps ids below %d)", kMaxObjects, kMaxObjects);
+    return rc_votes;
 }
 
 int semtsdf_integrate_dev(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d, const uint8_t* mask_d,
                           const float E[16], void* stream) {
     if (!v) return fail(SEMTSDF_ERR_INVALID, "NULL handle");
-    return integrate_impl(v, depth_d, rgb_d, mask_d, nullptr, E, pick(v, stream));
+    HIPC(hipSetDevice(v->device));
+    hipStream_t s = pick(v, stream);
+    if (int rc = observe_before(v, mask_d, s)) return rc;
+    if (int rc = integrate_impl(v, depth_d, rgb_d, mask_d, nullptr, E, s)) return rc;
+    observe_after(v);
+    return SEMTSDF_OK;
 }
 
 int semtsdf_integrate_dev_async(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d, const uint8_t* mask_d,
                                 const float E[16], void* inputs_ready, void* stream) {
     if (!v) return fail(SEMTSDF_ERR_INVALID, "NULL handle");
     HIPC(hipSetDevice(v->device));
-    return integrate_impl(v, depth_d, rgb_d, mask_d, nullptr, E, pick(v, stream), true, (hipEvent_t)inputs_ready);
+    hipStream_t s = pick(v, stream);
+    if (int rc = observe_before(v, mask_d, s)) return rc;
+    if (int rc = integrate_impl(v, depth_d, rgb_d, mask_d, nullptr, E, s, true, (hipEvent_t)inputs_ready)) return rc;
+    observe_after(v);
+    return SEMTSDF_OK;
 }
 
 int semtsdf_integrate_vote_dev(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d, const int32_t* cls_d,
@@ -1627,17 +1670,12 @@ int semtsdf_shard_assoc_apply(semtsdf_vol* v, const int64_t* reduced_d, uint8_t*
     return SEMTSDF_OK;
 }
 
+// ABI <= 11 advanced n_obs here after a sharded integrate; the integrate entry points do it
+// themselves since ABI 12 (observe_before/after), so this call only checks its handle.
 int semtsdf_shard_note_integrated(semtsdf_vol* v, const uint8_t* mask_d, void* stream) {
+    (void)mask_d;
+    (void)stream;
     if (!v) return fail(SEMTSDF_ERR_INVALID, "NULL argument");
-    HIPC(hipSetDevice(v->device));
-    hipStream_t s = pick(v, stream);
-    if (v->n_obs == 0 && (v->p.flags & SEMTSDF_F_SEMANTIC)) {
-        if (!mask_d) return fail(SEMTSDF_ERR_INVALID, "semantic volume needs a mask");
-        if (int rc = tables_ready(v, s)) return rc;
-        HIPC(launch_mask_stats(mask_d, (int)npx(v), v->tables_d, s));
-        HIPC(launch_first_frame_objs(v->tables_d, v->num_objs_d, s));
-    }
-    v->n_obs++;
     return SEMTSDF_OK;
 }
 
@@ -2095,10 +2133,11 @@ int semtsdf_get_timing(semtsdf_vol* v, semtsdf_timing* out) {
     out->full_units = c[5];
     out->lazy_voxels = c[6];
     out->touched_lines = c[7];
-    unsigned xr[2] = {0, 0};  // AssocExact::frames, rows
+    unsigned xr[3] = {0, 0, 0};  // AssocExact::frames, rows, pos_max
     HIPC(hipMemcpy(xr, &v->exact_d->frames, sizeof(xr), hipMemcpyDeviceToHost));
     out->assoc_exact_frames = xr[0];
     out->assoc_exact_rows = xr[1];
+    out->assoc_pos_max = xr[2] / kFixScale;
     out->prep_ms = v->t_prep;
     out->n_prep = v->n_prep;
     return SEMTSDF_OK;
@@ -2116,7 +2155,7 @@ int semtsdf_reset_timing(semtsdf_vol* v) {
     v->n_integrate = v->n_assoc = v->n_render = v->n_prep = 0;
     HIPC(hipMemset(v->counters_d, 0, 2 * sizeof(unsigned long long)));
     HIPC(hipMemset(v->counters_d + 3, 0, (kCounters - 3) * sizeof(unsigned long long)));
-    HIPC(hipMemset(&v->exact_d->frames, 0, 2 * sizeof(unsigned)));
+    HIPC(hipMemset(&v->exact_d->frames, 0, 3 * sizeof(unsigned)));
     return SEMTSDF_OK;
 }
 

@@ -214,7 +214,7 @@ struct AssocExact {
     unsigned counter;
     unsigned frames;        // decisions that took the exact path (instrumentation)
     unsigned rows;          // rows decided from exact sums, summed over frames
-    unsigned pad;
+    unsigned pos_max;       // largest AssocTables::pos_max any decision saw (instrumentation)
 };
 
 struct DecideArgs {

@@ -3613,11 +3613,14 @@ __global__ __launch_bounds__(256) void k_assoc_decide(DecideArgs a) {
         D->max_obj_now = mx;
         D->num_objs_before = num;
         D->num_objs_after = after;
-        D->bad_label = (after > kMaxObjects || mx > kMaxObjects) ? 1 : 0;
+        // only a frame that mints an id past the histogram (or brings a raw label past it) is
+        // flagged: later frames of a volume beyond 32 objects mint none of their own
+        D->bad_label = ((L.newcount > 0 && after > kMaxObjects) || mx > kMaxObjects) ? 1 : 0;
         D->exact_rows = Fx;
         D->exact_missing = have_px ? 0u : F;
         D->reject_rows = R;
         *a.num_objs_dev = after;
+        if (posm > a.X->pos_max) a.X->pos_max = posm;
         if (Fx) {
             a.X->frames += 1u;
             a.X->rows += (unsigned)__popc(Fx);

@@ -124,6 +124,7 @@ class Timing(C.Structure):
         ("assoc_exact_frames", C.c_uint64),
         ("assoc_exact_rows", C.c_uint64),
         ("touched_lines", C.c_uint64),
+        ("assoc_pos_max", C.c_double),
     ]
 
 

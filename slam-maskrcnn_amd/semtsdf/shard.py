@@ -272,15 +272,10 @@ class LocalShardGroup:
         self.vols[0].sync()  # the staging buffers are freed on return
 
     def parse_frame_dev(self, depth_ptr, rgb_ptr, mask_ptrs, E):
-        import ctypes as C
-
-        from . import _lib as L
-
         if self.vols[0].state().n_obs > 0:
             self.associate_dev(mask_ptrs, E)
-        for v, m in zip(self.vols, mask_ptrs):
+        for v, m in zip(self.vols, mask_ptrs):  # each integrate advances its handle's n_obs (ABI 12)
             v.integrate_dev(depth_ptr, rgb_ptr, m, E, self.stream)
-            L.check(L.load().semtsdf_shard_note_integrated(v.handle, C.c_void_p(m), self._s()))
 
 
 def _sum_int32_dev(ptrs, out_ptr, n, stream):
@@ -454,14 +449,9 @@ class DistShardGroup:
     def parse_frame_dev(self, depth_ptr: int, rgb_ptr: int, mask_ptr: int, E, want_stats=False):
         """One frame of the sharded pipeline (association when n_obs > 0, integrate); returns the
         association's stats when want_stats (None without an association)."""
-        import ctypes as C
-
-        from . import _lib as L
-
         st = None
         with self._on_stream():
             if self.vol.state().n_obs > 0:
                 st = self.associate_dev(mask_ptr, E, want_stats=want_stats)
-            self.vol.integrate_dev(depth_ptr, rgb_ptr, mask_ptr, E, self._stream())
-            L.check(L.load().semtsdf_shard_note_integrated(self.vol.handle, C.c_void_p(mask_ptr), self._stream()))
+            self.vol.integrate_dev(depth_ptr, rgb_ptr, mask_ptr, E, self._stream())  # advances n_obs
         return st

@@ -27,7 +27,7 @@ def test_library_exports_every_symbol():
     lib = L.load()
     for n in declared():
         assert hasattr(lib, n), n
-    assert lib.semtsdf_abi_version() == 11
+    assert lib.semtsdf_abi_version() == 12
     key = lib.semtsdf_build_key().decode()
     assert len(key) == 64 and int(key, 16) >= 0  # the sha-256 build key (__graft_entry__.build_key)
 
@@ -42,8 +42,8 @@ def test_structs_match_header_sizes():
     assert C.sizeof(L.AssocStats) == 4 * (2 + 32 + 32) + 256 + 4 + 4
     # semtsdf_state: u32 n_obs, i32 num_objs, 3 i32 local_dim (+ 4 B padding), 3 u64
     assert C.sizeof(L.State) == 4 * 5 + 4 + 8 * 3
-    # semtsdf_timing: 16 fields of 8 bytes (doubles or u64)
-    assert C.sizeof(L.Timing) == 8 * 17
+    # semtsdf_timing: 18 fields of 8 bytes (doubles or u64)
+    assert C.sizeof(L.Timing) == 8 * 18
 
 
 def test_argument_errors_without_a_device():

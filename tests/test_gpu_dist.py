@@ -86,7 +86,6 @@ def _rank_pass(semtsdf, L, DistShardGroup, torch, frames, rank, world, exchange,
             out["luts"].append(bytes(stt.lut))
             out["exact_rows"].append(int(stt.exact_rows))
         vol.integrate_dev(d.data_ptr(), r.data_ptr(), m.data_ptr(), E, grp._stream())
-        L.check(L.load().semtsdf_shard_note_integrated(vol.handle, L.ptr(m.data_ptr()), grp._stream()))
         torch.cuda.synchronize()
         out["masks"].append(m.cpu().numpy())
         if single is not None:

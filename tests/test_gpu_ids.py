@@ -3,11 +3,13 @@
 The reference gives every unmatched label the id num_objs++ without a bound
 (src/SfM_CUDA/tsdf.cu:379-383; the u8 mask stores it modulo 256) and its integrate counts an
 id >= 32 in the bins of the next voxel (tsdf.cu:61, out of bounds).  Here a stream whose masks
-keep introducing new instances drives more than 40 distinct ids through parse_frame_dev:
+keep introducing new instances drives more than 40 distinct ids through parse_frame_dev (and a last frame without
+instances):
 
 * policy 0 (default): the reference's ids and object count, votes of ids >= 32 dropped and
-  counted (semtsdf_state.label_votes_dropped); the host parse_frame reports ERR_LABEL for such
-  a frame after applying it in full, and the handle keeps integrating;
+  counted (semtsdf_state.label_votes_dropped); the host parse_frame, and the split host calls
+  (associate, then integrate), report ERR_LABEL for exactly the frames that mint such an id,
+  after applying them in full, and the handle keeps integrating;
 * policy 1 (SEMTSDF_F_ID_SATURATE, a documented deviation): a label that would get an id >= 32
   becomes background, num_objs stops at 32, nothing is dropped.
 
@@ -24,7 +26,7 @@ pytestmark = pytest.mark.gpu
 
 KI = (520.9, 521.0, 325.1, 249.7)
 D = 64
-NFR = 9
+NFR = 10  # the last frame carries no instance: it mints nothing on a volume past 32 objects
 
 
 def _frames():
@@ -37,7 +39,7 @@ def _frames():
     for k, fr in enumerate(frames):
         # 9 instance rectangles per frame at fresh places: most labels match no previous id
         m = np.zeros((480, 640), np.uint8)
-        for lab in range(1, 10):
+        for lab in range(1, 10 if k < NFR - 1 else 1):
             y, x = int(rng.integers(0, 400)), int(rng.integers(0, 560))
             h, w = int(rng.integers(40, 80)), int(rng.integers(40, 80))
             m[y:y + h, x:x + w] = lab
@@ -102,9 +104,14 @@ def test_more_than_31_ids_follow_the_id_policy(oracle, policy):
 
     vol = semtsdf.Volume(p, 0)  # device pipeline (parse_frame_dev)
     host = semtsdf.Volume(params(), 0)  # host pipeline (parse_frame): the synchronous error report
+    split = semtsdf.Volume(params(), 0)  # the split host calls: associate, then integrate (ABI 12)
     npx = 640 * 480
     dbuf, rbuf, mbuf = DeviceBuffer(npx * 2), DeviceBuffer(npx * 3), DeviceBuffer(npx)
-    label_errors = 0
+    # the frames that mint an id past the histogram under policy 0: exactly these report ERR_LABEL
+    # (a frame of a volume already beyond 32 objects that mints nothing does not)
+    minting = [k for k in range(1, NFR) if policy == 0 and ref_nums[k] > 32 and ref_nums[k] > ref_nums[k - 1]]
+    assert len(minting) >= 2 and any(ref_nums[k] > 32 and k not in minting for k in range(NFR)) or policy == 1
+    label_errors, split_errors = [], []
     for k, (fr, m) in enumerate(zip(frames, masks)):
         E = (fr.w2c @ frames[0].c2w).astype(np.float32)
         dbuf.upload(fr.depth, vol.stream)
@@ -122,16 +129,36 @@ def test_more_than_31_ids_follow_the_id_policy(oracle, policy):
             host.parse_frame(fr.depth, fr.rgb, mh, E)
         except L.SemTSDFError as e:  # the frame is applied in full before the error is reported
             assert e.code == L.ERR_LABEL and policy == 0, (k, str(e))
-            label_errors += 1
+            label_errors.append(k)
         assert np.array_equal(mh.reshape(-1), ref_masks[k].reshape(-1)), f"host frame {k}"
         assert host.state().num_objs == ref_nums[k]
+        ms = np.ascontiguousarray(m.copy())
+        failed = False
+        if k > 0:
+            try:
+                split.associate(ms, E)
+            except L.SemTSDFError as e:  # the mask is relabelled before the error is reported
+                assert e.code == L.ERR_LABEL and policy == 0, (k, str(e))
+                failed = True
+        try:
+            split.integrate(fr.depth, fr.rgb, ms, E)  # ids >= 32 integrated, their votes dropped
+        except L.SemTSDFError as e:
+            assert e.code == L.ERR_LABEL and policy == 0, (k, str(e))
+            failed = True
+        if failed:
+            split_errors.append(k)
+        assert np.array_equal(ms.reshape(-1), ref_masks[k].reshape(-1)), f"split frame {k}"
+        sst = split.state()
+        assert sst.num_objs == ref_nums[k] and sst.n_obs == k + 1, (k, sst.num_objs, sst.n_obs)
     st = vol.state()
+    assert label_errors == minting and split_errors == minting, (label_errors, split_errors, minting)
     if policy == 0:
-        assert st.num_objs >= 40 and st.label_votes_dropped > 0 and label_errors >= 2
+        assert st.num_objs >= 40 and st.label_votes_dropped > 0
+        assert split.state().label_votes_dropped == st.label_votes_dropped
     else:
-        assert st.num_objs == 32 and st.label_votes_dropped == 0 and label_errors == 0
+        assert st.num_objs == 32 and st.label_votes_dropped == 0
         assert max(int(x.max()) for x in ref_masks) < 32
-    for v in (vol, host):
+    for v in (vol, host, split):
         out = v.download(hist=True)
         assert np.array_equal(out["sdf"].view(np.uint32), ost.sdf.view(np.uint32))
         assert np.array_equal(out["wt"], ost.wt) and np.array_equal(out["color"], ost.color)
@@ -141,3 +168,4 @@ def test_more_than_31_ids_follow_the_id_policy(oracle, policy):
         b.free()
     vol.close()
     host.close()
+    split.close()

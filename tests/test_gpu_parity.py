@@ -464,14 +464,22 @@ def test_error_paths(S, stream):
         semtsdf.Volume(p, 0)  # not placed: voxel == 0
     semtsdf.place_from_frame(p, frames[0].depth, 2.5, L.PLACE_SFM)
     vol = semtsdf.Volume(p, 0)
-    bad = frames[1].mask.copy()
-    bad[0, 0] = 40
-    with pytest.raises(semtsdf.SemTSDFError) as e:
-        vol.integrate(frames[1].depth, frames[1].rgb, bad, np.eye(4, dtype=np.float32))
-    assert e.value.code == L.ERR_LABEL
     with pytest.raises(semtsdf.SemTSDFError) as e:
         vol.associate(np.ascontiguousarray(frames[1].mask.copy()), np.eye(4, dtype=np.float32))
     assert e.value.code == L.ERR_STATE  # n_obs == 0 (tsdf.cu:426)
+    bad = frames[1].mask.copy()
+    bad[0, 0] = 40
+    # id policy 0: the frame is applied (its observation counted), then ERR_LABEL is reported
+    with pytest.raises(semtsdf.SemTSDFError) as e:
+        vol.integrate(frames[1].depth, frames[1].rgb, bad, np.eye(4, dtype=np.float32))
+    assert e.value.code == L.ERR_LABEL and vol.state().n_obs == 1
+    vol.close()
+    # SEMTSDF_F_ID_SATURATE: no association mints such an id, so the label is refused, nothing applied
+    p.flags |= L.F_ID_SATURATE
+    vol = semtsdf.Volume(p, 0)
+    with pytest.raises(semtsdf.SemTSDFError) as e:
+        vol.integrate(frames[1].depth, frames[1].rgb, bad, np.eye(4, dtype=np.float32))
+    assert e.value.code == L.ERR_LABEL and vol.state().n_obs == 0
     vol.close()
 
 
@@ -573,7 +581,6 @@ def test_sharded_pipeline_equals_single_volume(S, oracle, stream, nshards, chunk
                 assert ss.num_objs == stats.num_objs and bytes(ss.lut) == bytes(stats.lut)
         for sh, mb in zip(shards, mbufs):
             sh.integrate_dev(dbuf.ptr, rbuf.ptr, mb.ptr, E, grp.stream)
-            L.check(L.load().semtsdf_shard_note_integrated(sh.handle, L.ptr(mb.ptr), L.ptr(grp.stream)))
         for mb in mbufs:
             got = np.zeros(npx, np.uint8)
             mb.download(got, grp.stream)
