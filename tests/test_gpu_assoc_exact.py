@@ -202,28 +202,78 @@ def _run(S, oracle, vol, case, W, H, eps=0.05):
     return st, got, r0, r1
 
 
-def tied_rows(T, max_obj_now, thr, rel=1e-5):
+TERM_SLACK = 2.0 ** -29 + 2.0 ** -20  # kTermSlack of k_assoc_decide (fixed point + device logf, per term)
+
+
+def term_counts(mask, box, max_obj_now):
+    """cnts[m][n] of filter_overlaps (tsdf.cu:312-334): the pixels of label m (first loop) plus
+    every box-n pixel of another label (second loop)."""
+    mk = mask.reshape(-1).astype(np.int64)
+    bx = box.reshape(mk.size, 32) != 0
+    c1 = np.bincount(mk, minlength=256)[:32].astype(np.int64)
+    c2 = bx.sum(axis=0).astype(np.int64)
+    C = np.zeros((32, 32), np.int64)
+    for m in range(1, min(max_obj_now, 32)):
+        C[m] = c1[m] + c2 - bx[mk == m].sum(axis=0)
+    return C
+
+
+def cert_interval(n, p):
+    """The certificate's interval (prob_interval in semtsdf_kernels.hip, no positive terms) around
+    a candidate of n terms whose mean log is log p: every f32 value exp(A / n) the reference can
+    form from those terms lies in it.  Its half-width is at least TERM_SLACK + gamma_n |log p| with
+    gamma_n ~ (n - 1) 2^-24 (recursive f32 summation)."""
+    S = n * np.log(p)
+    g = (n - 1) * 2.0 ** -24
+    gam = g / (1.0 - g)
+    slo = S - n * TERM_SLACK
+    shi = min(S + n * TERM_SLACK, 0.0)
+    alo, ahi = slo - gam * abs(slo), shi + gam * abs(shi)
+    q0, q1 = alo / n, ahi / n
+    return (np.exp(q0 - abs(q0) * 2.0 ** -24) * (1 - 2.0 ** -23),
+            np.exp(q1 + abs(q1) * 2.0 ** -24) * (1 + 2.0 ** -23))
+
+
+def tied_rows(T, max_obj_now, thr, C, rel=1e-5):
     """Rows of a decision whose outcome the reference's f32 rounding decides: from the candidate
     probabilities of double accumulation (oracle precision 1, table T), a row whose two best
     candidates lie within `rel` of each other (split), whose best candidate ties another row's
     for the same previous id (greedy), or whose best lies within `rel` of 3 * prior (threshold).
-    The certificate's intervals are far wider than `rel` (gamma = n 2^-24 over n >= 10^3 pixels),
-    so such a row is either proved rejected or decided from its exact f32 sums."""
-    rows, best = set(), {}
+
+    Why rel = 1e-5 is tighter than the certificate: the split and threshold generators give a
+    row n >= (W/4)(H/4) >= 1200 pixels and a mean log of magnitude >= 0.5 (half its terms are
+    log prior = -3.0, or the mean sits at log 0.15 = -1.9), so the f32 summation bound alone,
+    gamma_n |mean log| >= 1199 * 2^-24 * 0.5 = 3.6e-5, exceeds 1e-5; greedy ties are exact by
+    construction (equal terms).  The relation is asserted per row below (`undecidable`): the double
+    values of every tied row lie inside the certificate's own intervals (C: term counts), so the
+    certificate cannot decide such a row and it must be exact or certainly rejected."""
+    rows, best = {}, {}
     for i in range(1, min(max_obj_now, 32)):
         r = T[i, 1:]
-        o = np.sort(r)[::-1]
+        order = np.argsort(r)[::-1]
+        o = r[order]
         if o[0] <= 0:
             continue
-        best[i] = (int(np.argmax(r)) + 1, o[0])
+        best[i] = (int(order[0]) + 1, o[0])
         if o[1] > 0 and o[0] - o[1] <= rel * o[0]:
-            rows.add(i)
+            rows.setdefault(i, []).append(("split", (i, int(order[0]) + 1), (i, int(order[1]) + 1)))
         if abs(o[0] - thr) <= rel * thr:
-            rows.add(i)
+            rows.setdefault(i, []).append(("threshold", (i, int(order[0]) + 1), None))
     for i, (j, p) in best.items():
-        if any(k != i and j2 == j and abs(p - p2) <= rel * max(p, p2) for k, (j2, p2) in best.items()):
-            rows.add(i)
-    return rows, best
+        for k, (j2, p2) in best.items():
+            if k != i and j2 == j and abs(p - p2) <= rel * max(p, p2):
+                rows.setdefault(i, []).append(("greedy", (i, j), (k, j2)))
+
+    def undecidable(kind, a, b):
+        lo_a, hi_a = cert_interval(C[a], T[a])
+        if kind == "threshold":
+            return lo_a <= thr <= hi_a
+        lo_b, hi_b = cert_interval(C[b], T[b])
+        return lo_a <= hi_b and lo_b <= hi_a
+
+    for i, ties in rows.items():
+        assert any(undecidable(*t) for t in ties), (i, ties, [cert_interval(C[t[1]], T[t[1]]) for t in ties])
+    return set(rows), best
 
 
 @pytest.mark.parametrize("W,H,ncases,seed,min_disagree,min_ties",
@@ -264,7 +314,7 @@ def test_decisions_equal_f32_pixel_order_rule_on_near_ties(S, oracle, W, H, ncas
         probs, box, mask, n_obs, num_objs = case
         T = np.zeros((32, 32))
         oracle.filter_overlaps(probs.reshape(-1), box.reshape(-1), mask, n_obs, num_objs, 0.05, precision=1, table=T)
-        rows, best = tied_rows(T, mx0, thr)
+        rows, best = tied_rows(T, mx0, thr, term_counts(mask, box, mx0))
         for i in rows:
             ex, rj = (st.exact_rows >> i) & 1, (st.reject_rows >> i) & 1
             assert ex or rj, (c, kind.__name__, i, hex(st.exact_rows), hex(st.reject_rows))
