@@ -236,6 +236,9 @@ def loaded_build_key() -> str | None:
     return None if k in (None, "unknown") else k
 
 
+CALIBRATION = "profiles/r06/calib/calibration.json"  # tools/calib_pmc.sh
+
+
 def read_traffic(path, dim, world):
     """PMC bytes per launch of the integrate kernel, only if measured on this very library
     build (tools/traffic.py stamps the build key and the binary's SHA-256) and configuration."""
@@ -249,11 +252,13 @@ def read_traffic(path, dim, world):
     if tj.get("dim") != dim or tj.get("n_gpus", 1) != world:
         return None, "traffic record is for another configuration"
     key = loaded_build_key()
+    # the x2 / x1 corrections checked on known byte counts of the integrate's access patterns
+    cal = f"; corrections calibrated in {CALIBRATION}" if os.path.exists(os.path.join(ROOT, CALIBRATION)) else ""
     if tj.get("build_key") and key == tj["build_key"]:
-        return tj.get("bytes_per_launch"), f"PMC FETCH_SIZE x2 + WRITE_SIZE of build key {key[:12]}"
+        return tj.get("bytes_per_launch"), f"PMC FETCH_SIZE x2 + WRITE_SIZE of build key {key[:12]}{cal}"
     if tj.get("lib_sha256") != loaded_lib_sha256():
         return None, "traffic record was measured on another library build"
-    return tj.get("bytes_per_launch"), f"PMC FETCH_SIZE x2 + WRITE_SIZE of lib {tj['lib_sha256'][:12]}"
+    return tj.get("bytes_per_launch"), f"PMC FETCH_SIZE x2 + WRITE_SIZE of lib {tj['lib_sha256'][:12]}{cal}"
 
 
 def place(semtsdf, L, D, f0, dimz=None):

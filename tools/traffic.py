@@ -17,6 +17,10 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# known-byte record of the correction for the integrate's own access patterns (tools/membench_calib.hip,
+# tools/calib_pmc.sh): x2 holds for 16-B, 8-B and 4-B loads and line-distinct 8-B gathers; x1 for
+# 16-B non-temporal stores
+CALIBRATION = "profiles/r06/calib/calibration.json"
 
 
 def lib_sha256(path=None):
@@ -55,7 +59,8 @@ def main():
     rec = {"kernel": pat, "dim": dim, "n_gpus": n_gpus, "dispatches": len(agg["FETCH_SIZE"]),
            "fetch_size_kib_raw": fetch_kib, "write_size_kib_raw": write_kib,
            "fetch_bytes": fetch, "write_bytes": write, "bytes_per_launch": fetch + write,
-           "correction": "FETCH_SIZE x2 (gfx950 wide-read tally), WRITE_SIZE x1", "lib_sha256": lib_sha256(),
+           "correction": "FETCH_SIZE x2 (gfx950 wide-read tally), WRITE_SIZE x1", "calibration": CALIBRATION,
+           "lib_sha256": lib_sha256(),
            "build_key": lib_build_key()}
     with open(out, "w") as f:
         json.dump(rec, f, indent=1)
