@@ -98,6 +98,7 @@ struct semtsdf_vol {
         unsigned* unit_list = nullptr;   // live units of the frame (cull pass)
         unsigned* list_count = nullptr;  // [kLists][kListSegs * kListCountStride] (general, free, full free)
         unsigned* units = nullptr;       // the lists compacted back to back (k_compact_lists)
+        unsigned* first_tab = nullptr;   // inside units: each persistent wave's first group (XCD split)
         hipEvent_t prep_done = nullptr;  // the set's prepass finished (prep_stream)
         hipEvent_t set_free = nullptr;   // the integrate reading the set finished (recorded once async is in use)
         bool free_recorded = false;
@@ -412,6 +413,8 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
     a.unit_list = F.unit_list;
     a.list_count = F.list_count;
     a.units = F.units;
+    a.first_tab = F.first_tab;
+    a.first_nwaves = integrate_pre_waves();
     a.rcp_table = v->rcp_table_d;
     screen_map(a);
     a.pinhole = (a.K[1] == 0.0f && a.K[3] == 0.0f && a.K[6] == 0.0f && a.K[7] == 0.0f && a.K[8] == 1.0f) ? 1 : 0;
@@ -514,7 +517,12 @@ int integrate_impl(semtsdf_vol* v, const uint16_t* depth_d, const uint8_t* rgb_d
     F.reader = s;
     if (v->async_used && async && own_order) {
         F.free_recorded = false;  // a later prepass ordered otherwise records its event then
-    } else if (v->async_used) {  // a later asynchronous prepass into this set waits for this integrate
+    } else if (v->async_used || s != v->stream) {
+        // a later asynchronous prepass into this set waits for this integrate; recorded on a caller's
+        // stream before the first asynchronous frame too, so that frame's prepass (on the prep stream)
+        // waits for the stream that read the set, not for its own caller stream
+        if (!F.set_free)
+            if (int rc = ensure_prep_stream(v)) return rc;  // the sets' events
         HIPC(hipEventRecord(F.set_free, s));
         F.free_recorded = true;
     }
@@ -1048,8 +1056,10 @@ int semtsdf_create(const semtsdf_params* p, int device, semtsdf_vol** out) {
         if ((rc = dev_alloc(v, (void**)&f.list_count, kListCountWords * sizeof(unsigned)))) return bail(rc);
         // every unit in at most one list, + one pad per list, bases rounded up to even; at least two
         // entries per persistent wave (k_integrate reads a wave's first free group unconditionally)
-        const uint64_t nunits = std::max<uint64_t>(unit_count(g) + 2 * kLists + 2, 2u * 65536u);
-        if ((rc = dev_alloc(v, (void**)&f.units, nunits * sizeof(unsigned)))) return bail(rc);
+        const uint64_t nunits = std::max<uint64_t>(unit_count(g) + 2 * kLists + 2, 2u * (uint64_t)kPreWaves + 6u);
+        // + the first-group table of the XCD split (two entries per wave slot, k_compact_lists)
+        if ((rc = dev_alloc(v, (void**)&f.units, (nunits + 2u * (uint64_t)kPreWaves) * sizeof(unsigned)))) return bail(rc);
+        f.first_tab = f.units + nunits;
     }
     if ((rc = dev_alloc(v, (void**)&v->rcp_table_d, kRcpTable * sizeof(float)))) return bail(rc);
     {

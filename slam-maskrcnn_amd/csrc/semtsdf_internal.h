@@ -16,6 +16,7 @@ constexpr int kZAlign = 32;      // stored z planes per x,y column: a multiple o
 #endif
 constexpr int kBrickDistCap = SEMTSDF_BRICK_DIST_CAP;  // brick distance map: radius of the largest skip box (bricks)
 constexpr int kListSegs = 64;    // segments (and counters) of the live-unit list
+constexpr unsigned kPreWaves = 65534;  // k_integrate reads entries 2w+1 (+4) ahead for waves w < kPreWaves
 constexpr int kListCountStride = 64;  // counters 256 B apart (separate memory channels)
 #ifndef SEMTSDF_DYN_SUB
 #define SEMTSDF_DYN_SUB 8
@@ -164,6 +165,9 @@ struct IntegrateArgs {
                                    // pixel records carry the frame's raw labels; nullptr: none
     uint8_t* relabel_mask;         // the frame's mask, relabelled in place through lut by the kernel (nullable)
     const IntegrateRare* rare;     // rare-path fields (device memory)
+    unsigned* first_tab;           // XCD split: entries of each wave's first group of its first list, two per
+                                   // wave slot, written by k_compact_lists for first_nwaves persistent waves
+    unsigned first_nwaves;         // integrate_pre_waves(): the integrate reads the table only at this grid
 };
 constexpr int kWaveTraceWords = 8;
 
@@ -347,6 +351,7 @@ uint64_t unit_list_capacity(const VolGeom& g);
 int unit_grid_fits(int dimx, int dimy, int local_z);  // list entries (pack_unit) hold the unit grid
 hipError_t launch_cull(const IntegrateArgs& a, hipStream_t s);       // per-unit cull flags
 hipError_t launch_compact_lists(const IntegrateArgs& a, hipStream_t s);  // segments -> a.units
+unsigned integrate_pre_waves();  // persistent waves of the bench-mode integrate (first-group table size)
 hipError_t launch_tables_init(AssocTables* t, hipStream_t s);  // zero sums, first_px = UINT_MAX
 hipError_t launch_mask_stats(const uint8_t* mask, int npx, AssocTables* t, hipStream_t s);
 hipError_t launch_assoc_march(const AssocArgs& a, hipStream_t s);

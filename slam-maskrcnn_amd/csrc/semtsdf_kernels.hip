@@ -986,6 +986,9 @@ hipError_t launch_cull(const IntegrateArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+#ifndef SEMTSDF_XCD_SPLIT
+#define SEMTSDF_XCD_SPLIT 1  // each XCD's waves take a contiguous eighth of every list (list_view)
+#endif
 // The cull's segments compacted into one array: list l at an even base (so a group's two entries are
 // one 8-byte scalar load), followed by a ~0u pad (the second entry of a list's last group when
 // its count is odd), bases and totals after the dynamic counters of list_count.  One wave per
@@ -995,7 +998,9 @@ hipError_t launch_cull(const IntegrateArgs& a, hipStream_t s) {
 // at its start) and decodes no segment per entry.
 __global__ __launch_bounds__(256) void k_compact_lists(unsigned* __restrict__ list_count,
                                                        const unsigned* __restrict__ seg_list, unsigned seg_cap,
-                                                       unsigned* __restrict__ units) {
+                                                       unsigned* __restrict__ units, unsigned* __restrict__ first_tab,
+                                                       unsigned nwaves, unsigned first_list) {
+    __shared__ unsigned s_incl[64];
     // every wave of the workgroup computes the (tiny) prefix itself; all 256 lanes copy
     const unsigned lane = threadIdx.x & 63u, seg = blockIdx.x, l = blockIdx.y;
     unsigned c[kLists], tot[kLists];
@@ -1037,6 +1042,34 @@ __global__ __launch_bounds__(256) void k_compact_lists(unsigned* __restrict__ li
         for (int k = 0; k < 4; ++k)
             if (i0 + 256u * k < n) dst[i0 + 256u * k] = e[k];
     }
+    if (SEMTSDF_XCD_SPLIT && l == first_list && nwaves) {
+        // the first-group table of the XCD split (k_integrate, list_view): wave slot w (workgroup w / 4,
+        // XCD xi = workgroup % 8, index wx among the XCD's waves) starts at group lo(xi) + wx of the list;
+        // its two entries are read here from the cull's segments (the compacted array is being written
+        // by the other workgroups), the segment found by a binary search over the inclusive prefix
+        if (threadIdx.x < 64u) s_incl[threadIdx.x] = incl;
+        __syncthreads();
+        const unsigned w = seg * 256u + threadIdx.x;
+        const unsigned tl = tot[0] * (l == 0u) + tot[1] * (l == 1u) + tot[2] * (l == 2u);
+        const unsigned ng = (tl + 1u) / 2u, nwx = nwaves / 8u;
+        const unsigned blk = w >> 2, xi = blk & 7u, wx = (blk >> 3) * 4u + (w & 3u);
+        const unsigned g = ng * xi / 8u + wx;
+        if (w < nwaves && w < kPreWaves && wx < nwx && g < ng * (xi + 1u) / 8u) {
+            unsigned ev[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const unsigned idx = 2u * g + (unsigned)k;
+                unsigned j = 0;  // first segment whose inclusive prefix exceeds idx
+#pragma unroll
+                for (unsigned step = 32u; step; step >>= 1)
+                    if (s_incl[j + step - 1u] <= idx) j += step;
+                const unsigned before = j ? s_incl[j - 1u] : 0u;
+                ev[k] = idx < tl ? seg_list[((size_t)l * kListSegs + j) * seg_cap + (idx - before)] : ~0u;
+            }
+            first_tab[2u * w] = ev[0];
+            first_tab[2u * w + 1u] = ev[1];
+        }
+    }
     if (seg == 0u && l == 0u && threadIdx.x < (unsigned)kLists) {
         unsigned b = base[0], t = tot[0];
 #pragma unroll
@@ -1056,8 +1089,10 @@ hipError_t launch_compact_lists(const IntegrateArgs& a, hipStream_t s) {
     if (ug.n == 0) {  // a shard that owns no chunk: empty lists
         return hipMemsetAsync(a.list_count + kListTotalsWord, 0, 8 * sizeof(unsigned), s);
     }
+    // the first-group table for the list the integrate starts with: free units in the gated modes
+    const unsigned first_list = ((a.flags & 0x2u) && !(a.flags & 0x8u)) ? 1u : 0u;
     hipLaunchKernelGGL(k_compact_lists, dim3(kListSegs, kLists), dim3(256), 0, s, a.list_count, a.unit_list,
-                       list_seg_cap(ug), a.units);
+                       list_seg_cap(ug), a.units, a.first_tab, a.first_nwaves, first_list);
     return hipGetLastError();
 }
 
@@ -1504,6 +1539,9 @@ __device__ __forceinline__ void st_state(void* p, const T& v) {
     *reinterpret_cast<T*>(p) = v;
 }
 
+#ifndef SEMTSDF_DUMMY0
+#define SEMTSDF_DUMMY0 1  // the dummy address of a lane with nothing to load: 1 the array's start, 0 its unit's first line
+#endif
 // Unconditional loads: a lane with nothing to load reads the dummy line (one 16-B vector
 // shared by all such lanes), so the issue count is the same on every path.
 template <bool SEM, bool CI32, bool VOTE, bool FREE>
@@ -1533,12 +1571,22 @@ __device__ __forceinline__ void stage_load(const IntegrateArgs& a, const UnitPos
                       tile_line_all((C.sflag != 0u) & (C.sflag < kFlagMax) & fone & (C.tmask == 15u));
     L.skip = skip;
     L.lazy = lazy;
-    L.s4 = ld_state<float4>(a.b.sdf + (skip ? 0u : ub + lt));
-    L.w4 = ld_state<int4>(a.b.wt + (lazy ? 0u : ub + lt));
+    if (SEMTSDF_DUMMY0) {
+        // a lane with nothing to load reads the array's first vector, like a steady line: the line
+        // stays in L2, where the unit's first line (the other choice) is an extra line fetched
+        // whenever that line itself has no update
+        L.s4 = ld_state<float4>(a.b.sdf + ((skip | !t) ? 0u : v));
+        L.w4 = ld_state<int4>(a.b.wt + ((lazy | !t) ? 0u : v));
+    } else {
+        L.s4 = ld_state<float4>(a.b.sdf + (skip ? 0u : ub + lt));
+        L.w4 = ld_state<int4>(a.b.wt + (lazy ? 0u : ub + lt));
+    }
     if (FREE) return;  // sdf and weight only
     if (CI32) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) L.c32[k] = reinterpret_cast<const int4*>(a.b.color)[(uint64_t)ub + lg + (gt ? k : 0)];
+    } else if (SEMTSDF_DUMMY0) {
+        L.c8 = ld_state<uint4>(reinterpret_cast<const uint32_t*>(a.b.color) + (gt ? v : 0u));
     } else {
         L.c8 = ld_state<uint4>(reinterpret_cast<const uint32_t*>(a.b.color) + ub + lg);
     }
@@ -1810,20 +1858,30 @@ __device__ __forceinline__ void stage_store(const IntegrateArgs& a, const UnitPo
 // entries, one unit per slot, of the list's compact array (k_compact_lists).
 struct ListView {
     const unsigned* list;      // the list's first entry
-    unsigned total, ngroups;   // wave-uniform
+    unsigned total, ngroups;   // wave-uniform; ngroups: end of the wave's range of groups
+    unsigned cnt;              // groups in the wave's range (XCD split: its XCD's range)
     unsigned i;                // the wave's current group
 };
 
-// List l of the frame (base and total written by k_compact_lists; scalar loads).
+// List l of the frame (base and total written by k_compact_lists; scalar loads).  XCD split
+// (nsp == 8): the list's groups are cut into 8 contiguous ranges, range x taken by the waves of
+// XCD x (workgroups b with b % 8 == x; the dispatcher deals workgroups to the XCDs round-robin),
+// round-robin among them (wave index wave within the XCD, nwaves of them): a range is a compact
+// region of the volume (the cull's segments are y-bands), so each XCD's L2 holds the pixel records
+// and steady flags of its own region instead of every XCD fetching all of them.  ngroups is then
+// the range's end and cnt its length.
 __device__ __forceinline__ ListView list_view(const unsigned* units, const unsigned* list_count, int l, unsigned wave,
-                                              unsigned nwaves, unsigned rot) {
+                                              unsigned nwaves, unsigned rot, unsigned xi = 0u, unsigned nsp = 1u) {
     const __attribute__((address_space(4))) unsigned* tw =
         (const __attribute__((address_space(4))) unsigned*)(list_count + kListTotalsWord);
     ListView v;
     v.list = units + tw[2 * l];
     v.total = tw[2 * l + 1];
-    v.ngroups = (v.total + kSlots - 1) / kSlots;
-    v.i = (wave + nwaves - rot % nwaves) % nwaves;
+    const unsigned ng = (v.total + kSlots - 1) / kSlots;
+    const unsigned lo = nsp == 1u ? 0u : ng * xi / nsp;  // ng < 2^28 (list entries pack 32-bit unit ids)
+    v.ngroups = nsp == 1u ? ng : ng * (xi + 1u) / nsp;
+    v.cnt = v.ngroups - lo;
+    v.i = lo + (wave + nwaves - rot % nwaves) % nwaves;
     return v;
 }
 
@@ -2110,6 +2168,8 @@ __device__ __forceinline__ void integrate_tail(const IntegrateArgs& a, const Uni
 // pipeline chained from each list into the next.  A static round-robin share: dynamic
 // schedules (per-XCD device atomics, a whole-CU workgroup sharing an LDS queue) evened the
 // waves' end times but ran slower.
+static_assert(!SEMTSDF_XCD_SPLIT || (!SEMTSDF_DYN_LAST && !SEMTSDF_TAIL_PCT),
+              "the dynamic schedules hand out the whole list (no XCD ranges)");
 #ifndef SEMTSDF_INTEGRATE_WPE
 #define SEMTSDF_INTEGRATE_WPE 4  // waves per SIMD the register allocation targets (5 spills; measured equal)
 #endif
@@ -2148,29 +2208,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
     const unsigned* lst = a.units;
     unsigned n0;
     unsigned rot0 = 0;
+    // XCD split (list_view): the wave's XCD xi and its index wx among the XCD's nwx waves
+    const bool split = SEMTSDF_XCD_SPLIT && (gridDim.x & 7u) == 0u;
+    const unsigned nsp = split ? 8u : 1u, xi = split ? blockIdx.x & 7u : 0u;
+    const unsigned wx = split ? __builtin_amdgcn_readfirstlane((blockIdx.x >> 3) * (blockDim.x >> 6) + (threadIdx.x >> 6))
+                              : wave;
+    const unsigned nwx = nwaves / nsp;
     if (GATE && !VOTE) {  // free units exist only in gated modes (free_ok): full free, free, general
         // the free list lies at the start of the compact array and its groups start at the wave's
         // own index: the wave's first free group is read before the lists' totals have arrived
         // (one dependent load less at the start of the kernel; most waves prime a free group)
         const __attribute__((address_space(4))) unsigned* u4 = (const __attribute__((address_space(4))) unsigned*)lst;
-        const unsigned pre1[2] = {u4[2u * wave], u4[2u * wave + 1u]};
-        ListView vf = list_view(lst, cnt, 2, wave, nwaves, 0u);
-        ListView v1 = list_view(lst, cnt, 1, wave, nwaves, 0u);
-        rot0 = (vf.ngroups + v1.ngroups) % nwaves;
-        ListView v0 = list_view(lst, cnt, 0, wave, nwaves, rot0);
+        // (the array holds at least 2 x 65536 entries, semtsdf_api.cpp: waves past kPreWaves read their
+        // first group the ordinary way)
+        // XCD split: the wave's first free group from the table k_compact_lists wrote for this grid
+        const bool tab = split && a.first_nwaves == nwaves;
+        const unsigned wq = min(wave, kPreWaves - 1u);
+        const __attribute__((address_space(4))) unsigned* t4 =
+            tab ? (const __attribute__((address_space(4))) unsigned*)a.first_tab : u4;
+        const unsigned pre1[2] = {t4[2u * wq], t4[2u * wq + 1u]};
+        ListView vf = list_view(lst, cnt, 2, wx, nwx, 0u, xi, nsp);
+        ListView v1 = list_view(lst, cnt, 1, wx, nwx, 0u, xi, nsp);
+        rot0 = (vf.cnt + v1.cnt) % nwx;
+        ListView v0 = list_view(lst, cnt, 0, wx, nwx, rot0, xi, nsp);
         const unsigned tail0 = SEMTSDF_TAIL_PCT ? v0.ngroups * SEMTSDF_TAIL_PCT / 100u : 0u;
         v0.ngroups -= tail0;  // the static share: groups 0 .. ngroups - tail0 - 1
         if (vf.i < vf.ngroups)
             list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 2>(a, ug, seg_cap, vf, S, n);
         else if (v1.i < v1.ngroups)
-            list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 1>(a, ug, seg_cap, v1, S, n, pre1);
+            list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 1>(a, ug, seg_cap, v1, S, n,
+                                                                   (!split || tab) && wq == wave ? pre1 : nullptr);
         else if (v0.i < v0.ngroups)
             list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0>(a, ug, seg_cap, v0, S, n);
         __syncthreads();
         if (SEMTSDF_WAVE_TRACE) tr[1] = tr[2] = tr[3] = wall_clock64();
-        integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 2, 1>(a, ug, seg_cap, s_rcp, vf, &v1, nwaves, S, n);
+        integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 2, 1>(a, ug, seg_cap, s_rcp, vf, &v1, nwx, S, n);
         if (SEMTSDF_WAVE_TRACE) tr[2] = wall_clock64();
-        integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 1, 0>(a, ug, seg_cap, s_rcp, v1, &v0, nwaves, S, n);
+        integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 1, 0>(a, ug, seg_cap, s_rcp, v1, &v0, nwx, S, n);
         if (SEMTSDF_WAVE_TRACE) {
             tr[3] = wall_clock64();
             trn = groups_of(vf.total, 0u) | (groups_of(v1.total, 0u) << 20);
@@ -2178,7 +2252,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
         if (SEMTSDF_DYN_LAST)
             integrate_list_dyn<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>(a, ug, seg_cap, s_rcp, v0, nwaves, tail_counter, S, n);
         else
-            integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0, -1>(a, ug, seg_cap, s_rcp, v0, nullptr, nwaves, S, n);
+            integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0, -1>(a, ug, seg_cap, s_rcp, v0, nullptr, nwx, S, n);
         if (tail0) integrate_tail<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>(a, ug, seg_cap, s_rcp, v0, v0.ngroups, tail0,
                                                                            tail_counter, S, n);
         n0 = v0.total;
@@ -2192,19 +2266,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
         // starts at entry 4 of the compact array (k_compact_lists), so the wave's first group is
         // read before the totals arrive (used when the base is indeed 4)
         const __attribute__((address_space(4))) unsigned* u4 = (const __attribute__((address_space(4))) unsigned*)lst;
-        const unsigned pre0[2] = {u4[4u + 2u * wave], u4[5u + 2u * wave]};
-        ListView v0 = list_view(lst, cnt, 0, wave, nwaves, 0u);
+        const bool tab = split && a.first_nwaves == nwaves;
+        const unsigned wq = min(wave, kPreWaves - 1u);
+        const __attribute__((address_space(4))) unsigned* t4 =
+            tab ? (const __attribute__((address_space(4))) unsigned*)a.first_tab - 4 : u4;
+        const unsigned pre0[2] = {t4[4u + 2u * wq], t4[5u + 2u * wq]};
+        ListView v0 = list_view(lst, cnt, 0, wx, nwx, 0u, xi, nsp);
         const unsigned tail0 = SEMTSDF_TAIL_PCT ? v0.ngroups * SEMTSDF_TAIL_PCT / 100u : 0u;
         v0.ngroups -= tail0;
         if (v0.i < v0.ngroups)
             list_prime<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0>(a, ug, seg_cap, v0, S, n,
-                                                                   v0.list == lst + 4 ? pre0 : nullptr);
+                                                                   (tab || (!split && v0.list == lst + 4)) && wq == wave ? pre0
+                                                                                                                : nullptr);
         __syncthreads();
         if (SEMTSDF_WAVE_TRACE) tr[1] = tr[2] = tr[3] = wall_clock64();
         if (SEMTSDF_DYN_LAST)
             integrate_list_dyn<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>(a, ug, seg_cap, s_rcp, v0, nwaves, tail_counter, S, n);
         else
-            integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0, -1>(a, ug, seg_cap, s_rcp, v0, nullptr, nwaves, S, n);
+            integrate_list<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN, 0, -1>(a, ug, seg_cap, s_rcp, v0, nullptr, nwx, S, n);
         if (tail0) integrate_tail<SEM, GATE, CI32, VOTE, COUNT, SHARD, PIN>(a, ug, seg_cap, s_rcp, v0, v0.ngroups, tail0,
                                                                            tail_counter, S, n);
         n0 = v0.total;
@@ -2316,6 +2395,13 @@ static hipError_t launch_integrate_t(const IntegrateArgs& a, bool count, hipStre
     }
     if (pin) return launch_integrate_k<SEM, GATE, CI32, VOTE, false, false, true>(a, s, e0, e1);
     return launch_integrate_k<SEM, GATE, CI32, VOTE, false, false, false>(a, s, e0, e1);
+}
+
+unsigned integrate_pre_waves() {
+    // the SfM semantic instantiation (the others run at the same occupancy; where one does not, its
+    // waves read their first group the ordinary way: k_integrate compares first_nwaves with its grid)
+    static const unsigned w = 4u * resident_grid(k_integrate<true, true, false, false, false, false, true>, 256);
+    return w;
 }
 
 hipError_t launch_integrate(const IntegrateArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
