@@ -986,6 +986,9 @@ hipError_t launch_cull(const IntegrateArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+#ifndef SEMTSDF_TAIL_CULL_PROBE
+#define SEMTSDF_TAIL_CULL_PROBE 0  // instrumentation build: a whole-grid unit cull in the integrate's tail
+#endif
 #ifndef SEMTSDF_XCD_SPLIT
 #define SEMTSDF_XCD_SPLIT 1  // each XCD's waves take a contiguous eighth of every list (list_view)
 #endif
@@ -2288,6 +2291,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VOTE ? 3 : 
                                                                            tail_counter, S, n);
         n0 = v0.total;
     }
+#if SEMTSDF_TAIL_CULL_PROBE
+    {  // timing probe (instrumentation builds only): a unit cull of the whole grid as tail work,
+       // tasks of 64 units claimed through the XCD's own counter (zeroed by the prepass); results discarded
+        const unsigned xcc = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11))) & 7u;
+        unsigned* ctr = tail_counter + xcc * kListCountStride;
+        const unsigned ntask = (ug.n + 63u) / 64u;
+        const unsigned nmine = ntask > xcc ? (ntask - xcc + 7u) / 8u : 0u;
+        unsigned acc = 0;
+        for (;;) {
+            unsigned t = 0;
+            if (lane == 0) t = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            t = (unsigned)__builtin_amdgcn_readfirstlane((int)t);
+            if (t >= nmine) break;
+            const unsigned u = (t * 8u + xcc) * 64u + (unsigned)lane;
+            if (u < ug.n) {
+                const unsigned ux = u % ug.nux, r = u / ug.nux, uy = r % ug.nuy, uz = r / ug.nuy;
+                acc += (unsigned)unit_cull(a, (int)ux * UX, (int)uy * UY, (int)uz * UZ);
+            }
+        }
+        if (acc == 0xFFFFFFFFu) a.counters[7] = acc;  // keeps the work live
+    }
+#endif
     if (SEM && a.lut && a.relabel_mask) {  // the frame's mask through the same table, in place
         const unsigned npx = (unsigned)(a.width * a.height);
         const unsigned gid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
