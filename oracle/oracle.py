@@ -351,3 +351,43 @@ def masks_to_labels(masks, min_area=2000):
     first = mk.argmax(axis=2)
     out[any_] = (order[first[any_]] + 1).astype(np.uint8)
     return out, int(kept.size)
+
+
+def non_max_suppression(boxes, scores, threshold):
+    """Greedy NMS, Mask_RCNN/mrcnn/utils.py:116-150 (with compute_iou utils.py:58-76), in f32: indices of
+    the kept boxes, highest score first (a restatement for the tests; the product runs the HIP kernels
+    of libsemtsdf_det.so)."""
+    boxes = np.asarray(boxes, dtype=np.float32)
+    scores = np.asarray(scores)
+    y1, x1, y2, x2 = boxes[:, 0], boxes[:, 1], boxes[:, 2], boxes[:, 3]
+    area = (y2 - y1) * (x2 - x1)
+    ixs = scores.argsort(kind="stable")[::-1]
+    pick = []
+    while len(ixs) > 0:
+        i = ixs[0]
+        pick.append(i)
+        rest = ixs[1:]
+        yy1 = np.maximum(y1[i], y1[rest])
+        yy2 = np.minimum(y2[i], y2[rest])
+        xx1 = np.maximum(x1[i], x1[rest])
+        xx2 = np.minimum(x2[i], x2[rest])
+        inter = np.maximum(xx2 - xx1, np.float32(0)) * np.maximum(yy2 - yy1, np.float32(0))
+        with np.errstate(invalid="ignore", divide="ignore"):
+            iou = inter / (area[i] + area[rest] - inter)
+        ixs = np.delete(ixs, np.where(iou > threshold)[0] + 1)
+        ixs = np.delete(ixs, 0)
+    return np.array(pick, dtype=np.int32)
+
+
+def nms_sorted_cpu(boxes, iou_threshold, max_out):
+    """The product's nms_sorted contract (boxes sorted by descending score; keep [max_out] with -1
+    past the count, count [1]) on CPU torch tensors, from non_max_suppression above: for CPU tests of
+    the detector graph."""
+    import torch
+
+    b = boxes.detach().float().cpu().numpy()
+    n = b.shape[0]
+    pick = non_max_suppression(b, -np.arange(n, dtype=np.float64), iou_threshold)[:max_out] if n else np.zeros(0, np.int32)
+    keep = np.full(max(max_out, 1), -1, np.int32)
+    keep[:len(pick)] = pick
+    return torch.from_numpy(keep[:max_out]), torch.tensor([len(pick)], dtype=torch.int32)

@@ -97,3 +97,24 @@ def test_params_validation_without_a_device():
         h = C.c_void_p()
         rc = lib.semtsdf_create(C.byref(p), 0, C.byref(h))
         assert rc == L.ERR_INVALID and b"prior_mrcnn_err_rate" in lib.semtsdf_last_error(), bad
+
+
+def test_detector_library_exports_every_symbol():
+    """include/semtsdf_det.h (the Mask R-CNN producer's NMS, libsemtsdf_det.so): every declared symbol
+    exported; argument errors refused without touching a device."""
+    import ctypes as C
+
+    with open(os.path.join(ROOT, "include", "semtsdf_det.h")) as f:
+        txt = re.sub(r"/\*.*?\*/", "", f.read(), flags=re.S)
+    names = sorted(set(re.findall(r"\b(semtsdf_det_[a-z0-9_]+)\s*\(", txt)))
+    assert names == ["semtsdf_det_abi_version", "semtsdf_det_nms", "semtsdf_det_nms_workspace"]
+    lib = C.CDLL(os.path.join(ROOT, "slam-maskrcnn_amd", "semtsdf", "libsemtsdf_det.so"))
+    for n in names:
+        assert hasattr(lib, n), n
+    assert lib.semtsdf_det_abi_version() == 1
+    lib.semtsdf_det_nms_workspace.restype = C.c_size_t
+    assert lib.semtsdf_det_nms_workspace(6000) == 6000 * 94 * 8
+    lib.semtsdf_det_nms.argtypes = [C.c_void_p, C.c_int, C.c_float, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                    C.c_void_p]
+    assert lib.semtsdf_det_nms(None, 16385, 0.5, 10, None, None, None, None) == 1  # too many boxes, NULLs
+    assert lib.semtsdf_det_nms(None, -1, 0.5, 10, None, None, None, None) == 1

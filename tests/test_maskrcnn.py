@@ -1,0 +1,150 @@
+"""Mask R-CNN producer: semtsdf/maskrcnn.py and libsemtsdf_det.so.
+
+CPU: the box arithmetic and anchors against golden vectors of the reference's own mrcnn/utils.py
+(executed in this container by tests/golden/gen_mrcnn_utils.py), the oracle's NMS against the
+reference's non_max_suppression, and the detector graph end to end on a small configuration with the
+oracle NMS (the product refuses to run its NMS off the GPU).  GPU: the HIP NMS against the reference
+rule, and detect() on a 640x480 frame at the reference's configuration (ResNet-101-FPN, 1024x1024),
+its output contract and the labels semtsdf_masks_to_labels makes of it.  The weights are seeded random
+(no COCO checkpoint offline): detections are checked for their contract, not their content."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "slam-maskrcnn_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import oracle as O  # noqa: E402
+
+torch = pytest.importorskip("torch")
+from semtsdf import maskrcnn as MR  # noqa: E402
+
+G = np.load(os.path.join(ROOT, "tests", "golden", "mrcnn_utils_golden.npz"))
+
+
+@pytest.mark.parametrize("S", [1024, 256])
+def test_anchors_equal_reference(S):
+    strides = [4, 8, 16, 32, 64]
+    shapes = [(int(np.ceil(S / s)), int(np.ceil(S / s))) for s in strides]
+    a = MR.generate_pyramid_anchors((32, 64, 128, 256, 512), (0.5, 1, 2), shapes, strides, 1)
+    assert a.shape[0] == int(G[f"anchors_{S}_count"])
+    np.testing.assert_array_equal(a[::37], G[f"anchors_{S}_every37"])
+    np.testing.assert_array_equal(a.sum(axis=0), G[f"anchors_{S}_sum"])
+    an = MR.norm_boxes(a, (S, S))
+    np.testing.assert_array_equal(an[::37], G[f"anchors_norm_{S}_every37"])
+    np.testing.assert_array_equal(an.astype(np.float64).sum(axis=0), G[f"anchors_norm_{S}_sum"])
+
+
+def test_box_deltas_equal_reference():
+    got = MR.apply_box_deltas(torch.from_numpy(G["delta_boxes"]), torch.from_numpy(G["deltas"])).numpy()
+    # torch and NumPy f32 exp differ in the last ulp on some inputs
+    np.testing.assert_allclose(got, G["applied"], rtol=2e-6, atol=2e-7)
+
+
+@pytest.mark.parametrize("case", range(6))
+def test_oracle_nms_equals_reference(case):
+    b, s = G[f"nms{case}_boxes"], G[f"nms{case}_scores"]
+    for t in (0.3, 0.5, 0.7):
+        np.testing.assert_array_equal(O.non_max_suppression(b, s, t), G[f"nms{case}_keep_{t}"])
+
+
+def _small_config():
+    return MR.Config(IMAGE_MIN_DIM=192, IMAGE_MAX_DIM=256, PRE_NMS_LIMIT=1000, POST_NMS_ROIS_INFERENCE=200,
+                     DTYPE=torch.float32, BACKBONE="resnet50")
+
+
+def _check_contract(out, H, W, cfg):
+    rois, cls, sc, m = out["rois"], out["class_ids"], out["scores"], out["masks"]
+    n = int(rois.shape[0])
+    assert cls.shape == (n,) and sc.shape == (n,) and tuple(m.shape) == (H, W, n)
+    assert m.dtype == torch.uint8 and rois.dtype == torch.int32
+    assert n <= cfg.DETECTION_MAX_INSTANCES
+    r, c, s, mm = rois.cpu().numpy(), cls.cpu().numpy(), sc.float().cpu().numpy(), m.cpu().numpy()
+    assert ((c >= 1) & (c < cfg.NUM_CLASSES)).all()
+    assert (s >= cfg.DETECTION_MIN_CONFIDENCE).all() and (np.diff(s) <= 0).all()
+    assert ((r[:, 2] - r[:, 0]) * (r[:, 3] - r[:, 1]) > 0).all()
+    assert set(np.unique(mm)) <= {0, 1}
+    for k in range(n):  # a mask lies inside its box (unmold_mask pastes it at the box)
+        y1, x1, y2, x2 = r[k]
+        outside = mm[:, :, k].copy()
+        outside[max(y1, 0):max(y2, 0), max(x1, 0):max(x2, 0)] = 0
+        assert outside.sum() == 0
+    return n
+
+
+def test_detector_graph_cpu_contract_and_determinism():
+    cfg = _small_config()
+    img = torch.from_numpy(np.random.default_rng(0).integers(0, 256, (120, 160, 3), dtype=np.uint8))
+    a = MR.MaskRCNN(cfg, seed=0, nms=O.nms_sorted_cpu).eval().detect(img)
+    b = MR.MaskRCNN(cfg, seed=0, nms=O.nms_sorted_cpu).eval().detect(img)
+    n = _check_contract(a, 120, 160, cfg)
+    assert n > 0
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+
+
+def test_product_nms_refuses_cpu_tensors():
+    with pytest.raises(RuntimeError):
+        MR.nms_sorted(torch.zeros((4, 4)), 0.5, 4)
+
+
+@pytest.mark.gpu
+def test_hip_nms_equals_reference_rule():
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(3)
+    cases = [(G[f"nms{c}_boxes"], G[f"nms{c}_scores"]) for c in range(6)]
+    for n in (1, 63, 64, 65, 4097, 6000):  # block edges, the RPN's pre-NMS size
+        ctr = rng.uniform(0, 1, (max(n // 12, 1), 2))
+        k = rng.integers(0, ctr.shape[0], n)
+        cy, cx = ctr[k, 0] + rng.normal(0, 0.03, n), ctr[k, 1] + rng.normal(0, 0.03, n)
+        h, w = rng.uniform(0.01, 0.25, n), rng.uniform(0.01, 0.25, n)
+        cases.append((np.stack([cy - h / 2, cx - w / 2, cy + h / 2, cx + w / 2], 1).astype(np.float32),
+                      rng.uniform(0, 1, n).astype(np.float32)))
+    for b, s in cases:
+        order = np.argsort(-s, kind="stable")
+        bs = b[order]
+        for t in (0.3, 0.5, 0.7):
+            ref = O.non_max_suppression(bs, -np.arange(len(bs), dtype=np.float64), t)
+            for max_out in (len(bs), 100, 7):
+                keep, count = MR.nms_sorted(torch.from_numpy(bs).to(dev), t, max_out)
+                kn, cn = keep.cpu().numpy(), int(count.cpu()[0])
+                want = ref[:max_out]
+                assert cn == len(want), (len(bs), t, max_out)
+                np.testing.assert_array_equal(kn[:cn], want)
+                assert (kn[cn:] == -1).all()
+
+
+@pytest.mark.gpu
+def test_detect_on_device_reference_configuration():
+    from semtsdf.masks import masks_to_labels_dev
+    from semtsdf.synth import SyntheticStream
+
+    dev = torch.device("cuda", 0)
+    fr = SyntheticStream(seed=1, noise=True).frame(0)
+    img = torch.from_numpy(fr.rgb).to(dev)
+    cfg = MR.Config()
+    m = MR.MaskRCNN(cfg, seed=0).to(dev).to(cfg.DTYPE).eval()
+    a = m.detect(img)
+    n = _check_contract(a, 480, 640, cfg)
+    assert n > 0
+    # MIOpen's bf16 convolutions are not bit-reproducible from call to call: a second frame keeps the
+    # contract and nearly the same detections
+    b = m.detect(img)
+    nb = _check_contract(b, 480, 640, cfg)
+    assert abs(nb - n) <= max(2, n // 5)
+    # the fixed-row form a producer stream uses: the same detections first, then empty rows
+    c = m.detect(img, compact=False)
+    assert tuple(c["masks"].shape) == (480, 640, cfg.DETECTION_MAX_INSTANCES)
+    z = c["class_ids"] == 0  # rows past the detections (and zero-area ones): class 0, empty mask
+    nc = int((~z).sum())
+    assert abs(nc - n) <= max(2, n // 5) and int(c["masks"][:, :, z].sum()) == 0
+    # the producer contract of dmask.py: masks [H, W, N] -> u8 labels on the device
+    labels = torch.zeros(480 * 640, dtype=torch.uint8, device=dev)
+    kept = masks_to_labels_dev(a["masks"].data_ptr(), 640, 480, n, labels.data_ptr(),
+                               stream=torch.cuda.current_stream(dev).cuda_stream, want_count=True)
+    want, want_kept = O.masks_to_labels(a["masks"].cpu().numpy())
+    assert kept == want_kept
+    np.testing.assert_array_equal(labels.cpu().numpy().reshape(480, 640), want)

@@ -1,0 +1,37 @@
+"""Probe (not part of the product): Mask R-CNN producer time per frame under MIOpen settings.
+Usage: python tools/det_probe.py {cl|nchw} {bench0|bench1} [fp32]"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "slam-maskrcnn_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from semtsdf import maskrcnn as MR  # noqa: E402
+from semtsdf.synth import SyntheticStream  # noqa: E402
+
+layout, bench = sys.argv[1], sys.argv[2]
+fp32 = len(sys.argv) > 3
+torch.backends.cudnn.benchmark = bench == "bench1"
+dev = torch.device("cuda", 0)
+img = torch.from_numpy(SyntheticStream(seed=1, noise=True).frame(0).rgb).to(dev)
+cfg = MR.Config(DTYPE=torch.float32 if fp32 else torch.bfloat16)
+m = MR.MaskRCNN(cfg, seed=0).to(dev).to(cfg.DTYPE).eval()
+if layout == "nchw":
+    MR.CHANNELS_LAST = False
+t0 = time.perf_counter()
+m.detect(img, compact=False)
+torch.cuda.synchronize()
+t1 = time.perf_counter()
+for _ in range(3):
+    m.detect(img, compact=False)
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+for _ in range(10):
+    m.detect(img, compact=False)
+e1.record()
+e1.synchronize()
+print(f"{layout} {bench} {'fp32' if fp32 else 'bf16'}: first call {t1 - t0:.1f} s, {e0.elapsed_time(e1) / 10:.2f} ms per detect", flush=True)
