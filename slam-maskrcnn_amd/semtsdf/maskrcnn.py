@@ -216,6 +216,7 @@ class MaskRCNN(nn.Module):
         self.mask_out = _conv(256, nc, 1)
         self._init(seed)
         self._anchors = {}
+        self._consts = {}
 
     @torch.no_grad()
     def _init(self, seed):
@@ -292,6 +293,14 @@ class MaskRCNN(nn.Module):
         # dmask.py area rule (> 2000 px) and the fusion sees instances
         self.mask_out.bias.add_(2.0)
 
+    def _const(self, name, values, device):
+        """Small constant tensors made once per device (no host-to-device copy inside a graph capture)."""
+        key = (name, tuple(values), str(device))
+        c = self._consts.get(key)
+        if c is None:
+            c = self._consts[key] = torch.tensor(values, dtype=torch.float32, device=device)
+        return c
+
     # ---- stages of the graph
     def backbone(self, x):
         x = F.relu(self.conv1(x))
@@ -335,7 +344,7 @@ class MaskRCNN(nn.Module):
         scores = torch.softmax(logits, dim=1)[:, 1]
         k = min(cfg.PRE_NMS_LIMIT, scores.shape[0])
         top, ix = torch.topk(scores, k, sorted=True)
-        d = deltas[ix] * torch.tensor(cfg.RPN_BBOX_STD_DEV, device=deltas.device)
+        d = deltas[ix] * self._const("rpn_std", cfg.RPN_BBOX_STD_DEV, deltas.device)
         boxes = clip_boxes(apply_box_deltas(anchors[ix], d), (0.0, 0.0, 1.0, 1.0))
         keep, count = self._nms(boxes, cfg.RPN_NMS_THRESHOLD, cfg.POST_NMS_ROIS_INFERENCE)
         valid = keep >= 0
@@ -357,11 +366,9 @@ class MaskRCNN(nn.Module):
         for L in range(2, 6):
             fm = feats[L - 2]
             H, W = fm.shape[2], fm.shape[3]
-            sel = (lvl == L).nonzero(as_tuple=True)[0]
-            m = int(sel.numel())
-            if m == 0:
-                continue
-            b = rois[sel]
+            # every roi sampled on every level and the level's samples kept (static shapes: no host
+            # synchronisation, so a whole detect() can be captured in a HIP graph)
+            b = rois
             # crop_and_resize sample positions: y = y1 (H - 1) + i (y2 - y1) (H - 1) / (pool - 1)
             ys = b[:, 0:1] * (H - 1) + i[None, :] * ((b[:, 2:3] - b[:, 0:1]) * (H - 1) / (pool - 1))
             xs = b[:, 1:2] * (W - 1) + i[None, :] * ((b[:, 3:4] - b[:, 1:2]) * (W - 1) / (pool - 1))
@@ -369,11 +376,12 @@ class MaskRCNN(nn.Module):
             gx = xs / (W - 1) * 2 - 1
             grid = torch.stack([gx[:, None, :].expand(-1, pool, -1), gy[:, :, None].expand(-1, -1, pool)], dim=-1)
             # one batch: every roi's pool x pool samples as rows of a single grid over the level's map
-            smp = F.grid_sample(fm.float(), grid.reshape(1, m * pool, pool, 2), mode="bilinear",
-                                padding_mode="zeros", align_corners=True)  # [1, C, m pool, pool]
-            smp = smp.view(Cn, m, pool, pool).permute(1, 0, 2, 3)
+            smp = F.grid_sample(fm.float(), grid.reshape(1, n * pool, pool, 2), mode="bilinear",
+                                padding_mode="zeros", align_corners=True)  # [1, C, n pool, pool]
+            smp = smp.view(Cn, n, pool, pool).permute(1, 0, 2, 3)
             inside = ((ys >= 0) & (ys <= H - 1))[:, :, None] & ((xs >= 0) & (xs <= W - 1))[:, None, :]
-            out[sel] = (smp * inside[:, None].to(smp.dtype)).to(out.dtype)
+            keep = inside[:, None] & (lvl == L)[:, None, None, None]
+            out = out + torch.where(keep, smp, torch.zeros((), device=smp.device)).to(out.dtype)
         return out
 
     def classifier(self, pooled):
@@ -388,8 +396,8 @@ class MaskRCNN(nn.Module):
         per-class NMS as one NMS over class-offset boxes (boxes of different classes never overlap)."""
         cfg = self.config
         score, cls = probs.max(dim=1)
-        d = deltas[torch.arange(deltas.shape[0], device=deltas.device), cls] * torch.tensor(cfg.BBOX_STD_DEV,
-                                                                                             device=deltas.device)
+        d = deltas[torch.arange(deltas.shape[0], device=deltas.device), cls] * self._const("bbox_std", cfg.BBOX_STD_DEV,
+                                                                                           deltas.device)
         refined = clip_boxes(apply_box_deltas(rois, d), window)
         ok = (cls > 0) & (score >= cfg.DETECTION_MIN_CONFIDENCE) & (rois.abs().sum(1) > 0)
         score_k = torch.where(ok, score, torch.full_like(score, -1.0))
@@ -425,7 +433,7 @@ class MaskRCNN(nn.Module):
         if scale != 1:
             x = F.interpolate(x, size=(nh, nw), mode="bilinear", align_corners=False)
         top, left = (cfg.IMAGE_MAX_DIM - nh) // 2, (cfg.IMAGE_MAX_DIM - nw) // 2
-        x = x - torch.tensor(cfg.MEAN_PIXEL, device=x.device)[None, :, None, None]
+        x = x - self._const("mean", cfg.MEAN_PIXEL, x.device)[None, :, None, None]
         x = F.pad(x, (left, cfg.IMAGE_MAX_DIM - nw - left, top, cfg.IMAGE_MAX_DIM - nh - top))
         return x, (top, left, nh + top, nw + left), scale
 
@@ -464,11 +472,11 @@ class MaskRCNN(nn.Module):
         n = int((det[:, 4] > 0).sum().item()) if compact else int(det.shape[0])
         d = det[:n]
         wy1, wx1, wy2, wx2 = (float(v) for v in nwin)
-        shift = torch.tensor([wy1, wx1, wy1, wx1], device=dev)
-        scale = torch.tensor([wy2 - wy1, wx2 - wx1, wy2 - wy1, wx2 - wx1], device=dev)
+        shift = self._const("shift", (wy1, wx1, wy1, wx1), dev)
+        scale = self._const("scale", (wy2 - wy1, wx2 - wx1, wy2 - wy1, wx2 - wx1), dev)
         b = (d[:, :4] - shift) / scale
-        px = torch.round(b * torch.tensor([H0 - 1, W0 - 1, H0 - 1, W0 - 1], device=dev)
-                         + torch.tensor([0, 0, 1, 1], device=dev)).to(torch.int32)
+        px = torch.round(b * self._const("den", (H0 - 1, W0 - 1, H0 - 1, W0 - 1), dev)
+                         + self._const("den_shift", (0, 0, 1, 1), dev)).to(torch.int32)
         cls = d[:, 4].long()
         ok = ((px[:, 2] - px[:, 0]) * (px[:, 3] - px[:, 1]) > 0) & (cls > 0)
         if compact:
@@ -497,3 +505,32 @@ class MaskRCNN(nn.Module):
         full = ((full >= 0.5) & inside).to(torch.uint8)
         return {"rois": px, "class_ids": cls.to(torch.int32), "scores": scores,
                 "masks": full.permute(1, 2, 0).contiguous()}
+
+
+class GraphDetector:
+    """`MaskRCNN.detect(compact=False)` for one image size captured in a HIP graph (torch.cuda.CUDAGraph:
+    the backbone's and heads' several hundred launches, the NMS kernels and the unmold replayed as one):
+    a frame is one copy into the static input and one replay on the current stream; the returned tensors
+    are static and are overwritten by the next call.  Calibrate the model first (detect() would do it
+    inside the capture otherwise)."""
+
+    def __init__(self, model: MaskRCNN, image_shape, device, warmup: int = 3):
+        if not model._calibrated:
+            raise RuntimeError("calibrate the model before capturing it")
+        self.model = model
+        self.inp = torch.zeros(tuple(image_shape), dtype=torch.uint8, device=device)
+        side = torch.cuda.Stream(device)
+        side.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(side):
+            for _ in range(warmup):  # MIOpen's solver choice and the allocator's pools settle first
+                model.detect(self.inp, compact=False)
+        torch.cuda.current_stream(device).wait_stream(side)
+        torch.cuda.synchronize(device)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = model.detect(self.inp, compact=False)
+
+    def __call__(self, image_u8: torch.Tensor) -> dict:
+        self.inp.copy_(image_u8)
+        self.graph.replay()
+        return self.out

@@ -148,3 +148,26 @@ def test_detect_on_device_reference_configuration():
     want, want_kept = O.masks_to_labels(a["masks"].cpu().numpy())
     assert kept == want_kept
     np.testing.assert_array_equal(labels.cpu().numpy().reshape(480, 640), want)
+
+
+@pytest.mark.gpu
+def test_graph_detector_replays_the_detector():
+    """GraphDetector: detect(compact=False) captured once, replayed per frame (the bench's C5 producer)."""
+    from semtsdf.synth import SyntheticStream
+
+    dev = torch.device("cuda", 0)
+    st = SyntheticStream(seed=1, noise=True)
+    imgs = [torch.from_numpy(st.frame(k).rgb).to(dev) for k in range(3)]
+    cfg = MR.Config()
+    m = MR.MaskRCNN(cfg, seed=0).to(dev).to(cfg.DTYPE).eval()
+    m.calibrate(dev, imgs[0])
+    g = MR.GraphDetector(m, imgs[0].shape, dev)
+    for im in imgs:
+        out = g(im)
+        torch.cuda.synchronize()
+        z = out["class_ids"] == 0
+        assert tuple(out["masks"].shape) == (480, 640, cfg.DETECTION_MAX_INSTANCES)
+        assert int((~z).sum()) > 0 and int(out["masks"][:, :, z].sum()) == 0
+        assert (out["scores"][~z] >= cfg.DETECTION_MIN_CONFIDENCE).all()
+        r = out["rois"][~z].cpu().numpy()
+        assert ((r[:, 2] - r[:, 0]) * (r[:, 3] - r[:, 1]) > 0).all()
