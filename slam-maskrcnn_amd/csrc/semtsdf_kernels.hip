@@ -1512,7 +1512,7 @@ __device__ __forceinline__ bool tile_line_all(bool p) {
 #define SEMTSDF_NT_LOAD 0  // nt loads measured 3-5 % slower once the pipeline was chained (r03, same box)
 #endif
 #ifndef SEMTSDF_NT_STORE
-#define SEMTSDF_NT_STORE 1
+#define SEMTSDF_NT_STORE 0  // default-policy state stores: r06 A/B 73.7 -> 72.2 us (C3), 19.1 -> 18.9 us (C2) over six rounds (profiles/r06/ab/r06_store_policy.txt); nt until r05
 #endif
 #ifndef SEMTSDF_NT_HIST
 #define SEMTSDF_NT_HIST 0  // histogram lines are partial (one bin plane per lane): default policy
