@@ -497,8 +497,10 @@ class MaskRCNN(nn.Module):
         ys = torch.arange(H0, device=dev, dtype=torch.float32)
         xs = torch.arange(W0, device=dev, dtype=torch.float32)
         y1, x1, y2, x2 = (px[:, k].float()[:, None] for k in range(4))
-        gy = (2 * (ys[None] - y1) + 1) / (y2 - y1) - 1  # [N, H0]
-        gx = (2 * (xs[None] - x1) + 1) / (x2 - x1) - 1  # [N, W0]
+        # (the empty rows of the fixed-row form have zero extents: a unit divisor keeps their grid
+        # finite; `inside` below zeroes them)
+        gy = (2 * (ys[None] - y1) + 1) / (y2 - y1).clamp(min=1.0) - 1  # [N, H0]
+        gx = (2 * (xs[None] - x1) + 1) / (x2 - x1).clamp(min=1.0) - 1  # [N, W0]
         grid = torch.stack([gx[:, None, :].expand(-1, H0, -1), gy[:, :, None].expand(-1, -1, W0)], dim=-1)
         full = F.grid_sample(m[:, None], grid, mode="bilinear", padding_mode="zeros", align_corners=False)[:, 0]
         inside = ((ys[None] >= y1) & (ys[None] < y2))[:, :, None] & ((xs[None] >= x1) & (xs[None] < x2))[:, None, :]
