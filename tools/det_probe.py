@@ -13,14 +13,14 @@ from semtsdf import maskrcnn as MR  # noqa: E402
 from semtsdf.synth import SyntheticStream  # noqa: E402
 
 layout, bench = sys.argv[1], sys.argv[2]
-fp32 = len(sys.argv) > 3
+dt = sys.argv[3] if len(sys.argv) > 3 else "bf16"
+fp32 = dt == "fp32"
 torch.backends.cudnn.benchmark = bench == "bench1"
 dev = torch.device("cuda", 0)
 img = torch.from_numpy(SyntheticStream(seed=1, noise=True).frame(0).rgb).to(dev)
-cfg = MR.Config(DTYPE=torch.float32 if fp32 else torch.bfloat16)
+cfg = MR.Config(DTYPE={"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}[dt])
 m = MR.MaskRCNN(cfg, seed=0).to(dev).to(cfg.DTYPE).eval()
-if layout == "nchw":
-    MR.CHANNELS_LAST = False
+MR.CHANNELS_LAST = layout == "cl"
 t0 = time.perf_counter()
 m.detect(img, compact=False)
 torch.cuda.synchronize()
@@ -34,4 +34,4 @@ for _ in range(10):
     m.detect(img, compact=False)
 e1.record()
 e1.synchronize()
-print(f"{layout} {bench} {'fp32' if fp32 else 'bf16'}: first call {t1 - t0:.1f} s, {e0.elapsed_time(e1) / 10:.2f} ms per detect", flush=True)
+print(f"{layout} {bench} {dt}: first call {t1 - t0:.1f} s, {e0.elapsed_time(e1) / 10:.2f} ms per detect", flush=True)
