@@ -292,6 +292,13 @@ class MaskRCNN(nn.Module):
         # mask logits centred at +2 (most of a box above the 0.5 threshold), so that detections reach the
         # dmask.py area rule (> 2000 px) and the fusion sees instances
         self.mask_out.bias.add_(2.0)
+        # the refined boxes 3.5x the proposal's height and width (log-scale deltas over BBOX_STD_DEV): the
+        # random RPN favours the smallest anchors (20x20 px at 640x480, profiles/r06/det/areas_probe.txt),
+        # whose masks stay below the 2000-px rule and would leave the fusion without instances
+        gb = torch.zeros(cfg.NUM_CLASSES, 4, device=self.bbox_fc.bias.device, dtype=torch.float32)
+        gb[:, 2] = float(np.log(3.5)) / cfg.BBOX_STD_DEV[2]
+        gb[:, 3] = float(np.log(3.5)) / cfg.BBOX_STD_DEV[3]
+        self.bbox_fc.bias.add_(gb.view(-1).to(self.bbox_fc.bias.dtype))
 
     def _const(self, name, values, device):
         """Small constant tensors made once per device (no host-to-device copy inside a graph capture)."""

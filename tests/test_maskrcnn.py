@@ -151,14 +151,16 @@ def test_detect_on_device_reference_configuration():
 
 
 @pytest.mark.gpu
-def test_graph_detector_replays_the_detector():
-    """GraphDetector: detect(compact=False) captured once, replayed per frame (the bench's C5 producer)."""
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+def test_graph_detector_replays_the_detector(dtype):
+    """GraphDetector: detect(compact=False) captured once, replayed per frame (the bench's C5 producer
+    runs it in fp16)."""
     from semtsdf.synth import SyntheticStream
 
     dev = torch.device("cuda", 0)
     st = SyntheticStream(seed=1, noise=True)
     imgs = [torch.from_numpy(st.frame(k).rgb).to(dev) for k in range(3)]
-    cfg = MR.Config()
+    cfg = MR.Config(DTYPE={"bf16": torch.bfloat16, "fp16": torch.float16}[dtype])
     m = MR.MaskRCNN(cfg, seed=0).to(dev).to(cfg.DTYPE).eval()
     m.calibrate(dev, imgs[0])
     g = MR.GraphDetector(m, imgs[0].shape, dev)
