@@ -164,6 +164,7 @@ def test_graph_detector_replays_the_detector(dtype):
     m = MR.MaskRCNN(cfg, seed=0).to(dev).to(cfg.DTYPE).eval()
     m.calibrate(dev, imgs[0])
     g = MR.GraphDetector(m, imgs[0].shape, dev)
+    kept = 0
     for im in imgs:
         out = g(im)
         torch.cuda.synchronize()
@@ -173,3 +174,6 @@ def test_graph_detector_replays_the_detector(dtype):
         assert (out["scores"][~z] >= cfg.DETECTION_MIN_CONFIDENCE).all()
         r = out["rois"][~z].cpu().numpy()
         assert ((r[:, 2] - r[:, 0]) * (r[:, 3] - r[:, 1]) > 0).all()
+        # the calibrated producer hands the fusion instances: masks past dmask.py's 2000-px area rule
+        kept += O.masks_to_labels(out["masks"].cpu().numpy())[1]
+    assert kept > 0
