@@ -18,7 +18,7 @@
 extern "C" {
 #endif
 
-#define SEMTSDF_DET_ABI_VERSION 1
+#define SEMTSDF_DET_ABI_VERSION 2
 #define SEMTSDF_DET_ERR_INVALID 1
 #define SEMTSDF_DET_ERR_HIP 2
 #define SEMTSDF_DET_MAX_BOXES 16384
@@ -38,6 +38,16 @@ size_t semtsdf_det_nms_workspace(int n);
  *   work:   semtsdf_det_nms_workspace(n) bytes */
 int semtsdf_det_nms(const float* boxes, int n, float iou_threshold, int max_out, int32_t* keep, int32_t* count,
                     void* work, void* stream);
+
+/* PyramidROIAlign of mrcnn/model.py:374-452 (ABI 2): rois [n][4] f32 (y1, x1, y2, x2) normalised to the
+ * image, each sampled on its own level lvl[r] in 2..5 (the caller's level rule, model.py:406-413), at
+ * tf.image.crop_and_resize's pool x pool positions y = y1 (H - 1) + i (y2 - y1) (H - 1) / (pool - 1),
+ * bilinearly in f32, 0 outside the map (extrapolation value 0).
+ *   feats:  the four levels P2..P5, each [C][H[k]][W[k]] contiguous (batch 1, NCHW) in dtype
+ *   dtype:  0 fp16, 1 bf16 (the maps' and the output's element type)
+ *   out:    [n][C][pool][pool] in dtype */
+int semtsdf_det_roi_align(const void* const feats[4], const int H[4], const int W[4], int C, const float* rois,
+                          const int32_t* lvl, int n, int pool, int dtype, void* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -9,8 +9,11 @@
 // the block's diagonal words (a register per lane, broadcast by readlane: no memory round trip per box);
 // then the 256 threads OR the kept rows' words right of the block into the LDS removed-bitmap (every
 // load independent, one LDS atomic per word and wave).  Stops when max_out boxes are kept.
+#include <hip/hip_bf16.h>
+#include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "../../include/semtsdf_det.h"
@@ -122,6 +125,62 @@ __global__ __launch_bounds__(256) void k_nms_sweep(const unsigned long long* __r
     if (t == 0) *count = cnt;
 }
 
+
+// PyramidROIAlign (model.py:374-452) over the four pyramid levels P2..P5 [C][H][W] (NCHW, batch 1): the
+// output element (roi r, channel c, py, px) samples roi r's own level (lvl[r], 2..5) at the
+// crop_and_resize position y = y1 (H - 1) + py ((y2 - y1) (H - 1) / (pool - 1)) (same for x, the
+// same f32 operations as the PyTorch formulation), bilinearly in f32, 0 outside [0, H - 1] x [0, W - 1]
+// (extrapolation_value).  One thread per output element, px fastest (neighbouring threads read
+// neighbouring x of one channel row); only the roi's level is read, where a static-shape PyTorch
+// graph samples all four.
+struct Levels {
+    const void* f[4];
+    int H[4], W[4];
+};
+
+template <typename T>
+__device__ __forceinline__ float to_f(T v);
+template <>
+__device__ __forceinline__ float to_f<__half>(__half v) { return __half2float(v); }
+template <>
+__device__ __forceinline__ float to_f<__hip_bfloat16>(__hip_bfloat16 v) { return __bfloat162float(v); }
+template <typename T>
+__device__ __forceinline__ T from_f(float v);
+template <>
+__device__ __forceinline__ __half from_f<__half>(float v) { return __float2half(v); }
+template <>
+__device__ __forceinline__ __hip_bfloat16 from_f<__hip_bfloat16>(float v) { return __float2bfloat16(v); }
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_roi_align(Levels L, int C, const float* __restrict__ rois,
+                                                   const int32_t* __restrict__ lvl, int n, int pool,
+                                                   T* __restrict__ out) {
+    const long long total = (long long)n * C * pool * pool;
+    for (long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x; o < total;
+         o += (long long)gridDim.x * blockDim.x) {
+        const int px = (int)(o % pool), py = (int)((o / pool) % pool);
+        const long long rc = o / ((long long)pool * pool);
+        const int c = (int)(rc % C), r = (int)(rc / C);
+        const int l = min(max(lvl[r], 2), 5) - 2;
+        const int H = L.H[l], W = L.W[l];
+        const float y1 = rois[4 * r], x1 = rois[4 * r + 1], y2 = rois[4 * r + 2], x2 = rois[4 * r + 3];
+        const float hm = (float)(H - 1), wm = (float)(W - 1), pm = (float)(pool - 1);
+        const float y = y1 * hm + (float)py * (((y2 - y1) * hm) / pm);
+        const float x = x1 * wm + (float)px * (((x2 - x1) * wm) / pm);
+        float v = 0.0f;
+        if (y >= 0.0f && y <= hm && x >= 0.0f && x <= wm) {
+            const T* f = reinterpret_cast<const T*>(L.f[l]) + (size_t)c * H * W;
+            const int y0 = (int)floorf(y), x0 = (int)floorf(x);
+            const int yb = min(y0 + 1, H - 1), xb = min(x0 + 1, W - 1);
+            const float fy = y - (float)y0, fx = x - (float)x0;
+            const float v00 = to_f(f[(size_t)y0 * W + x0]), v01 = to_f(f[(size_t)y0 * W + xb]);
+            const float v10 = to_f(f[(size_t)yb * W + x0]), v11 = to_f(f[(size_t)yb * W + xb]);
+            const float top = v00 * (1.0f - fx) + v01 * fx, bot = v10 * (1.0f - fx) + v11 * fx;
+            v = top * (1.0f - fy) + bot * fy;
+        }
+        out[o] = from_f<T>(v);
+    }
+}
 }  // namespace semtsdf_det
 
 using namespace semtsdf_det;
@@ -150,6 +209,30 @@ int semtsdf_det_nms(const float* boxes, int n, float iou_threshold, int max_out,
     }
     hipLaunchKernelGGL(k_nms_sweep, dim3(1), dim3(256), 0, s, reinterpret_cast<const unsigned long long*>(work), n,
                        ncol, max_out, keep, count);
+    return hipGetLastError() == hipSuccess ? 0 : SEMTSDF_DET_ERR_HIP;
+}
+
+int semtsdf_det_roi_align(const void* const feats[4], const int H[4], const int W[4], int C, const float* rois,
+                          const int32_t* lvl, int n, int pool, int dtype, void* out, void* stream) {
+    if (!feats || !H || !W || C <= 0 || n < 0 || pool < 2 || (dtype != 0 && dtype != 1) || (n > 0 && (!rois || !lvl || !out)))
+        return SEMTSDF_DET_ERR_INVALID;
+    Levels L;
+    for (int k = 0; k < 4; ++k) {
+        if (!feats[k] || H[k] < 2 || W[k] < 2) return SEMTSDF_DET_ERR_INVALID;
+        L.f[k] = feats[k];
+        L.H[k] = H[k];
+        L.W[k] = W[k];
+    }
+    if (n == 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    const long long total = (long long)n * C * pool * pool;
+    const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 8192);
+    if (dtype == 0)
+        hipLaunchKernelGGL(k_roi_align<__half>, dim3(grid), dim3(256), 0, s, L, C, rois, lvl, n, pool,
+                           reinterpret_cast<__half*>(out));
+    else
+        hipLaunchKernelGGL(k_roi_align<__hip_bfloat16>, dim3(grid), dim3(256), 0, s, L, C, rois, lvl, n, pool,
+                           reinterpret_cast<__hip_bfloat16*>(out));
     return hipGetLastError() == hipSuccess ? 0 : SEMTSDF_DET_ERR_HIP;
 }
 

@@ -44,6 +44,7 @@ DET_LIB = os.path.join(_ROOT, "libsemtsdf_det.so")
 # NCHW activations: MIOpen's immediate mode runs them at 10.8 ms per 1024x1024 frame against 28.7 ms for
 # NHWC (8.9 ms only after a 30-s per-shape find with torch.backends.cudnn.benchmark; tools/det_probe.py)
 CHANNELS_LAST = False
+ROI_ALIGN_HIP = True  # the device ROI align (libsemtsdf_det.so); False: the PyTorch grid_sample formulation
 
 
 @dataclass
@@ -88,6 +89,10 @@ def _det_lib():
         lib.semtsdf_det_nms.restype = C.c_int
         lib.semtsdf_det_nms.argtypes = [C.c_void_p, C.c_int, C.c_float, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                                         C.c_void_p]
+        lib.semtsdf_det_roi_align.restype = C.c_int
+        lib.semtsdf_det_roi_align.argtypes = [C.POINTER(C.c_void_p), C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int,
+                                              C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                              C.c_void_p]
         _det = lib
     return _det
 
@@ -110,6 +115,27 @@ def nms_sorted(boxes: torch.Tensor, iou_threshold: float, max_out: int) -> tuple
     if rc:
         raise RuntimeError(f"semtsdf_det_nms failed ({rc})")
     return keep[:max_out], count
+
+
+def roi_align_dev(rois: torch.Tensor, lvl: torch.Tensor, feats, pool: int) -> torch.Tensor:
+    """PyramidROIAlign on the device (the HIP kernel of libsemtsdf_det.so): rois [n, 4] normalised, lvl
+    [n] in 2..5, feats the four levels [1, C, H, W] in fp16 or bf16 -> [n, C, pool, pool] in their dtype,
+    asynchronous on the current stream.  Each roi reads only its own level."""
+    lib = _det_lib()
+    fs = [f.contiguous() for f in feats]
+    dt = {torch.float16: 0, torch.bfloat16: 1}[fs[0].dtype]
+    n, Cn = int(rois.shape[0]), int(fs[0].shape[1])
+    out = torch.empty((n, Cn, pool, pool), dtype=fs[0].dtype, device=rois.device)
+    r = rois.to(torch.float32).contiguous()
+    lv = lvl.to(torch.int32).contiguous()
+    ptrs = (C.c_void_p * 4)(*[f.data_ptr() for f in fs])
+    H = (C.c_int * 4)(*[int(f.shape[2]) for f in fs])
+    W = (C.c_int * 4)(*[int(f.shape[3]) for f in fs])
+    rc = lib.semtsdf_det_roi_align(ptrs, H, W, Cn, C.c_void_p(r.data_ptr()), C.c_void_p(lv.data_ptr()), n, int(pool),
+                                   dt, C.c_void_p(out.data_ptr()), C.c_void_p(torch.cuda.current_stream(rois.device).cuda_stream))
+    if rc:
+        raise RuntimeError(f"semtsdf_det_roi_align failed ({rc})")
+    return out
 
 
 # ---------------------------------------------------------------------------------- anchors
@@ -367,6 +393,8 @@ class MaskRCNN(nn.Module):
         lvl = torch.log2(torch.sqrt(h * w) / (224.0 / math.sqrt(area)))
         lvl = torch.clamp(4 + torch.round(lvl), 2, 5)  # empty (zero) rois: log2(0) = -inf -> level 2
         lvl = torch.where(torch.isnan(lvl), torch.full_like(lvl, 2.0), lvl).long()
+        if rois.device.type == "cuda" and feats[0].dtype in (torch.float16, torch.bfloat16) and ROI_ALIGN_HIP:
+            return roi_align_dev(rois, lvl, feats, pool)
         n, Cn = rois.shape[0], feats[0].shape[1]
         out = torch.zeros((n, Cn, pool, pool), dtype=feats[0].dtype, device=rois.device)
         i = torch.arange(pool, device=rois.device, dtype=torch.float32)

@@ -107,11 +107,11 @@ def test_detector_library_exports_every_symbol():
     with open(os.path.join(ROOT, "include", "semtsdf_det.h")) as f:
         txt = re.sub(r"/\*.*?\*/", "", f.read(), flags=re.S)
     names = sorted(set(re.findall(r"\b(semtsdf_det_[a-z0-9_]+)\s*\(", txt)))
-    assert names == ["semtsdf_det_abi_version", "semtsdf_det_nms", "semtsdf_det_nms_workspace"]
+    assert names == ["semtsdf_det_abi_version", "semtsdf_det_nms", "semtsdf_det_nms_workspace", "semtsdf_det_roi_align"]
     lib = C.CDLL(os.path.join(ROOT, "slam-maskrcnn_amd", "semtsdf", "libsemtsdf_det.so"))
     for n in names:
         assert hasattr(lib, n), n
-    assert lib.semtsdf_det_abi_version() == 1
+    assert lib.semtsdf_det_abi_version() == 2
     lib.semtsdf_det_nms_workspace.restype = C.c_size_t
     assert lib.semtsdf_det_nms_workspace(6000) == 6000 * 94 * 8
     lib.semtsdf_det_nms.argtypes = [C.c_void_p, C.c_int, C.c_float, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,

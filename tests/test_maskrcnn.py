@@ -118,6 +118,39 @@ def test_hip_nms_equals_reference_rule():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["fp16", "bf16"])
+def test_hip_roi_align_equals_the_pytorch_formulation(dtype):
+    """semtsdf_det_roi_align (each roi on its own level) against the static-shape PyTorch formulation
+    (grid_sample of every roi on every level, the roi's level kept), both from the same f32 sample
+    positions; rois inside, straddling and outside the image, zero rois, all four levels."""
+    dev = torch.device("cuda", 0)
+    dt = {"fp16": torch.float16, "bf16": torch.bfloat16}[dtype]
+    g = torch.Generator(device="cpu").manual_seed(5)
+    feats = [torch.randn((1, 32, s, s), generator=g).to(dev, dt) for s in (256, 128, 64, 32)]
+    n = 300
+    c = torch.rand((n, 2), generator=g) * 1.2 - 0.1
+    hw = torch.rand((n, 2), generator=g) ** 3 * 0.8
+    rois = torch.cat([c - hw / 2, c + hw / 2], 1)[:, [0, 1, 2, 3]].to(dev)
+    rois[:10] = 0.0  # zero rois (the fixed-row form's padding)
+    m = MR.MaskRCNN(MR.Config(DTYPE=dt, BACKBONE="resnet50"), seed=0)
+    for pool in (7, 14):
+        MR.ROI_ALIGN_HIP = True
+        a = m.roi_align(rois, feats, pool, (1024, 1024)).float()
+        MR.ROI_ALIGN_HIP = False
+        try:
+            b = m.roi_align(rois, feats, pool, (1024, 1024)).float()
+        finally:
+            MR.ROI_ALIGN_HIP = True
+        torch.cuda.synchronize()
+        assert a.shape == b.shape == (n, 32, pool, pool)
+        # the same f32 bilinear value up to grid_sample's normalise/unnormalise round trip, then one
+        # rounding to the maps' type
+        tol = 4e-3 if dtype == "fp16" else 3e-2
+        assert float((a - b).abs().max()) <= tol * max(1.0, float(b.abs().max())), pool
+        assert float(a[:10].abs().max()) == float(b[:10].abs().max())
+
+
+@pytest.mark.gpu
 def test_detect_on_device_reference_configuration():
     from semtsdf.masks import masks_to_labels_dev
     from semtsdf.synth import SyntheticStream
