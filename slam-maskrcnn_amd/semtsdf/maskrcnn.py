@@ -2,9 +2,10 @@
 
 The reference's detector is matterport's Keras/TensorFlow Mask R-CNN (Mask_RCNN/mrcnn/model.py) run
 with COCO weights by Mask_RCNN/dmask.py and mask_process.py.  This module restates its inference graph
-(`MaskRCNN.build`, mode "inference", model.py:1833-2053) layer for layer in PyTorch, bf16 convolutions
-on MIOpen for the backbone and heads, f32 box arithmetic, and the greedy NMS as HIP
-kernels (libsemtsdf_det.so, include/semtsdf_det.h); `detect` returns what model.py:2436-2492 returns
+(`MaskRCNN.build`, mode "inference", model.py:1833-2053) layer for layer in PyTorch, fp16 or bf16
+convolutions on MIOpen for the backbone and heads (`Config.DTYPE`; the bench's producer runs fp16), f32
+box arithmetic, and the greedy NMS and the PyramidROIAlign as HIP kernels (libsemtsdf_det.so,
+include/semtsdf_det.h); `detect` returns what model.py:2436-2492 returns
 (rois, class_ids, scores, masks[H, W, N]), on the device, and feeds semtsdf_masks_to_labels (the
 dmask.py rule) without leaving HBM.
 
